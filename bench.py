@@ -1,0 +1,176 @@
+#!/usr/bin/env python3
+"""Headline benchmark: candidate route evaluations per second.
+
+Workload (BASELINE.json configs[1]): CVRP, 100 customers, 8 vehicles,
+uniform capacity, random Euclidean integer durations, on one MI355X.  One
+"step" is one pass of the scoring hot path (``vrpms_eval``) over a batch of
+C candidate giant tours (uint8, 100 B each) that is already resident in HBM
+and larger than the 256 MiB Infinity Cache, so every step streams it from
+HBM.  Multi-GPU: every rank scores its own batch (independent islands, no
+collective in the data path) -> weak scaling; the driver launches one
+process per GPU via torch.distributed.run.
+
+Reported beside the value:
+  roofline      the dominant kernel (eval_cvrp_packed) timed with HIP events
+                on the stream it runs on; achieved = algorithmic HBM bytes per
+                launch (C x (100 B tour + 8 B key)) / mean launch time.
+  cpu_baseline  the C restatement of the spec (oracle/oracle_c.c, OpenMP)
+                on a bounded sample of the same workload, rank 0 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "candidate route evals/sec (1/2/4/8 GPU) + best-cost gap at fixed wall time"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--candidates", type=int, default=16 * 1024 * 1024)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="target CPU work for the cpu_baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def make_batch(torch, C, n, dev, seed):
+    """C random permutations of 1..n as uint8 rows, generated on the device
+    in chunks (argsort of uniform keys)."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    out = torch.empty((C, n), dtype=torch.uint8, device=dev)
+    chunk = 1 << 20
+    for s in range(0, C, chunk):
+        e = min(C, s + chunk)
+        r = torch.rand((e - s, n), generator=g, device=dev)
+        out[s:e] = (r.argsort(dim=1) + 1).to(torch.uint8)
+    return out
+
+
+def cpu_baseline(inst, perms_dev, seconds):
+    """Time the C oracle (OpenMP, all threads it is given) on a bounded
+    sample of the same tours; returns the cpu_baseline object."""
+    import numpy as np
+    from oracle import coracle
+    coracle.build()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or coracle.max_threads()
+    probe = perms_dev[:20000].cpu().numpy()
+    t0 = time.perf_counter()
+    coracle.eval_batch(inst.durations, probe, inst.demand, inst.capacities, inst.start_times,
+                       1, 0, threads=threads)
+    rate = probe.shape[0] / max(time.perf_counter() - t0, 1e-9)
+    S = int(min(perms_dev.shape[0], max(20000, rate * seconds)))
+    sample = perms_dev[:S].cpu().numpy()
+    t0 = time.perf_counter()
+    ref = coracle.eval_batch(inst.durations, sample, inst.demand, inst.capacities,
+                             inst.start_times, 1, 0, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": S / dt, "unit": "evals/s", "cores": threads, "kind": "port",
+            "sample": f"first {S} of the same CVRP-100 tours, C restatement oracle/oracle_c.c "
+                      f"(OpenMP, {threads} threads), {dt:.2f} s"}, ref, S
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from vrpms_amd import synth
+    from vrpms_amd.core import CVRP, Context
+    inst = synth.cvrp(100, 8, seed=args.seed)
+    ctx = Context(local)
+    ctx.set_instance(CVRP, inst.durations, inst.demand, inst.capacities, inst.start_times)
+    C, n = args.candidates, inst.n
+    perms = make_batch(torch, C, n, dev, args.seed * 1000 + rank)
+    keys = torch.empty(C, dtype=torch.int64, device=dev)
+    path = ctx.eval_path(perms)
+    assert path == 0, f"expected the packed-LDS kernel, got path {path}"
+
+    for _ in range(args.warmup):
+        ctx.eval(perms, out=keys)
+    stream = torch.cuda.current_stream(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        ctx.eval(perms, out=keys)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    total_evals = C * args.steps * world
+    value = total_evals / wall
+
+    out = None
+    if rank == 0:
+        bytes_per_launch = C * (n + 8)
+        achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": wall * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (seeded CVRP-100 instance, device-generated random giant tours)",
+            "config": {"workload": "cvrp100_k8_full_tour_eval", "customers": n, "vehicles": 8,
+                       "candidates_per_step": C, "tour_dtype": "u8", "per_rank_batch": C,
+                       "parallelism": f"islands{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "eval_cvrp_packed", "kernel_ms": kernel_ms,
+                         "bytes_per_launch": bytes_per_launch,
+                         "gathers_per_s": C * (n + 1) / (kernel_ms * 1e-3)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            cb, ref, S = cpu_baseline(inst, perms, args.cpu_seconds)
+            import numpy as np
+            got = keys[:S].cpu().numpy().view(np.uint64)
+            cb["parity_on_sample"] = bool((got == ref[0]).all())
+            out["cpu_baseline"] = cb
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

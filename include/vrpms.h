@@ -1,0 +1,107 @@
+/* vrpms.h -- C ABI of the MI355X (gfx950) vrpms solver core.
+ *
+ * The reference (metehkaya/vrpms) has no native code and no FFI: its solver
+ * slot is the `# TODO: Run algorithm` block of each HTTP handler and the stub
+ * `src/solver.py`.  This header is the boundary the Python front-end
+ * (`vrpms_amd/solver.py`, which keeps the `src/solver.py` entry points and the
+ * handler result dicts) binds through ctypes.  Each entry point names the
+ * reference line whose behaviour it supplies.
+ *
+ * Conventions
+ *   - Every function returns 0 (VRPMS_OK) or a negative VRPMS_E* code; the
+ *     message is in vrpms_last_error() (thread-local).  No C++ exception ever
+ *     crosses this boundary.
+ *   - All `d_*` pointers are DEVICE pointers owned by the caller (PyTorch-ROCm
+ *     tensors in the Python front-end); the library never frees them.  The
+ *     context owns its own scratch and derived matrix layouts.
+ *   - `stream` is a hipStream_t (NULL = default stream).  Every call after
+ *     vrpms_set_instance is asynchronous on that stream; nothing synchronises
+ *     except vrpms_set_instance (validation readback) and vrpms_ctx_destroy.
+ *   - Nodes are compact indices: node 0 is the depot (VRP, A1) or the
+ *     startNode (TSP, A4); customers are 1..N-1.  Tours are "giant tours":
+ *     a permutation of customers without the depot, stored as uint8 (N<=256)
+ *     or uint16 rows of `ld` elements.
+ *   - Semantics are SURVEY.md Appendix A (frozen in oracle/spec.py).
+ */
+#ifndef VRPMS_H
+#define VRPMS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VRPMS_OK 0
+#define VRPMS_EINVAL (-1)   /* bad argument / shape */
+#define VRPMS_EHIP (-2)     /* HIP runtime error */
+#define VRPMS_ERANGE (-3)   /* A9 overflow guard: clock could exceed int32 */
+#define VRPMS_ESTATE (-4)   /* no instance loaded */
+#define VRPMS_ENOMEM (-5)
+
+#define VRPMS_TSP 0
+#define VRPMS_CVRP 1
+
+#define VRPMS_OBJ_SUM 0 /* primary durationSum, secondary durationMax */
+#define VRPMS_OBJ_MAX 1 /* primary durationMax, secondary durationSum */
+
+typedef struct vrpms_ctx vrpms_ctx;
+
+/* Library version, (major << 16) | minor. */
+int vrpms_version(void);
+
+/* Thread-local message for the last failing call on this thread. */
+const char* vrpms_last_error(void);
+
+/* Create / destroy a solver context bound to HIP device `device`. */
+int vrpms_ctx_create(int device, vrpms_ctx** out);
+int vrpms_ctx_destroy(vrpms_ctx* ctx);
+
+/* Load an instance (replaces the DB fetch result consumed at
+ * api/vrp/ga/index.py:41-42 / api/tsp/ga/index.py:33-34).
+ *   problem  VRPMS_TSP or VRPMS_CVRP
+ *   d_dur    int32 [H][N][N] durations in minutes (A2/A3), H = 1 or 24
+ *   d_demand int32 [N] (demand[0] ignored); NULL for TSP
+ *   d_cap    int32 [K] vehicle capacities (api/parameters.py:11); NULL for TSP
+ *   d_start  int32 [K] start minutes (api/parameters.py:12; TSP: K = 1 and
+ *            d_start[0] = startTime, api/parameters.py:43)
+ * Validates non-negativity and the A9 int32 guard (synchronises once).
+ * Chooses the on-chip tier (LDS-resident / L2-resident) and builds the
+ * packed device layouts used by the kernels. */
+int vrpms_set_instance(vrpms_ctx* ctx, int32_t problem, const int32_t* d_dur, int32_t H,
+                       int32_t N, const int32_t* d_demand, const int32_t* d_cap,
+                       const int32_t* d_start, int32_t K, int32_t objective, void* stream);
+
+/* Batched full evaluation of C candidate giant tours (the scoring half of
+ * the hot path; the reference's would-be cost function behind
+ * api/{tsp,vrp}/<algo>/index.py's TODO slot).
+ *   d_perms   [C][ld] uint8 (perm_bytes=1) or uint16 (perm_bytes=2), n used
+ *   d_keys    [C] A8 objective keys (required)
+ *   d_sum     [C] durationSum (TSP: duration)  -- nullable
+ *   d_max     [C] durationMax (TSP: duration)  -- nullable
+ *   d_unv     [C] unvisited customer count     -- nullable */
+int vrpms_eval(vrpms_ctx* ctx, const void* d_perms, int32_t perm_bytes, int64_t C, int32_t n,
+               int64_t ld, uint64_t* d_keys, int32_t* d_sum, int32_t* d_max, int32_t* d_unv,
+               void* stream);
+
+/* Which scoring kernel vrpms_eval picks for these tour buffers:
+ * 0 = eval_cvrp_packed (LDS packed matrix + LDS-staged tiles),
+ * 1 = eval_tsp_staged, 2 = eval_generic; -1 = no instance. */
+int vrpms_eval_path(vrpms_ctx* ctx, int32_t perm_bytes, int64_t ld, const void* d_perms);
+
+/* Decode ONE giant tour into the result dict of api/vrp/ga/index.py:49-53
+ * (A6/A7): d_vehicle_of[i] = vehicle serving perm position i, or -1 when
+ * unvisited; d_route_dur[k] = duration of vehicle k (0 if unused). */
+int vrpms_decode(vrpms_ctx* ctx, const void* d_perm, int32_t perm_bytes, int32_t n,
+                 int32_t* d_vehicle_of, int32_t* d_route_dur, void* stream);
+
+/* Argmin over C keys: d_out[0] = min key, d_out[1] = smallest index holding
+ * it.  Wave64 shuffle reduction + one 64-bit atomicMin pass. */
+int vrpms_argmin(vrpms_ctx* ctx, const uint64_t* d_keys, int64_t C, uint64_t* d_out,
+                 void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VRPMS_H */

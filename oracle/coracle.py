@@ -1,0 +1,69 @@
+"""ctypes wrapper of liboracle.so (the C restatement) -- TEST INFRASTRUCTURE."""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    src = os.path.join(HERE, "oracle_c.c")
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-B" if force else "-s", "-C", HERE], check=True)
+    return LIB
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        lib = ctypes.CDLL(LIB)
+        vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+        lib.oracle_eval_batch.restype = ctypes.c_int
+        lib.oracle_eval_batch.argtypes = [i32, vp, i32, i32, vp, vp, vp, i32, i32, vp, vp, i64,
+                                          i32, i64, vp, vp, vp, vp, i32]
+        lib.oracle_max_threads.restype = ctypes.c_int
+        _lib = lib
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def eval_batch(durations, perms, demand=None, capacities=None, start_times=(0,),
+               problem: int = 1, objective: int = 0, n: int | None = None, threads: int = 0):
+    """Returns (keys u64, sums, maxs, unv) numpy arrays."""
+    lib = load()
+    D = np.asarray(durations, dtype=np.int32)
+    if D.ndim == 2:
+        D = D[None]
+    D = np.ascontiguousarray(D)
+    H, N = D.shape[0], D.shape[1]
+    perms = np.ascontiguousarray(perms)
+    C, ld = perms.shape
+    n = ld if n is None else n
+    st = np.ascontiguousarray(np.asarray(start_times, dtype=np.int32).reshape(-1))
+    K = st.shape[0]
+    dem = None if demand is None else np.ascontiguousarray(np.asarray(demand, dtype=np.int32))
+    cap = None if capacities is None else np.ascontiguousarray(np.asarray(capacities, dtype=np.int32))
+    p8 = perms if perms.dtype == np.uint8 else None
+    p16 = perms.astype(np.uint16, copy=False) if p8 is None else None
+    keys = np.empty(C, dtype=np.uint64)
+    sums = np.empty(C, dtype=np.int32)
+    maxs = np.empty(C, dtype=np.int32)
+    unv = np.empty(C, dtype=np.int32)
+    lib.oracle_eval_batch(problem, _p(D), H, N, _p(dem), _p(cap), _p(st), K, objective, _p(p8),
+                          _p(p16), C, n, ld, _p(keys), _p(sums), _p(maxs), _p(unv), threads)
+    return keys, sums, maxs, unv
+
+
+def max_threads() -> int:
+    return load().oracle_max_threads()

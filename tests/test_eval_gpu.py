@@ -1,0 +1,180 @@
+"""GPU parity of batched scoring (vrpms_eval) against the spec oracle.
+
+Bar: bit-exact keys, durationSum, durationMax and unvisited counts on the
+same tours, for every kernel path (packed-LDS CVRP, staged TSP, generic
+LDS/L2 tiers, H = 24 time-dependent) and the edge cases the spec defines.
+"""
+import numpy as np
+import pytest
+
+from oracle import spec
+from vrpms_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def upload(ctx, P):
+    torch = _torch()
+    t = torch.from_numpy(P.view(np.int16) if P.dtype == np.uint16 else P)
+    return t.to(ctx.dev)
+
+
+def load(ctx, inst, objective=0):
+    from vrpms_amd.core import CVRP, TSP
+    if inst.problem == "tsp":
+        ctx.set_instance(TSP, inst.durations, start_times=inst.start_times, objective=objective)
+    else:
+        ctx.set_instance(CVRP, inst.durations, inst.demand, inst.capacities, inst.start_times,
+                         objective=objective)
+
+
+def check_batch(ctx, coracle, inst, P, n=None, objective=0, expect_path=None):
+    load(ctx, inst, objective)
+    dP = upload(ctx, P)
+    if expect_path is not None:
+        assert ctx.eval_path(dP) == expect_path
+    keys, sums, maxs, unv = ctx.eval(dP, n=n, with_parts=True)
+    ref = coracle.eval_batch(inst.durations, P, inst.demand, inst.capacities, inst.start_times,
+                             problem=0 if inst.problem == "tsp" else 1, objective=objective, n=n)
+    got_k = keys.cpu().numpy().view(np.uint64)
+    np.testing.assert_array_equal(got_k, ref[0])
+    np.testing.assert_array_equal(sums.cpu().numpy(), ref[1])
+    np.testing.assert_array_equal(maxs.cpu().numpy(), ref[2])
+    np.testing.assert_array_equal(unv.cpu().numpy(), ref[3])
+    # and a few rows straight against the pure-Python spec
+    for i in range(0, P.shape[0], max(1, P.shape[0] // 7)):
+        row = P[i, : (P.shape[1] if n is None else n)]
+        if inst.problem == "tsp":
+            assert got_k[i] == spec.tsp_key(spec.eval_tsp(inst.durations, row,
+                                                          int(inst.start_times[0])))
+        else:
+            r = spec.eval_cvrp(inst.durations, row, inst.demand, inst.capacities,
+                               inst.start_times, objective)
+            assert got_k[i] == r["key"]
+    return got_k
+
+
+@pytest.mark.parametrize("objective", [0, 1])
+def test_cvrp100_packed_path(ctx, coracle, objective):
+    inst = synth.cvrp(100, 8, seed=0)
+    P = synth.random_perms(20000 + 37, inst.n, seed=1)          # ragged last tile
+    check_batch(ctx, coracle, inst, P, objective=objective, expect_path=0)
+
+
+def test_cvrp_tight_capacity_unvisited(ctx, coracle):
+    inst = synth.cvrp(100, 8, seed=2, slack=0.85)
+    P = synth.random_perms(5000, inst.n, seed=3)
+    k = check_batch(ctx, coracle, inst, P, expect_path=0)
+    assert (k >> np.uint64(56)).max() > 0
+
+
+def test_cvrp_heterogeneous_fleet_and_oversized_demand(ctx, coracle):
+    inst = synth.cvrp(60, 6, seed=4)
+    inst.capacities = np.array([40, 5, 90, 30, 7, 60])
+    inst.demand[5] = 80                        # only vehicle 2 can ever carry it
+    inst.start_times = np.array([0, 5, 10, 0, 3, 9])
+    P = synth.random_perms(4096, inst.n, seed=5)
+    check_batch(ctx, coracle, inst, P, expect_path=0)
+
+
+def test_cvrp_generic_path_unaligned_ld(ctx, coracle):
+    inst = synth.cvrp(50, 5, seed=6)
+    P = synth.random_perms(3000, inst.n, seed=7, ld=inst.n + 1)    # ld % 4 != 0
+    check_batch(ctx, coracle, inst, P, n=inst.n, expect_path=2)
+
+
+def test_cvrp_uint16_tours(ctx, coracle):
+    inst = synth.cvrp(100, 8, seed=8)
+    P = synth.random_perms(3000, inst.n, seed=9, dtype=np.uint16)
+    check_batch(ctx, coracle, inst, P, expect_path=2)
+
+
+def test_tdvrp200_l2_tier(ctx, coracle):
+    inst = synth.td_cvrp(200, 16, seed=0)
+    P = synth.random_perms(8192, inst.n, seed=2)
+    check_batch(ctx, coracle, inst, P, expect_path=2)
+
+
+def test_tdvrp_small_lds_tier(ctx, coracle):
+    inst = synth.td_cvrp(20, 3, seed=3)       # 24 x 21 x 21 x 2 B fits the LDS tier
+    P = synth.random_perms(4000, inst.n, seed=4)
+    check_batch(ctx, coracle, inst, P, expect_path=2)
+
+
+def test_x1000_l2_tier(ctx, coracle):
+    inst = synth.x_style(1000, seed=0)
+    P = synth.random_perms(2048, inst.n, seed=1, dtype=np.uint16)
+    check_batch(ctx, coracle, inst, P, expect_path=2)
+
+
+@pytest.mark.parametrize("maker", [synth.tsp20, synth.tsp50])
+def test_tsp_staged_path(ctx, coracle, maker):
+    inst = maker(3)
+    ld = (inst.n + 3) // 4 * 4
+    P = synth.random_perms(10000 + 5, inst.n, seed=5, ld=ld)
+    check_batch(ctx, coracle, inst, P, n=inst.n, expect_path=1)
+
+
+def test_tsp_time_dependent(ctx, coracle):
+    base = synth.td_cvrp(30, 2, seed=1)
+    inst = synth.Instance("tdtsp", base.durations, None, None, np.array([415]), "tsp")
+    P = synth.random_perms(3000, inst.n, seed=6)
+    check_batch(ctx, coracle, inst, P, expect_path=2)
+
+
+def test_large_matrix_int32_values(ctx, coracle):
+    rng = np.random.default_rng(0)
+    N = 40
+    D = rng.integers(60000, 900000, size=(N, N))         # > 65535: int32 matrix path
+    np.fill_diagonal(D, 0)
+    inst = synth.Instance("big", D[None], np.concatenate([[0], rng.integers(1, 9, N - 1)]),
+                          np.array([60, 60, 60, 60]), np.zeros(4, dtype=np.int64), "cvrp")
+    P = synth.random_perms(2000, inst.n, seed=1)
+    check_batch(ctx, coracle, inst, P)
+
+
+def test_empty_batch_and_zero_length_tours(ctx, coracle):
+    torch = _torch()
+    inst = synth.cvrp(10, 2, seed=1)
+    load(ctx, inst)
+    empty = torch.zeros((0, 12), dtype=torch.uint8, device=ctx.dev)
+    assert ctx.eval(empty).numel() == 0
+    P = np.zeros((5, 4), dtype=np.uint8)
+    k = ctx.eval(upload(ctx, P), n=0).cpu().numpy().view(np.uint64)
+    assert (k == 0).all()
+
+
+def test_decode_matches_spec_routes(ctx):
+    for inst in (synth.cvrp(100, 8, seed=3, slack=0.9), synth.td_cvrp(40, 4, seed=2)):
+        load(ctx, inst)
+        P = synth.random_perms(4, inst.n, seed=11)
+        for row in P:
+            veh, dur = ctx.decode(upload(ctx, row[None]))
+            r = spec.eval_cvrp(inst.durations, row, inst.demand, inst.capacities,
+                               inst.start_times)
+            assert veh == r["vehicle_of"]
+            assert dur == r["durations"]
+
+
+def test_argmin(ctx):
+    torch = _torch()
+    rng = np.random.default_rng(0)
+    keys = rng.integers(0, 2**62, size=100003, dtype=np.int64)
+    keys[[777, 5000, 99999]] = 3
+    best, idx = ctx.argmin(torch.from_numpy(keys).to(ctx.dev))
+    assert (best, idx) == (3, 777)
+
+
+def test_errors_are_raised(ctx):
+    from vrpms_amd.core import CVRP, VrpmsError
+    D = np.ones((5, 5), dtype=np.int64)
+    D[1, 2] = -1
+    with pytest.raises(VrpmsError, match="negative duration"):
+        ctx.set_instance(CVRP, D, [0, 1, 1, 1, 1], [3], [0])
+    with pytest.raises(VrpmsError, match="A9"):
+        ctx.set_instance(CVRP, np.full((5, 5), 2**29), [0, 1, 1, 1, 1], [3], [0])

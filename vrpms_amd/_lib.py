@@ -1,0 +1,85 @@
+"""ctypes binding of ``include/vrpms.h`` (the C-ABI of libvrpms.so).
+
+There is deliberately no CPU fallback: if the HIP library is missing or no
+GPU is visible, every compute entry point raises.  ``torch`` is imported
+before the library is opened so that libvrpms's ``NEEDED libamdhip64.so.7``
+binds to the HIP runtime torch already loaded (same SONAME), giving one HIP
+runtime per process and letting torch streams/tensors cross the boundary.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libvrpms.so")
+
+VRPMS_OK = 0
+VRPMS_EINVAL = -1
+VRPMS_EHIP = -2
+VRPMS_ERANGE = -3
+VRPMS_ESTATE = -4
+VRPMS_ENOMEM = -5
+
+TSP = 0
+CVRP = 1
+OBJ_SUM = 0
+OBJ_MAX = 1
+
+_c = ctypes
+_vp = _c.c_void_p
+_i32 = _c.c_int32
+_i64 = _c.c_int64
+_u64 = _c.c_uint64
+
+# name -> (restype, argtypes); mirrors include/vrpms.h one-for-one.
+SIGNATURES = {
+    "vrpms_version": (_c.c_int, []),
+    "vrpms_last_error": (_c.c_char_p, []),
+    "vrpms_ctx_create": (_c.c_int, [_c.c_int, _c.POINTER(_vp)]),
+    "vrpms_ctx_destroy": (_c.c_int, [_vp]),
+    "vrpms_set_instance": (_c.c_int, [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _i32, _i32, _vp]),
+    "vrpms_eval": (_c.c_int, [_vp, _vp, _i32, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "vrpms_eval_path": (_c.c_int, [_vp, _i32, _i64, _vp]),
+    "vrpms_decode": (_c.c_int, [_vp, _vp, _i32, _i32, _vp, _vp, _vp]),
+    "vrpms_argmin": (_c.c_int, [_vp, _vp, _i64, _vp, _vp]),
+}
+
+
+class VrpmsError(RuntimeError):
+    """A libvrpms call returned a negative status."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(f"[vrpms {code}] {message}")
+        self.code = code
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Open libvrpms.so (once) and declare every symbol of include/vrpms.h."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        import torch  # noqa: F401  -- binds libamdhip64.so.7 before our NEEDED entry
+        if not os.path.exists(path):
+            raise ImportError(
+                f"libvrpms.so not found at {path}; build it with "
+                "`python -m vrpms_amd.build` (hipcc --offload-arch=gfx950)")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def check(code: int) -> None:
+    if code != VRPMS_OK:
+        msg = _lib.vrpms_last_error()
+        raise VrpmsError(code, msg.decode() if msg else "unknown error")

@@ -1,0 +1,165 @@
+"""Device context: owns one ``vrpms_ctx`` and moves instances/tours through the
+C-ABI.  PyTorch-ROCm tensors are used only as device-buffer owners and for
+the current HIP stream; all arithmetic happens in libvrpms's kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import CVRP, OBJ_MAX, OBJ_SUM, TSP, VrpmsError, check  # noqa: F401
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def require_gpu():
+    torch = _torch()
+    if not torch.cuda.is_available():
+        raise RuntimeError("vrpms_amd needs a ROCm GPU: torch.cuda.is_available() is False "
+                           "(there is no CPU fallback by design)")
+    return torch
+
+
+def perm_dtype_bytes(t) -> int:
+    torch = _torch()
+    if t.dtype == torch.uint8:
+        return 1
+    if t.dtype in (torch.int16, getattr(torch, "uint16", torch.int16)):
+        return 2
+    raise TypeError(f"tours must be uint8 or (u)int16, got {t.dtype}")
+
+
+def tour_dtype(N: int):
+    """Narrowest tour element for an N-node instance (uint8 for N <= 256)."""
+    torch = _torch()
+    return torch.uint8 if N <= 256 else torch.int16
+
+
+class Context:
+    """One solver context on one GPU (``vrpms_ctx_create``)."""
+
+    def __init__(self, device: int = 0):
+        torch = require_gpu()
+        self.lib = _lib.load()
+        self.device = int(device)
+        self.dev = torch.device("cuda", self.device)
+        ptr = ctypes.c_void_p()
+        check(self.lib.vrpms_ctx_create(self.device, ctypes.byref(ptr)))
+        self._ctx = ptr
+        self.problem = None
+        self.N = self.H = self.K = 0
+        self.objective = OBJ_SUM
+
+    # -- lifetime -----------------------------------------------------------
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self.lib.vrpms_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._ctx
+
+    def stream(self):
+        return ctypes.c_void_p(_torch().cuda.current_stream(self.dev).cuda_stream)
+
+    # -- instance -----------------------------------------------------------
+    def set_instance(self, problem: int, durations, demand=None, capacities=None,
+                     start_times=(0,), objective: int = OBJ_SUM):
+        """``durations``: int [N][N] or [H][N][N] (compact node indices)."""
+        torch = _torch()
+        D = np.asarray(durations)
+        if D.ndim == 2:
+            D = D[None]
+        if D.ndim != 3 or D.shape[1] != D.shape[2]:
+            raise ValueError("durations must be [N][N] or [H][N][N]")
+        if D.size and (D.min() < np.iinfo(np.int32).min or D.max() > np.iinfo(np.int32).max):
+            raise VrpmsError(_lib.VRPMS_ERANGE, "durations do not fit int32")
+        H, N = int(D.shape[0]), int(D.shape[1])
+        st = np.asarray(start_times, dtype=np.int64).reshape(-1)
+        K = int(st.shape[0])
+        d_dur = torch.as_tensor(np.ascontiguousarray(D, dtype=np.int32), device=self.dev)
+        d_st = torch.as_tensor(st.astype(np.int32), device=self.dev)
+        d_dem = d_cap = None
+        if problem == CVRP:
+            d_dem = torch.as_tensor(np.asarray(demand, dtype=np.int32).reshape(-1), device=self.dev)
+            d_cap = torch.as_tensor(np.asarray(capacities, dtype=np.int32).reshape(-1), device=self.dev)
+            if d_dem.numel() != N:
+                raise ValueError(f"demand has {d_dem.numel()} entries, matrix has {N} nodes")
+            if d_cap.numel() != K:
+                raise ValueError("capacities and start_times must have the same length")
+        check(self.lib.vrpms_set_instance(
+            self._ctx, int(problem), d_dur.data_ptr(), H, N,
+            d_dem.data_ptr() if d_dem is not None else None,
+            d_cap.data_ptr() if d_cap is not None else None,
+            d_st.data_ptr(), K, int(objective), self.stream()))
+        self.problem, self.N, self.H, self.K, self.objective = problem, N, H, K, objective
+
+    # -- scoring ------------------------------------------------------------
+    def eval(self, perms, n: int | None = None, with_parts: bool = False, out=None):
+        """Score a [C][ld] tour tensor on the device.  Returns keys (uint64
+        stored as int64) or (keys, sums, maxs, unvisited) with ``with_parts``."""
+        torch = _torch()
+        if perms.device != self.dev or perms.dim() != 2:
+            raise ValueError(f"tours must be a 2-D tensor on {self.dev}")
+        if not perms.is_contiguous():
+            raise ValueError("tours must be contiguous")
+        C, ld = perms.shape
+        n = ld if n is None else int(n)
+        pb = perm_dtype_bytes(perms)
+        keys = out if out is not None else torch.empty(C, dtype=torch.int64, device=self.dev)
+        sums = maxs = unv = None
+        if with_parts:
+            sums = torch.empty(C, dtype=torch.int32, device=self.dev)
+            maxs = torch.empty(C, dtype=torch.int32, device=self.dev)
+            unv = torch.empty(C, dtype=torch.int32, device=self.dev)
+        ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        check(self.lib.vrpms_eval(self._ctx, perms.data_ptr(), pb, C, n, ld, keys.data_ptr(),
+                                  ptr(sums), ptr(maxs), ptr(unv), self.stream()))
+        return (keys, sums, maxs, unv) if with_parts else keys
+
+    def eval_path(self, perms) -> int:
+        return self.lib.vrpms_eval_path(self._ctx, perm_dtype_bytes(perms), perms.shape[-1],
+                                        perms.data_ptr())
+
+    def decode(self, perm, n: int | None = None):
+        """Vehicle of each tour position and per-vehicle durations (host lists)."""
+        torch = _torch()
+        perm = perm.reshape(-1).contiguous()
+        n = perm.numel() if n is None else int(n)
+        veh = torch.empty(max(n, 1), dtype=torch.int32, device=self.dev)
+        dur = torch.empty(self.K, dtype=torch.int32, device=self.dev)
+        check(self.lib.vrpms_decode(self._ctx, perm.data_ptr(), perm_dtype_bytes(perm), n,
+                                    veh.data_ptr(), dur.data_ptr(), self.stream()))
+        return veh[:n].cpu().tolist(), dur.cpu().tolist()
+
+    def argmin(self, keys):
+        """(min key, first index) over a key tensor, reduced on the device."""
+        torch = _torch()
+        out = torch.empty(2, dtype=torch.int64, device=self.dev)
+        check(self.lib.vrpms_argmin(self._ctx, keys.data_ptr(), keys.numel(), out.data_ptr(),
+                                    self.stream()))
+        k, i = out.cpu().tolist()
+        return k & ((1 << 64) - 1), i
+
+
+def keys_to_u64(keys) -> np.ndarray:
+    """int64 tensor of A8 keys -> numpy uint64 (bit-identical view)."""
+    return keys.cpu().numpy().view(np.uint64)

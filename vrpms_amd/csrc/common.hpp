@@ -1,0 +1,69 @@
+// Shared device helpers for the vrpms gfx950 library.
+//
+// Everything here is integer arithmetic except the SA acceptance test, which
+// uses the deterministic exp2 below (IEEE basic ops only, built with
+// -ffp-contract=off) so that the CPU oracle reproduces it bit for bit.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define VRPMS_DEV __device__ __forceinline__
+
+namespace vrpms {
+
+constexpr int kWave = 64;                 // CDNA wavefront width (never 32)
+constexpr uint32_t kKeyClamp = (1u << 28) - 1;
+constexpr uint32_t kUnvClamp = 255;
+
+// unv<<56 | min(P,2^28-1)<<28 | min(S,2^28-1).
+VRPMS_DEV uint64_t pack_key(uint32_t unv, uint32_t primary, uint32_t secondary) {
+  unv = unv < kUnvClamp ? unv : kUnvClamp;
+  primary = primary < kKeyClamp ? primary : kKeyClamp;
+  secondary = secondary < kKeyClamp ? secondary : kKeyClamp;
+  return ((uint64_t)unv << 56) | ((uint64_t)primary << 28) | (uint64_t)secondary;
+}
+
+// A8 with the objective selector: 0 = sum first, 1 = max first.
+VRPMS_DEV uint64_t cvrp_key(uint32_t unv, uint32_t dsum, uint32_t dmax, int objective) {
+  return objective ? pack_key(unv, dmax, dsum) : pack_key(unv, dsum, dmax);
+}
+
+// Philox4x32-10 (Salmon et al. SC'11), Random123 constants.
+struct u32x4 { uint32_t x, y, z, w; };
+
+VRPMS_DEV u32x4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                       uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+  }
+  return {c0, c1, c2, c3};
+}
+
+// Wave64 min over uint64 via cross-lane shuffles (xor butterfly, 6 steps).
+VRPMS_DEV uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t o = __shfl_xor(v, off, kWave);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+// Lexicographic (key, idx) min across the wave.
+VRPMS_DEV void wave_argmin(uint64_t& key, uint64_t& idx) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t ok = __shfl_xor(key, off, kWave);
+    const uint64_t oi = __shfl_xor(idx, off, kWave);
+    const bool take = ok < key || (ok == key && oi < idx);
+    key = take ? ok : key;
+    idx = take ? oi : idx;
+  }
+}
+
+}  // namespace vrpms

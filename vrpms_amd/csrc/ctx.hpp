@@ -1,0 +1,58 @@
+// Solver context shared by the translation units of libvrpms.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/vrpms.h"
+
+namespace vrpms {
+
+// Where the kernels read the duration matrix from (SURVEY.md §8d tiers).
+enum MatTier : int {
+  kTierLdsPacked = 0,  // static CVRP, N <= 128: packed u64 {dur | ret,out,dem} in LDS
+  kTierLds = 1,        // whole [H][N][N] (u16 or i32) staged in LDS per workgroup
+  kTierGlobal = 2,     // L2 / Infinity-Cache resident gathers (u16 or i32)
+};
+
+struct Instance {
+  int problem = VRPMS_TSP;
+  int H = 1, N = 0, K = 1, objective = VRPMS_OBJ_SUM;
+  int max_dur = 0, max_dem = 0, max_start = 0, min_cap = 0, max_cap = 0;
+  bool uniform_cap = true;
+  int cap0 = 0;
+  // device copies owned by the context
+  int32_t* mat32 = nullptr;    // [H][N][N]
+  uint16_t* mat16 = nullptr;   // [H][N][N] when max_dur <= 65535
+  uint64_t* pack64 = nullptr;  // [N][N] packed static CVRP layout (tier 0)
+  int32_t* dem = nullptr;      // [N]
+  int32_t* cap = nullptr;      // [K]
+  int32_t* start = nullptr;    // [K]
+  int pack_w = 0;              // field width of ret/out in the packed hi word
+  int tier = kTierGlobal;
+  bool use16 = false;
+};
+
+}  // namespace vrpms
+
+struct vrpms_ctx {
+  int device = 0;
+  bool has_instance = false;
+  vrpms::Instance inst;
+  int num_cus = 256;
+  size_t max_lds = 160 * 1024;
+  int32_t* d_stats = nullptr;   // scratch for set_instance validation
+  uint64_t* d_scratch = nullptr;  // small reduction scratch
+};
+
+namespace vrpms {
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+int hip_fail(hipError_t e, const char* what);
+}  // namespace vrpms
+
+#define VRPMS_HIP(call)                                               \
+  do {                                                                \
+    hipError_t _e = (call);                                           \
+    if (_e != hipSuccess) return ::vrpms::hip_fail(_e, #call);        \
+  } while (0)
