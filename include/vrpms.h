@@ -84,10 +84,30 @@ int vrpms_eval(vrpms_ctx* ctx, const void* d_perms, int32_t perm_bytes, int64_t 
                int64_t ld, uint64_t* d_keys, int32_t* d_sum, int32_t* d_max, int32_t* d_unv,
                void* stream);
 
+/* Same scoring on the word-interleaved tour layout (VRPMS_LAYOUT_WORDS):
+ *   d_words   uint32 [ceil(n/4)][C]; word w of candidate c packs customers
+ *             4w..4w+3 (uint8 each, low byte first).  N <= 256.
+ * Lane c's loads of word w form one contiguous 256-B wave access, so tours
+ * stream HBM -> registers with no LDS staging (the layout the on-device
+ * search kernels emit).  Outputs as vrpms_eval. */
+int vrpms_eval_words(vrpms_ctx* ctx, const uint32_t* d_words, int64_t C, int32_t n,
+                     uint64_t* d_keys, int32_t* d_sum, int32_t* d_max, int32_t* d_unv,
+                     void* stream);
+
+/* Re-layout uint8 rows [C][ld] into the word-interleaved layout. */
+int vrpms_rows_to_words(vrpms_ctx* ctx, const uint8_t* d_rows, int64_t C, int32_t n, int64_t ld,
+                        uint32_t* d_words, void* stream);
+
 /* Which scoring kernel vrpms_eval picks for these tour buffers:
  * 0 = eval_cvrp_packed (LDS packed matrix + LDS-staged tiles),
  * 1 = eval_tsp_staged, 2 = eval_generic; -1 = no instance. */
 int vrpms_eval_path(vrpms_ctx* ctx, int32_t perm_bytes, int64_t ld, const void* d_perms);
+
+/* Context options (kernel-variant overrides for A/B tests and profiling).
+ *   VRPMS_OPT_SPLIT_MODE: 0 = auto (branch-free prefix-ret split whenever its
+ *   packed layout fits), 2 = force the branchy split in eval_cvrp_packed. */
+#define VRPMS_OPT_SPLIT_MODE 1
+int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value);
 
 /* Decode ONE giant tour into the result dict of api/vrp/ga/index.py:49-53
  * (A6/A7): d_vehicle_of[i] = vehicle serving perm position i, or -1 when

@@ -59,18 +59,89 @@ def check_batch(ctx, coracle, inst, P, n=None, objective=0, expect_path=None):
     return got_k
 
 
+@pytest.fixture(params=[0, 2], ids=["prefix_ret", "branchy"])
+def split_mode(request, ctx):
+    ctx.set_split_mode(request.param)
+    yield request.param
+    ctx.set_split_mode(0)
+
+
 @pytest.mark.parametrize("objective", [0, 1])
-def test_cvrp100_packed_path(ctx, coracle, objective):
+def test_cvrp100_packed_path(ctx, coracle, objective, split_mode):
     inst = synth.cvrp(100, 8, seed=0)
     P = synth.random_perms(20000 + 37, inst.n, seed=1)          # ragged last tile
     check_batch(ctx, coracle, inst, P, objective=objective, expect_path=0)
 
 
-def test_cvrp_tight_capacity_unvisited(ctx, coracle):
+def test_cvrp_tight_capacity_unvisited(ctx, coracle, split_mode):
     inst = synth.cvrp(100, 8, seed=2, slack=0.85)
     P = synth.random_perms(5000, inst.n, seed=3)
     k = check_batch(ctx, coracle, inst, P, expect_path=0)
     assert (k >> np.uint64(56)).max() > 0
+
+
+def test_cvrp_single_vehicle_and_oversized_first(ctx, coracle, split_mode):
+    inst = synth.cvrp(30, 1, seed=5, slack=0.5)            # K = 1: exhausts early
+    P = synth.random_perms(3000, inst.n, seed=6, ld=32)
+    check_batch(ctx, coracle, inst, P, n=inst.n, expect_path=0)
+    inst = synth.cvrp(30, 4, seed=7)
+    inst.demand[3] = int(inst.capacities[0]) + 1           # fits no vehicle at all
+    P = synth.random_perms(3000, inst.n, seed=8, ld=32)
+    P[:50, 0] = 3                                           # ... and sometimes comes first
+    P[:50, 1:inst.n] = np.array([x for x in range(1, inst.n + 1) if x != 3], dtype=np.uint8)
+    check_batch(ctx, coracle, inst, P, n=inst.n, expect_path=0)
+
+
+def test_cvrp_asymmetric_matrix_prefix_ret(ctx, coracle, split_mode):
+    # asymmetric durations: dur(a,b) + ret(b) - ret(a) goes negative often
+    rng = np.random.default_rng(3)
+    N = 70
+    D = rng.integers(0, 3000, size=(N, N))
+    np.fill_diagonal(D, 0)
+    D[:, 0] = rng.integers(2000, 3000, size=N)              # expensive returns
+    D[0, 0] = 0
+    dem = np.concatenate([[0], rng.integers(1, 30, N - 1)])
+    inst = synth.Instance("asym", D[None], dem, np.full(6, 200), np.zeros(6, dtype=np.int64),
+                          "cvrp")
+    P = synth.random_perms(6000, inst.n, seed=4, ld=72)
+    check_batch(ctx, coracle, inst, P, n=inst.n, expect_path=0)
+
+
+def check_words(ctx, coracle, inst, P, n, objective=0):
+    """Same tours through the word-interleaved layout (vrpms_eval_words)."""
+    load(ctx, inst, objective)
+    words = ctx.to_words(upload(ctx, P), n=n)
+    keys, sums, maxs, unv = ctx.eval_words(words, n, with_parts=True)
+    ref = coracle.eval_batch(inst.durations, P, inst.demand, inst.capacities, inst.start_times,
+                             problem=1, objective=objective, n=n)
+    np.testing.assert_array_equal(keys.cpu().numpy().view(np.uint64), ref[0])
+    np.testing.assert_array_equal(sums.cpu().numpy(), ref[1])
+    np.testing.assert_array_equal(maxs.cpu().numpy(), ref[2])
+    np.testing.assert_array_equal(unv.cpu().numpy(), ref[3])
+
+
+@pytest.mark.parametrize("C", [1, 1023, 70001])
+def test_words_layout_cvrp100(ctx, coracle, C):
+    inst = synth.cvrp(100, 8, seed=0)
+    check_words(ctx, coracle, inst, synth.random_perms(C, inst.n, seed=C), inst.n)
+
+
+@pytest.mark.parametrize("n,K,slack", [(29, 1, 0.5), (37, 4, 0.9), (5, 2, 1.0), (64, 8, 0.8)])
+def test_words_layout_ragged_and_tight(ctx, coracle, n, K, slack, split_mode):
+    inst = synth.cvrp(n, K, seed=n, slack=slack)
+    P = synth.random_perms(20000, inst.n, seed=1)
+    check_words(ctx, coracle, inst, P, inst.n, objective=n % 2)
+
+
+def test_words_layout_oversize_and_fallbacks(ctx, coracle):
+    inst = synth.cvrp(40, 4, seed=7)
+    inst.demand[3] = int(inst.capacities[0]) + 1            # OVS variant of the fast kernel
+    check_words(ctx, coracle, inst, synth.random_perms(9000, inst.n, seed=2), inst.n)
+    het = synth.cvrp(60, 6, seed=4)
+    het.capacities = np.array([40, 5, 90, 30, 7, 60])        # generic fallback, words access
+    check_words(ctx, coracle, het, synth.random_perms(5000, het.n, seed=3), het.n)
+    td = synth.td_cvrp(30, 3, seed=3)                        # H = 24 through words
+    check_words(ctx, coracle, td, synth.random_perms(5000, td.n, seed=4), td.n)
 
 
 def test_cvrp_heterogeneous_fleet_and_oversized_demand(ctx, coracle):

@@ -1,0 +1,51 @@
+#!/usr/bin/env bash
+# Guarded GPU session: every step has its own time limit; a crash, abort,
+# fault or timeout (any status other than 0 or a plain test failure 1) ends
+# the script before anything else touches the GPU.
+# usage: tools/gpu_run.sh <step>...   steps: tests smoke bench prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+run() {  # name, seconds, cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 25 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ] && [ $rc -ne 2 ]; then
+    echo "!! $name ended with status $rc: stopping, nothing else runs on the GPU"
+    exit $rc
+  fi
+  return 0
+}
+
+for step in "$@"; do
+  case $step in
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py ;;
+    benchq) run bench_quick 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
+    prof)
+      cd /tmp
+      run rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline
+      cd "$ROOT" ;;
+    pmc)
+      cd /tmp
+      B="python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline"
+      run pmc_a 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS \
+          --output-format csv -d "$OUT/pmc_a" -o run -- $B
+      run pmc_b 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_SCA \
+          --output-format csv -d "$OUT/pmc_b" -o run -- $B
+      run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- $B
+      run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- $B
+      cd "$ROOT" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== all steps done"

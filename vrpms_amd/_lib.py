@@ -24,6 +24,7 @@ VRPMS_ENOMEM = -5
 
 TSP = 0
 CVRP = 1
+OPT_SPLIT_MODE = 1
 OBJ_SUM = 0
 OBJ_MAX = 1
 
@@ -42,6 +43,9 @@ SIGNATURES = {
     "vrpms_set_instance": (_c.c_int, [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _i32, _i32, _vp]),
     "vrpms_eval": (_c.c_int, [_vp, _vp, _i32, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _vp]),
     "vrpms_eval_path": (_c.c_int, [_vp, _i32, _i64, _vp]),
+    "vrpms_eval_words": (_c.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "vrpms_rows_to_words": (_c.c_int, [_vp, _vp, _i64, _i32, _i64, _vp, _vp]),
+    "vrpms_set_option": (_c.c_int, [_vp, _i32, _i32]),
     "vrpms_decode": (_c.c_int, [_vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "vrpms_argmin": (_c.c_int, [_vp, _vp, _i64, _vp, _vp]),
 }

@@ -135,6 +135,36 @@ class Context:
                                   ptr(sums), ptr(maxs), ptr(unv), self.stream()))
         return (keys, sums, maxs, unv) if with_parts else keys
 
+    def to_words(self, perms, n: int | None = None):
+        """uint8 [C][ld] rows -> int32 [ceil(n/4)][C] word-interleaved layout."""
+        torch = _torch()
+        C, ld = perms.shape
+        n = ld if n is None else int(n)
+        words = torch.empty(((n + 3) // 4, C), dtype=torch.int32, device=self.dev)
+        check(self.lib.vrpms_rows_to_words(self._ctx, perms.data_ptr(), C, n, ld,
+                                           words.data_ptr(), self.stream()))
+        return words
+
+    def eval_words(self, words, n: int, with_parts: bool = False, out=None):
+        """Score tours in the word-interleaved layout (see vrpms_eval_words)."""
+        torch = _torch()
+        if words.device != self.dev or words.dim() != 2 or not words.is_contiguous():
+            raise ValueError("words must be a contiguous 2-D tensor on the context device")
+        if words.shape[0] != (int(n) + 3) // 4:
+            raise ValueError("words must have ceil(n/4) rows")
+        C = words.shape[1]
+        keys = out if out is not None else torch.empty(C, dtype=torch.int64, device=self.dev)
+        parts = [torch.empty(C, dtype=torch.int32, device=self.dev) for _ in range(3)] \
+            if with_parts else [None, None, None]
+        ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        check(self.lib.vrpms_eval_words(self._ctx, words.data_ptr(), C, int(n), keys.data_ptr(),
+                                        *[ptr(p) for p in parts], self.stream()))
+        return (keys, *parts) if with_parts else keys
+
+    def set_split_mode(self, mode: int):
+        """0 = auto (branch-free prefix-ret split when it fits), 2 = branchy."""
+        check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_SPLIT_MODE, int(mode)))
+
     def eval_path(self, perms) -> int:
         return self.lib.vrpms_eval_path(self._ctx, perm_dtype_bytes(perms), perms.shape[-1],
                                         perms.data_ptr())

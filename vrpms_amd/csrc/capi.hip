@@ -96,6 +96,28 @@ __global__ void pack64_kernel(const int32_t* __restrict__ D, const int32_t* __re
   }
 }
 
+// Prefix-ret layout (uniform fleet).  A route's accumulator is
+// acc = load << S | (cur + ret(prev)); appending b after a adds
+// lo(a,b) = dem(b) << S + dur(a,b) + ret(b) - ret(a), which may be negative in
+// its low part but keeps acc exact in 32-bit two's complement because the
+// true running value stays in [0, 2^S).  ret(depot) is taken as 0.
+__global__ void pack_prefix_kernel(const int32_t* __restrict__ D, const int32_t* __restrict__ dem,
+                                   int N, int S, uint64_t* __restrict__ out) {
+  const int64_t total = (int64_t)N * N;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int a = (int)(i / N), b = (int)(i % N);
+    uint32_t lo = 0, hi = 0;
+    if (b > 0) {
+      const int64_t retb = D[(int64_t)b * N], reta = a > 0 ? D[(int64_t)a * N] : 0;
+      const int64_t d = (int64_t)D[(int64_t)a * N + b] + retb - reta;
+      lo = (uint32_t)(((int64_t)dem[b] << S) + d);
+      hi = (uint32_t)(D[b] + retb) | ((uint32_t)dem[b] << S);
+    }
+    out[i] = (uint64_t)lo | ((uint64_t)hi << 32);
+  }
+}
+
 static int bits_for(int v) {
   int b = 1;
   while (b < 31 && (1 << b) <= v) ++b;
@@ -106,6 +128,7 @@ static void free_instance(Instance& in) {
   (void)hipFree(in.mat32);
   (void)hipFree(in.mat16);
   (void)hipFree(in.pack64);
+  (void)hipFree(in.pack64p);
   (void)hipFree(in.dem);
   (void)hipFree(in.cap);
   (void)hipFree(in.start);
@@ -155,6 +178,17 @@ int vrpms_ctx_destroy(vrpms_ctx* ctx) {
   (void)hipFree(ctx->d_scratch);
   delete ctx;
   return VRPMS_OK;
+}
+
+int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value) {
+  if (!ctx) return fail(VRPMS_EINVAL, "vrpms_set_option: ctx is NULL");
+  if (option == VRPMS_OPT_SPLIT_MODE) {
+    if (value != 0 && value != 2)
+      return fail(VRPMS_EINVAL, "vrpms_set_option: split mode must be 0 (auto) or 2 (branchy)");
+    ctx->opt_split_mode = value;
+    return VRPMS_OK;
+  }
+  return fail(VRPMS_EINVAL, "vrpms_set_option: unknown option " + std::to_string(option));
 }
 
 int vrpms_set_instance(vrpms_ctx* ctx, int32_t problem, const int32_t* d_dur, int32_t H,
@@ -248,6 +282,20 @@ int vrpms_set_instance(vrpms_ctx* ctx, int32_t problem, const int32_t* d_dur, in
       pack64_kernel<<<(N * N + 255) / 256, 256, 0, s>>>(in.mat32, in.dem, N, w, in.pack64);
       VRPMS_HIP(hipGetLastError());
       in.tier = kTierLdsPacked;
+    }
+    // prefix-ret layout: S bits hold any route's cur + ret(last) <= (N+1)*max_dur,
+    // the bits above hold load + demand <= cap + max_dem.
+    const int64_t route_bound = (int64_t)(N + 1) * in.max_dur;
+    int S = 1;
+    while (S < 31 && ((int64_t)1 << S) <= route_bound) ++S;
+    const int64_t load_bound = (int64_t)in.cap0 + in.max_dem + 1;
+    if (in.pack64 && in.uniform_cap && S < 32 && (load_bound << S) < ((int64_t)1 << 32)) {
+      in.pref_S = S;
+      in.pref_lim = (uint32_t)(((int64_t)in.cap0 + 1) << S);
+      in.pref_smask = (uint32_t)(((int64_t)1 << S) - 1);
+      VRPMS_HIP(hipMalloc(&in.pack64p, (size_t)N * N * 8));
+      pack_prefix_kernel<<<(N * N + 255) / 256, 256, 0, s>>>(in.mat32, in.dem, N, S, in.pack64p);
+      VRPMS_HIP(hipGetLastError());
     }
   }
   VRPMS_HIP(hipStreamSynchronize(s));

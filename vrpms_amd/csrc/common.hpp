@@ -12,6 +12,10 @@
 namespace vrpms {
 
 constexpr int kWave = 64;                 // CDNA wavefront width (never 32)
+
+// Native 16-byte vector (HIP's uint4 is a union-wrapped struct that can
+// defeat scalar replacement and push register arrays to scratch).
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 constexpr uint32_t kKeyClamp = (1u << 28) - 1;
 constexpr uint32_t kUnvClamp = 255;
 

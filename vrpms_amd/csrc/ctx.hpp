@@ -29,6 +29,11 @@ struct Instance {
   int32_t* cap = nullptr;      // [K]
   int32_t* start = nullptr;    // [K]
   int pack_w = 0;              // field width of ret/out in the packed hi word
+  // "prefix-ret" layout for a uniform fleet (eval_cvrp_packed MODE 1):
+  // lo = dem(b) << S + dur(a,b) + ret(b) - ret(a) (mod 2^32), hi = out(b) + ret(b) | dem(b) << S
+  uint64_t* pack64p = nullptr;
+  int pref_S = 0;
+  uint32_t pref_lim = 0, pref_smask = 0;
   int tier = kTierGlobal;
   bool use16 = false;
 };
@@ -41,6 +46,7 @@ struct vrpms_ctx {
   vrpms::Instance inst;
   int num_cus = 256;
   size_t max_lds = 160 * 1024;
+  int opt_split_mode = 0;       // VRPMS_OPT_SPLIT_MODE (0 auto, 2 force branchy)
   int32_t* d_stats = nullptr;   // scratch for set_instance validation
   uint64_t* d_scratch = nullptr;  // small reduction scratch
 };

@@ -67,7 +67,19 @@ VRPMS_DEV void write_out(const EvalArgs& a, int64_t c, uint64_t key, int32_t s, 
 // ---------------------------------------------------------------------------
 // Generic lane-per-candidate evaluation (any tier / H / perm width).
 // ---------------------------------------------------------------------------
-template <typename MatT, bool LDS, bool CVRP, int HM, typename PermT>
+// Tour element i of candidate c in either layout.
+template <typename PermT, bool WORDS>
+struct TourAccess {
+  const PermT* row;
+  const uint32_t* w;
+  int64_t C, c;
+  VRPMS_DEV uint32_t operator[](int i) const {
+    if constexpr (WORDS) return (w[(int64_t)(i >> 2) * C + c] >> (8 * (i & 3))) & 0xffu;
+    else return (uint32_t)row[i];
+  }
+};
+
+template <typename MatT, bool LDS, bool CVRP, int HM, typename PermT, bool WORDS = false>
 __global__ __launch_bounds__(256) void eval_generic(EvalArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = a.N;
@@ -89,7 +101,7 @@ __global__ __launch_bounds__(256) void eval_generic(EvalArgs a) {
   const uint32_t Nm1 = (uint32_t)N - 1;
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < a.C;
        c += (int64_t)gridDim.x * blockDim.x) {
-    const PermT* row = P + c * a.ld;
+    const TourAccess<PermT, WORDS> row{P + c * a.ld, static_cast<const uint32_t*>(a.perms), a.C, c};
     if constexpr (!CVRP) {
       const int t0 = a.start[0];
       int t = t0;
@@ -155,8 +167,8 @@ __global__ __launch_bounds__(256) void eval_generic(EvalArgs a) {
 template <int BLOCK>
 VRPMS_DEV void stage_tile(unsigned char* tile, const unsigned char* g, uint32_t bytes) {
   const uint32_t nvec = bytes / 16;
-  const uint4* gs = reinterpret_cast<const uint4*>(g);
-  uint4* ts = reinterpret_cast<uint4*>(tile);
+  const v4u* gs = reinterpret_cast<const v4u*>(g);
+  v4u* ts = reinterpret_cast<v4u*>(tile);
   for (uint32_t i = threadIdx.x; i < nvec; i += BLOCK) ts[i] = gs[i];
   const uint32_t* gw = reinterpret_cast<const uint32_t*>(g);
   uint32_t* tw = reinterpret_cast<uint32_t*>(tile);
@@ -167,6 +179,7 @@ struct PackedArgs {
   const uint64_t* pack;
   int N, K, w;
   int uniform_cap, cap0;
+  uint32_t lim, smask;  // MODE 1: (cap0 + 1) << S and (1 << S) - 1
   const int32_t* cap;
   const uint8_t* perms;
   int64_t C;
@@ -183,17 +196,60 @@ struct PackedArgs {
 // grows by dur(prev,c), else the route closes with ret(prev) (kept from the
 // previous gather) and vehicle k+1 opens with out(c).  Static H = 1, so a
 // route's duration is the sum of its legs (A7, start time cancels).
-template <int BLOCK, bool UNIFORM>
+//
+// Address chain: the gather for position i reads E[p(i-1)][p(i)], which
+// depends only on the tour -- never on the split state -- because a
+// visited customer always becomes `prev` and, once every vehicle is closed
+// (k == K), `prev` is never read again.  So the gathers of a whole perm
+// word (4 customers) are issued one word ahead of the split arithmetic and
+// the LDS latency overlaps the VALU work instead of serialising it.
+//
+// Tile pipeline: the next tile's tours are loaded into registers (16-B
+// coalesced loads) while the current tile is scored, then written to the
+// LDS tile between two barriers.
+template <int NV>
+VRPMS_DEV void prefetch_tile(v4u (&pf)[NV], const unsigned char* g, uint32_t bytes, int block) {
+  // unconditional (clamped) loads keep pf[] in registers
+  const uint32_t last = bytes >= 16 ? bytes / 16 - 1 : 0;
+  const v4u* gs = reinterpret_cast<const v4u*>(g);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const uint32_t idx = threadIdx.x + (uint32_t)v * block;
+    pf[v] = gs[min(idx, last)];
+  }
+}
+
+template <int NV>
+VRPMS_DEV void commit_tile(const v4u (&pf)[NV], unsigned char* tile, const unsigned char* g,
+                           uint32_t bytes, int block) {
+  const uint32_t nvec = bytes / 16;
+  v4u* ts = reinterpret_cast<v4u*>(tile);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const uint32_t idx = threadIdx.x + (uint32_t)v * block;
+    if (idx < nvec) ts[idx] = pf[v];
+  }
+  // ragged last tile: the few trailing dwords are copied directly
+  const uint32_t* gw = reinterpret_cast<const uint32_t*>(g);
+  uint32_t* tw = reinterpret_cast<uint32_t*>(tile);
+  for (uint32_t i = nvec * 4 + threadIdx.x; i < bytes / 4; i += block) tw[i] = gw[i];
+}
+
+// MODE 0: heterogeneous fleet (capacities from LDS, branchy split)
+// MODE 1: uniform fleet, "prefix-ret" layout (branch-free split, see step())
+// MODE 2: uniform fleet, branchy split (when the prefix-ret fields do not fit)
+template <int BLOCK, int MODE, int NV>
 __global__ __launch_bounds__(BLOCK) void eval_cvrp_packed(PackedArgs a) {
+  constexpr bool UNIFORM = MODE != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = a.N;
   const uint32_t ebytes = (uint32_t)N * N * 8;
   const uint32_t ebytes16 = (ebytes + 15) & ~15u;
   unsigned char* tile = smem + ebytes16;
-  int32_t* capL = reinterpret_cast<int32_t*>(tile + (uint32_t)BLOCK * a.ld);
+  int32_t* capL = reinterpret_cast<int32_t*>(tile + (uint32_t)BLOCK * a.ld + 16);
   {
-    const uint4* src = reinterpret_cast<const uint4*>(a.pack);
-    uint4* dst = reinterpret_cast<uint4*>(smem);
+    const v4u* src = reinterpret_cast<const v4u*>(a.pack);
+    v4u* dst = reinterpret_cast<v4u*>(smem);
     for (uint32_t i = threadIdx.x; i < ebytes / 16; i += BLOCK) dst[i] = src[i];
     if ((ebytes & 8u) && threadIdx.x == 0)
       reinterpret_cast<uint64_t*>(smem)[ebytes / 8 - 1] = a.pack[ebytes / 8 - 1];
@@ -204,71 +260,280 @@ __global__ __launch_bounds__(BLOCK) void eval_cvrp_packed(PackedArgs a) {
   const int K = a.K, n = a.n, ld = a.ld;
   const uint32_t w = (uint32_t)a.w, wmask = (1u << w) - 1u, dshift = 2u * w;
   const int cap0 = a.cap0;
+  const uint32_t lim = a.lim, smask = a.smask;
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  const int nwords = (n + 3) >> 2;
 
-  for (int64_t base = blockIdx.x * (int64_t)BLOCK; base < a.C; base += (int64_t)gridDim.x * BLOCK) {
+  v4u pf[NV];
+  int64_t base = blockIdx.x * (int64_t)BLOCK;
+  if (base < a.C)
+    prefetch_tile<NV>(pf, a.perms + base * ld, (uint32_t)min<int64_t>(BLOCK, a.C - base) * ld,
+                      BLOCK);
+  for (; base < a.C; base += stride) {
     const int rows = (int)min<int64_t>(BLOCK, a.C - base);
-    __syncthreads();  // previous tile fully consumed (and E/capL staged on entry)
-    stage_tile<BLOCK>(tile, a.perms + base * ld, (uint32_t)rows * ld);
+    __syncthreads();  // previous tile consumed (and E / capL staged on entry)
+    commit_tile<NV>(pf, tile, a.perms + base * ld, (uint32_t)rows * ld, BLOCK);
     __syncthreads();
+    const int64_t nbase = base + stride;
+    if (nbase < a.C)
+      prefetch_tile<NV>(pf, a.perms + nbase * ld, (uint32_t)min<int64_t>(BLOCK, a.C - nbase) * ld,
+                        BLOCK);
     if ((int)threadIdx.x >= rows) continue;
     const uint32_t* row = reinterpret_cast<const uint32_t*>(tile + threadIdx.x * (uint32_t)ld);
 
+    uint32_t dsum = 0, dmax = 0, unv = 0;
     int k = 0;
-    int rcap = UNIFORM ? cap0 : capL[0];
-    uint32_t cur = 0, prow = 0, hprev = 0, dsum = 0, dmax = 0, unv = 0;
-    auto visit = [&](uint32_t c) {
-      const uint64_t e = E[prow + c];
-      const uint32_t dur = (uint32_t)e, hi = (uint32_t)(e >> 32);
-      const int dem = (int)(hi >> dshift);
-      if (dem <= rcap) {
-        cur += dur;
-        rcap -= dem;
-        prow = c * (uint32_t)N;
-        hprev = hi;
-      } else if (k >= K) {
-        ++unv;
+    // MODE 1 state (prefix-ret): acc = load << S | (cur + ret(prev))
+    uint32_t acc = 0;
+    bool dead = false;
+    // MODE 0/2 state
+    int rcap = MODE == 0 ? capL[0] : cap0;
+    uint32_t cur = 0, hprev = 0;
+    // one split step at tour position `pos`
+    auto step = [&](uint64_t e, int pos) {
+      const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
+      if constexpr (MODE == 1) {
+        // Branch-free: one add + one unsigned compare is the capacity test
+        // (the load sits above bit S); closing a route reads its duration
+        // straight out of the low field because ret(prev) is pre-added.
+        const uint32_t t = acc + lo;
+        const bool f = t < lim || dead;
+        const uint32_t rd = f ? 0u : (acc & smask);
+        dsum += rd;
+        dmax = max(dmax, rd);
+        k += f ? 0 : 1;
+        const bool die = !f && (k >= K || hi >= lim);  // no vehicle left / fits none
+        unv = die ? (uint32_t)(n - pos) : unv;
+        dead = dead || die;
+        acc = f ? t : hi;  // hi = open'(c): a fresh route holding c
       } else {
-        if (prow) {  // close the open route: prev -> depot
-          const uint32_t rd = cur + (hprev & wmask);
-          dsum += rd;
-          dmax = max(dmax, rd);
-        }
-        ++k;
-        while (k < K && dem > (UNIFORM ? cap0 : capL[k])) ++k;  // empty vehicles: unused
-        if (k < K) {
-          cur = (hi >> w) & wmask;  // depot -> c
-          rcap = (UNIFORM ? cap0 : capL[k]) - dem;
-          prow = c * (uint32_t)N;
-          hprev = hi;
-        } else {
+        const int dem = (int)(hi >> dshift);
+        if (dem <= rcap) {
+          cur += lo;
+          rcap -= dem;
+        } else if (k >= K) {
           ++unv;
-          rcap = INT_MIN;
-          prow = 0;
+        } else {
+          if (pos != 0) {  // close the open route: prev -> depot
+            const uint32_t rd = cur + (hprev & wmask);
+            dsum += rd;
+            dmax = max(dmax, rd);
+          }
+          ++k;
+          if constexpr (MODE == 2) {
+            if (dem > cap0) k = K;  // fits no (empty) vehicle: all remaining ones unused
+          } else {
+            while (k < K && dem > capL[k]) ++k;
+          }
+          if (k < K) {
+            cur = (hi >> w) & wmask;  // depot -> c
+            rcap = (MODE == 2 ? cap0 : capL[k]) - dem;
+          } else {
+            ++unv;
+            rcap = INT_MIN;
+          }
         }
+        hprev = hi;
       }
     };
-    const int n4 = n >> 2;
-    for (int j = 0; j < n4; ++j) {
-      const uint32_t w4 = row[j];
-      visit(w4 & 0xffu);
-      visit((w4 >> 8) & 0xffu);
-      visit((w4 >> 16) & 0xffu);
-      visit(w4 >> 24);
+    // byte offsets of E[a][b]: a * 8N + 8b with 24-bit multiplies
+    const uint32_t N8 = 8u * (uint32_t)N;
+    const unsigned char* Eb = reinterpret_cast<const unsigned char*>(E);
+    auto gat = [&](uint32_t a_, uint32_t b_) {
+      return *reinterpret_cast<const uint64_t*>(Eb + (__umul24(a_, N8) + (b_ << 3)));
+    };
+    uint32_t wd = row[0];
+    uint32_t c0 = wd & 0xffu, c1 = (wd >> 8) & 0xffu, c2 = (wd >> 16) & 0xffu, c3 = wd >> 24;
+    uint64_t e0 = gat(0, c0), e1 = gat(c0, c1), e2 = gat(c1, c2), e3 = gat(c2, c3);
+    for (int j = 0; j < nwords; ++j) {
+      // issue the next word's gathers before consuming this word's
+      const uint32_t wn = row[j + 1];
+      const uint32_t n0 = wn & 0xffu, n1 = (wn >> 8) & 0xffu, n2 = (wn >> 16) & 0xffu,
+                     n3 = wn >> 24;
+      const uint64_t f0 = gat(c3, n0), f1 = gat(n0, n1), f2 = gat(n1, n2), f3 = gat(n2, n3);
+      const int pos = 4 * j;
+      if (pos + 4 <= n) {
+        step(e0, pos);
+        step(e1, pos + 1);
+        step(e2, pos + 2);
+        step(e3, pos + 3);
+      } else {
+        step(e0, pos);
+        if (pos + 1 < n) step(e1, pos + 1);
+        if (pos + 2 < n) step(e2, pos + 2);
+      }
+      c3 = n3;
+      e0 = f0;
+      e1 = f1;
+      e2 = f2;
+      e3 = f3;
     }
-    if (n & 3) {
-      const uint32_t w4 = row[n4];
-      for (int q = 0; q < (n & 3); ++q) visit((w4 >> (8 * q)) & 0xffu);
-    }
-    if (k < K && prow) {
-      const uint32_t rd = cur + (hprev & wmask);
-      dsum += rd;
-      dmax = max(dmax, rd);
+    if constexpr (MODE == 1) {
+      if (!dead && n > 0) {
+        const uint32_t rd = acc & smask;
+        dsum += rd;
+        dmax = max(dmax, rd);
+      }
+    } else {
+      if (k < K && n > 0) {
+        const uint32_t rd = cur + (hprev & wmask);
+        dsum += rd;
+        dmax = max(dmax, rd);
+      }
     }
     const int64_t c = base + threadIdx.x;
     a.keys[c] = cvrp_key(unv, dsum, dmax, a.objective);
     if (a.sums) a.sums[c] = (int32_t)dsum;
     if (a.maxs) a.maxs[c] = (int32_t)dmax;
     if (a.unv) a.unv[c] = (int32_t)unv;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Word-interleaved tour layout (VRPMS_LAYOUT_WORDS): uint32 W[ceil(n/4)][C],
+// word w of candidate c holds customers 4w..4w+3 (one byte each).  Lane c's
+// loads of word w are one contiguous 256-B wave access, so tours go straight
+// from HBM to registers: no LDS tile, the LDS holds only the matrix and a
+// workgroup can be 1024 lanes (16 waves per CU instead of 8).
+//
+// Each lane streams its candidates through an R-deep register ring of tour
+// words.  Every candidate occupies NWP = roundup(nw, R) ring slots (the
+// padding slots load nothing), so ring slot u always holds word w0 + u and
+// every register index is a compile-time constant; refills run across the
+// candidate boundary (the next candidate's first words are in flight while
+// this one finishes).
+// ---------------------------------------------------------------------------
+struct WordsArgs {
+  const uint64_t* pack;
+  int N, K;
+  uint32_t lim, smask;
+  const uint32_t* words;
+  int64_t C;
+  int n;
+  int objective;
+  uint64_t* keys;
+  int32_t* sums;
+  int32_t* maxs;
+  int32_t* unv;
+};
+
+template <int R, bool OVS>
+__global__ __launch_bounds__(1024) void eval_cvrp_words(WordsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int N = a.N;
+  {
+    const uint32_t ebytes = (uint32_t)N * N * 8;
+    const v4u* src = reinterpret_cast<const v4u*>(a.pack);
+    v4u* dst = reinterpret_cast<v4u*>(smem);
+    for (uint32_t i = threadIdx.x; i < ebytes / 16; i += blockDim.x) dst[i] = src[i];
+    if ((ebytes & 8u) && threadIdx.x == 0)
+      reinterpret_cast<uint64_t*>(smem)[ebytes / 8 - 1] = a.pack[ebytes / 8 - 1];
+  }
+  __syncthreads();
+  const unsigned char* Eb = smem;
+  const uint32_t N8 = 8u * (uint32_t)N;
+  auto gat = [&](uint32_t x, uint32_t y) {
+    return *reinterpret_cast<const uint64_t*>(Eb + (__umul24(x, N8) + (y << 3)));
+  };
+  const int64_t C = a.C;
+  const int n = a.n, nw = (n + 3) >> 2, NWP = (nw + R - 1) / R * R;
+  const uint32_t K = (uint32_t)a.K, lim = a.lim, smask = a.smask;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (c >= C || n == 0) {
+    for (; c < C; c += stride) {
+      a.keys[c] = 0;
+      if (a.sums) a.sums[c] = 0;
+      if (a.maxs) a.maxs[c] = 0;
+      if (a.unv) a.unv[c] = 0;
+    }
+    return;
+  }
+  const uint32_t* W = a.words;
+  uint32_t ring[R];
+  // slot s of the stream = word (s mod NWP) of candidate c + (s / NWP) * stride
+#pragma unroll
+  for (int u = 0; u < R; ++u) ring[u] = u < nw ? W[(int64_t)u * C + c] : 0u;
+
+  for (; c < C; c += stride) {
+    const int64_t cn = c + stride;
+    uint32_t acc = 0, dsum = 0, dmax = 0, unv = 0, k = 0;
+    bool dead = false;
+    uint32_t wd = ring[0];
+    uint32_t c3 = wd >> 24;
+    uint64_t e0 = gat(0, wd & 0xffu), e1 = gat(wd & 0xffu, (wd >> 8) & 0xffu),
+             e2 = gat((wd >> 8) & 0xffu, (wd >> 16) & 0xffu), e3 = gat((wd >> 16) & 0xffu, c3);
+    auto step = [&](uint64_t e) {
+      const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
+      const uint32_t t = acc + lo;
+      const bool f = t < lim || dead;
+      const uint32_t rd = f ? 0u : (acc & smask);
+      dsum += rd;
+      dmax = max(dmax, rd);
+      k += f ? 0u : 1u;
+      const bool die = !f && (k >= K || (OVS && hi >= lim));
+      dead = dead || die;
+      unv += dead ? 1u : 0u;
+      acc = f ? t : hi;
+    };
+    for (int w0 = 0; w0 < NWP; w0 += R) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const int w = w0 + u;
+        if (w < nw) {
+          // refill this slot with the word R slots ahead in the stream
+          const int wr = w + R;
+          if (wr < nw) ring[u] = W[(int64_t)wr * C + c];
+          else if (wr - NWP >= 0 && wr - NWP < nw && cn < C) ring[u] = W[(int64_t)(wr - NWP) * C + cn];
+          // gathers of the next word, issued before this word's split steps
+          const uint32_t wn = (w + 1 < nw) ? ring[(u + 1) % R] : 0u;
+          const uint32_t n0 = wn & 0xffu, n1 = (wn >> 8) & 0xffu, n2 = (wn >> 16) & 0xffu,
+                         n3 = wn >> 24;
+          const uint64_t f0 = gat(c3, n0), f1 = gat(n0, n1), f2 = gat(n1, n2), f3 = gat(n2, n3);
+          const int pos = 4 * w;
+          step(e0);
+          if (pos + 1 < n) step(e1);
+          if (pos + 2 < n) step(e2);
+          if (pos + 3 < n) step(e3);
+          c3 = n3;
+          e0 = f0;
+          e1 = f1;
+          e2 = f2;
+          e3 = f3;
+        } else {
+          // padding slot: refill with the next candidate's word, if any
+          const int wr = w + R - NWP;
+          if (wr >= 0 && wr < nw && cn < C) ring[u] = W[(int64_t)wr * C + cn];
+        }
+      }
+    }
+    if (!dead) {
+      const uint32_t rd = acc & smask;
+      dsum += rd;
+      dmax = max(dmax, rd);
+    }
+    a.keys[c] = cvrp_key(unv, dsum, dmax, a.objective);
+    if (a.sums) a.sums[c] = (int32_t)dsum;
+    if (a.maxs) a.maxs[c] = (int32_t)dmax;
+    if (a.unv) a.unv[c] = (int32_t)unv;
+  }
+}
+
+// rows (uint8 [C][ld]) -> words (uint32 [ceil(n/4)][C]); one lane per (word, candidate)
+__global__ void rows_to_words_kernel(const uint8_t* __restrict__ rows, int64_t C, int n,
+                                     int64_t ld, uint32_t* __restrict__ words) {
+  const int nw = (n + 3) >> 2;
+  const int64_t total = (int64_t)nw * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int w = (int)(i / C);
+    const int64_t c = i - (int64_t)w * C;
+    const uint8_t* r = rows + c * ld + 4 * w;
+    uint32_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (4 * w + q < n) v |= (uint32_t)r[q] << (8 * q);
+    words[i] = v;
   }
 }
 
@@ -423,7 +688,7 @@ static void allow_lds(K kern, size_t bytes) {
                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
-template <typename MatT, bool LDS, bool CVRP, typename PermT>
+template <typename MatT, bool LDS, bool CVRP, typename PermT, bool WORDS>
 static int launch_generic_h(vrpms_ctx* ctx, const EvalArgs& a, hipStream_t s) {
   const Instance& in = ctx->inst;
   const int64_t blocks_needed = (a.C + 255) / 256;
@@ -436,7 +701,7 @@ static int launch_generic_h(vrpms_ctx* ctx, const EvalArgs& a, hipStream_t s) {
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(blocks_needed, (int64_t)ctx->num_cus * per_cu));
 #define VRPMS_LAUNCH_G(HM)                                                     \
   do {                                                                         \
-    auto kern = eval_generic<MatT, LDS, CVRP, HM, PermT>;                      \
+    auto kern = eval_generic<MatT, LDS, CVRP, HM, PermT, WORDS>;               \
     if (lds > 65536) allow_lds(kern, lds);                                     \
     kern<<<grid, 256, lds, s>>>(a);                                            \
   } while (0)
@@ -451,7 +716,7 @@ static int launch_generic_h(vrpms_ctx* ctx, const EvalArgs& a, hipStream_t s) {
   return VRPMS_OK;
 }
 
-template <typename PermT>
+template <typename PermT, bool WORDS = false>
 static int launch_generic(vrpms_ctx* ctx, EvalArgs a, hipStream_t s) {
   const Instance& in = ctx->inst;
   const bool lds = in.tier != kTierGlobal &&
@@ -459,15 +724,51 @@ static int launch_generic(vrpms_ctx* ctx, EvalArgs a, hipStream_t s) {
   const bool cvrp = in.problem == VRPMS_CVRP;
   a.mat = in.use16 ? static_cast<const void*>(in.mat16) : static_cast<const void*>(in.mat32);
   if (in.use16) {
-    if (lds) return cvrp ? launch_generic_h<uint16_t, true, true, PermT>(ctx, a, s)
-                         : launch_generic_h<uint16_t, true, false, PermT>(ctx, a, s);
-    return cvrp ? launch_generic_h<uint16_t, false, true, PermT>(ctx, a, s)
-                : launch_generic_h<uint16_t, false, false, PermT>(ctx, a, s);
+    if (lds) return cvrp ? launch_generic_h<uint16_t, true, true, PermT, WORDS>(ctx, a, s)
+                         : launch_generic_h<uint16_t, true, false, PermT, WORDS>(ctx, a, s);
+    return cvrp ? launch_generic_h<uint16_t, false, true, PermT, WORDS>(ctx, a, s)
+                : launch_generic_h<uint16_t, false, false, PermT, WORDS>(ctx, a, s);
   }
-  if (lds) return cvrp ? launch_generic_h<int32_t, true, true, PermT>(ctx, a, s)
-                       : launch_generic_h<int32_t, true, false, PermT>(ctx, a, s);
-  return cvrp ? launch_generic_h<int32_t, false, true, PermT>(ctx, a, s)
-              : launch_generic_h<int32_t, false, false, PermT>(ctx, a, s);
+  if (lds) return cvrp ? launch_generic_h<int32_t, true, true, PermT, WORDS>(ctx, a, s)
+                       : launch_generic_h<int32_t, true, false, PermT, WORDS>(ctx, a, s);
+  return cvrp ? launch_generic_h<int32_t, false, true, PermT, WORDS>(ctx, a, s)
+              : launch_generic_h<int32_t, false, false, PermT, WORDS>(ctx, a, s);
+}
+
+// words-layout fast path available? (uniform fleet, prefix-ret layout, matrix fits LDS)
+static bool words_fast_ok(const vrpms_ctx* ctx) {
+  const Instance& in = ctx->inst;
+  return in.problem == VRPMS_CVRP && in.pack64p && ctx->opt_split_mode != 2 &&
+         (size_t)in.N * in.N * 8 <= ctx->max_lds;
+}
+
+template <int NV>
+static int launch_packed(const PackedArgs& p, bool big, int mode, int grid, size_t lds,
+                         hipStream_t s) {
+  auto go = [&](auto kern, int block) {
+    allow_lds(kern, lds);
+    kern<<<grid, block, lds, s>>>(p);
+  };
+  if (big) {
+    if (mode == 1) go(eval_cvrp_packed<512, 1, NV>, 512);
+    else if (mode == 2) go(eval_cvrp_packed<512, 2, NV>, 512);
+    else go(eval_cvrp_packed<512, 0, NV>, 512);
+  } else {
+    if (mode == 1) go(eval_cvrp_packed<256, 1, NV>, 256);
+    else if (mode == 2) go(eval_cvrp_packed<256, 2, NV>, 256);
+    else go(eval_cvrp_packed<256, 0, NV>, 256);
+  }
+  VRPMS_HIP(hipGetLastError());
+  return VRPMS_OK;
+}
+
+// Split variant for the packed path: 1 (prefix-ret) whenever its layout was
+// built, unless a test forced 2 through vrpms_set_option.
+static int packed_mode(const vrpms_ctx* ctx) {
+  const Instance& in = ctx->inst;
+  if (!in.uniform_cap) return 0;
+  if (in.pack64p && ctx->opt_split_mode != 2) return 1;
+  return 2;
 }
 
 }  // namespace vrpms
@@ -480,8 +781,9 @@ extern "C" int vrpms_eval_path(vrpms_ctx* ctx, int32_t perm_bytes, int64_t ld, c
   const Instance& in = ctx->inst;
   const bool aligned = ((uintptr_t)d_perms & 15u) == 0;
   const bool staged_ok = perm_bytes == 1 && (ld & 3) == 0 && aligned && in.N <= 256;
-  if (in.problem == VRPMS_CVRP && in.tier == kTierLdsPacked && staged_ok) {
-    const size_t need256 = (((size_t)in.N * in.N * 8 + 15) & ~(size_t)15) + 256 * (size_t)ld + 4 * in.K;
+  if (in.problem == VRPMS_CVRP && in.tier == kTierLdsPacked && staged_ok && ld <= 128) {
+    const size_t need256 =
+        (((size_t)in.N * in.N * 8 + 15) & ~(size_t)15) + 256 * (size_t)ld + 16 + 4 * in.K;
     if (need256 <= ctx->max_lds) return 0;
   }
   if (in.problem == VRPMS_TSP && in.H == 1 && staged_ok) {
@@ -508,30 +810,21 @@ extern "C" int vrpms_eval(vrpms_ctx* ctx, const void* d_perms, int32_t perm_byte
   hipStream_t s = (hipStream_t)stream;
   const int path = vrpms_eval_path(ctx, perm_bytes, ld, d_perms);
   if (path == 0) {
-    PackedArgs p{in.pack64, in.N, in.K, in.pack_w, in.uniform_cap ? 1 : 0, in.cap0, in.cap,
+    const int mode = packed_mode(ctx);
+    PackedArgs p{mode == 1 ? in.pack64p : in.pack64, in.N, in.K, in.pack_w,
+                 in.uniform_cap ? 1 : 0, in.cap0, in.pref_lim, in.pref_smask, in.cap,
                  static_cast<const uint8_t*>(d_perms), C, n, (int)ld, in.objective, d_keys, d_sum,
                  d_max, d_unv};
     const size_t e16 = ((size_t)in.N * in.N * 8 + 15) & ~(size_t)15;
-    const bool big = e16 + 512 * (size_t)ld + 4 * in.K <= ctx->max_lds;
+    const bool big = e16 + 512 * (size_t)ld + 16 + 4 * in.K <= ctx->max_lds;
     const int block = big ? 512 : 256;
-    const size_t lds = e16 + (size_t)block * ld + 4 * (size_t)in.K;
+    const size_t lds = e16 + (size_t)block * ld + 16 + 4 * (size_t)in.K;
     const int per_cu = std::max<int>(1, (int)(ctx->max_lds / lds));
     const int64_t tiles = (C + block - 1) / block;
     const int grid = (int)std::min<int64_t>(tiles, (int64_t)ctx->num_cus * per_cu);
-#define VRPMS_LAUNCH_P(B, U)                                \
-  do {                                                      \
-    auto kern = eval_cvrp_packed<B, U>;                     \
-    allow_lds(kern, lds);                                   \
-    kern<<<grid, B, lds, s>>>(p);                           \
-  } while (0)
-    if (big) {
-      if (in.uniform_cap) VRPMS_LAUNCH_P(512, true); else VRPMS_LAUNCH_P(512, false);
-    } else {
-      if (in.uniform_cap) VRPMS_LAUNCH_P(256, true); else VRPMS_LAUNCH_P(256, false);
-    }
-#undef VRPMS_LAUNCH_P
-    VRPMS_HIP(hipGetLastError());
-    return VRPMS_OK;
+    return ld <= 32 ? launch_packed<2>(p, big, mode, grid, lds, s)
+         : ld <= 64 ? launch_packed<4>(p, big, mode, grid, lds, s)
+                    : launch_packed<8>(p, big, mode, grid, lds, s);
   }
   if (path == 1) {
     TspArgs t{in.use16 ? static_cast<const void*>(in.mat16) : static_cast<const void*>(in.mat32),
@@ -557,6 +850,51 @@ extern "C" int vrpms_eval(vrpms_ctx* ctx, const void* d_perms, int32_t perm_byte
   EvalArgs a{nullptr, in.N, in.H, in.K, in.dem, in.cap, in.start, d_perms, C, n, ld,
              in.objective, d_keys, d_sum, d_max, d_unv};
   return perm_bytes == 1 ? launch_generic<uint8_t>(ctx, a, s) : launch_generic<uint16_t>(ctx, a, s);
+}
+
+extern "C" int vrpms_eval_words(vrpms_ctx* ctx, const uint32_t* d_words, int64_t C, int32_t n,
+                                uint64_t* d_keys, int32_t* d_sum, int32_t* d_max, int32_t* d_unv,
+                                void* stream) {
+  if (!ctx) return fail(VRPMS_EINVAL, "vrpms_eval_words: ctx is NULL");
+  if (!ctx->has_instance) return fail(VRPMS_ESTATE, "vrpms_eval_words: no instance loaded");
+  if (C < 0 || n < 0) return fail(VRPMS_EINVAL, "vrpms_eval_words: need C >= 0, n >= 0");
+  if (C == 0) return VRPMS_OK;
+  if (!d_words || !d_keys) return fail(VRPMS_EINVAL, "vrpms_eval_words: d_words/d_keys NULL");
+  const Instance& in = ctx->inst;
+  if (in.N > 256) return fail(VRPMS_EINVAL, "vrpms_eval_words: uint8 tours need N <= 256");
+  VRPMS_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = (hipStream_t)stream;
+  if (words_fast_ok(ctx)) {
+    WordsArgs w{in.pack64p, in.N, in.K, in.pref_lim, in.pref_smask, d_words, C, n,
+                in.objective, d_keys, d_sum, d_max, d_unv};
+    const size_t lds = ((size_t)in.N * in.N * 8 + 15) & ~(size_t)15;
+    const int per_cu = std::max<int>(1, std::min<int>(2, (int)(ctx->max_lds / lds)));
+    const int64_t blocks = (C + 1023) / 1024;
+    const int grid = (int)std::min<int64_t>(blocks, (int64_t)ctx->num_cus * per_cu);
+    const bool ovs = in.max_dem > in.cap0;
+    auto kern = ovs ? eval_cvrp_words<8, true> : eval_cvrp_words<8, false>;
+    allow_lds(kern, lds);
+    kern<<<grid, 1024, lds, s>>>(w);
+    VRPMS_HIP(hipGetLastError());
+    return VRPMS_OK;
+  }
+  EvalArgs a{nullptr, in.N, in.H, in.K, in.dem, in.cap, in.start, d_words, C, n, 0,
+             in.objective, d_keys, d_sum, d_max, d_unv};
+  return launch_generic<uint8_t, true>(ctx, a, s);
+}
+
+extern "C" int vrpms_rows_to_words(vrpms_ctx* ctx, const uint8_t* d_rows, int64_t C, int32_t n,
+                                   int64_t ld, uint32_t* d_words, void* stream) {
+  if (!ctx) return fail(VRPMS_EINVAL, "vrpms_rows_to_words: ctx is NULL");
+  if (C < 0 || n < 0 || ld < n) return fail(VRPMS_EINVAL, "vrpms_rows_to_words: bad shape");
+  if (C == 0 || n == 0) return VRPMS_OK;
+  if (!d_rows || !d_words) return fail(VRPMS_EINVAL, "vrpms_rows_to_words: NULL buffer");
+  VRPMS_HIP(hipSetDevice(ctx->device));
+  const int64_t total = (int64_t)((n + 3) / 4) * C;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, (int64_t)ctx->num_cus * 8));
+  rows_to_words_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(d_rows, C, n, ld, d_words);
+  VRPMS_HIP(hipGetLastError());
+  return VRPMS_OK;
 }
 
 extern "C" int vrpms_decode(vrpms_ctx* ctx, const void* d_perm, int32_t perm_bytes, int32_t n,
