@@ -118,6 +118,17 @@ __global__ void pack_prefix_kernel(const int32_t* __restrict__ D, const int32_t*
   }
 }
 
+// Same layout with the open-route word biased by -lim (mod 2^32), so the
+// words kernel can keep its accumulator biased and test capacity by sign.
+__global__ void bias_hi_kernel(const uint64_t* __restrict__ in, int64_t total, uint32_t lim,
+                               uint64_t* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t e = in[i];
+    out[i] = (e & 0xffffffffull) | ((uint64_t)((uint32_t)(e >> 32) - lim) << 32);
+  }
+}
+
 static int bits_for(int v) {
   int b = 1;
   while (b < 31 && (1 << b) <= v) ++b;
@@ -129,6 +140,7 @@ static void free_instance(Instance& in) {
   (void)hipFree(in.mat16);
   (void)hipFree(in.pack64);
   (void)hipFree(in.pack64p);
+  (void)hipFree(in.pack64w);
   (void)hipFree(in.dem);
   (void)hipFree(in.cap);
   (void)hipFree(in.start);
@@ -295,6 +307,10 @@ int vrpms_set_instance(vrpms_ctx* ctx, int32_t problem, const int32_t* d_dur, in
       in.pref_smask = (uint32_t)(((int64_t)1 << S) - 1);
       VRPMS_HIP(hipMalloc(&in.pack64p, (size_t)N * N * 8));
       pack_prefix_kernel<<<(N * N + 255) / 256, 256, 0, s>>>(in.mat32, in.dem, N, S, in.pack64p);
+      VRPMS_HIP(hipGetLastError());
+      VRPMS_HIP(hipMalloc(&in.pack64w, (size_t)N * N * 8));
+      bias_hi_kernel<<<(N * N + 255) / 256, 256, 0, s>>>(in.pack64p, (int64_t)N * N, in.pref_lim,
+                                                         in.pack64w);
       VRPMS_HIP(hipGetLastError());
     }
   }

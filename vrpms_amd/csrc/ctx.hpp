@@ -32,6 +32,7 @@ struct Instance {
   // "prefix-ret" layout for a uniform fleet (eval_cvrp_packed MODE 1):
   // lo = dem(b) << S + dur(a,b) + ret(b) - ret(a) (mod 2^32), hi = out(b) + ret(b) | dem(b) << S
   uint64_t* pack64p = nullptr;
+  uint64_t* pack64w = nullptr;  // pack64p with hi biased by -lim (eval_cvrp_words)
   int pref_S = 0;
   uint32_t pref_lim = 0, pref_smask = 0;
   int tier = kTierGlobal;

@@ -396,17 +396,27 @@ __global__ __launch_bounds__(BLOCK) void eval_cvrp_packed(PackedArgs a) {
 // from HBM to registers: no LDS tile, the LDS holds only the matrix and a
 // workgroup can be 1024 lanes (16 waves per CU instead of 8).
 //
-// Each lane streams its candidates through an R-deep register ring of tour
-// words.  Every candidate occupies NWP = roundup(nw, R) ring slots (the
-// padding slots load nothing), so ring slot u always holds word w0 + u and
-// every register index is a compile-time constant; refills run across the
-// candidate boundary (the next candidate's first words are in flight while
-// this one finishes).
+// Split arithmetic (prefix-ret layout, uniform fleet, every demand fits an
+// empty vehicle), per customer, branch-free:
+//   t    = acc + lo                     load << S | (cur + ret(prev)) grows
+//   f    = t < lim                      capacity test
+//   rd'  = (acc & smask) | 1 << KS      finished route, vehicle count above KS
+//   dsum += f ? 0 : rd';  dmax = max(dmax, f ? 0 : rd')
+//   acc  = f ? t : (dsum >= K << KS ? DEAD : hi)
+// The vehicle counter lives in dsum's high bits; once it reaches K the
+// accumulator is parked at DEAD = (cap + 2) << S, which never fits again and
+// contributes 0 duration, so every later customer adds exactly one count:
+// unvisited = count - K + 1.  No per-lane flags, no divergent branches.
+//
+// Each lane walks its candidates through an R-deep ring of tour words
+// (R divides the word count when possible, so no slot is wasted); ring slot
+// indices are compile-time constants.
 // ---------------------------------------------------------------------------
 struct WordsArgs {
   const uint64_t* pack;
   int N, K;
   uint32_t lim, smask;
+  uint32_t ks, klim, dead;  // 1 << ks counts vehicles; klim = initial dsum; dead = biased DEAD
   const uint32_t* words;
   int64_t C;
   int n;
@@ -417,7 +427,7 @@ struct WordsArgs {
   int32_t* unv;
 };
 
-template <int R, bool OVS>
+template <int R>
 __global__ __launch_bounds__(1024) void eval_cvrp_words(WordsArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = a.N;
@@ -436,89 +446,99 @@ __global__ __launch_bounds__(1024) void eval_cvrp_words(WordsArgs a) {
     return *reinterpret_cast<const uint64_t*>(Eb + (__umul24(x, N8) + (y << 3)));
   };
   const int64_t C = a.C;
-  const int n = a.n, nw = (n + 3) >> 2, NWP = (nw + R - 1) / R * R;
-  const uint32_t K = (uint32_t)a.K, lim = a.lim, smask = a.smask;
+  const int n = a.n, nw = (n + 3) >> 2, nfull = n >> 2;
+  const uint32_t lim = a.lim, smask = a.smask, kinc = 1u << a.ks, klim = a.klim;
+  const uint32_t deadacc = a.dead, lowmask = kinc - 1u;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (c >= C || n == 0) {
-    for (; c < C; c += stride) {
-      a.keys[c] = 0;
-      if (a.sums) a.sums[c] = 0;
-      if (a.maxs) a.maxs[c] = 0;
-      if (a.unv) a.unv[c] = 0;
-    }
-    return;
-  }
-  const uint32_t* W = a.words;
-  uint32_t ring[R];
-  // slot s of the stream = word (s mod NWP) of candidate c + (s / NWP) * stride
-#pragma unroll
-  for (int u = 0; u < R; ++u) ring[u] = u < nw ? W[(int64_t)u * C + c] : 0u;
 
-  for (; c < C; c += stride) {
-    const int64_t cn = c + stride;
-    uint32_t acc = 0, dsum = 0, dmax = 0, unv = 0, k = 0;
-    bool dead = false;
+  const int nblk = nfull / R;                 // blocks of R full words: the fast loop
+  const int64_t last_off = (int64_t)(nw - 1) * C;
+
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < C; c += stride) {
+    const uint32_t* Wc = a.words + c;
+    uint32_t ring[R];
+    // every load is unconditional (clamped to the last word) so the
+    // compiler can keep counted vmcnt waits instead of draining to 0
+#pragma unroll
+    for (int u = 0; u < R; ++u) ring[u] = Wc[min((int64_t)u * C, last_off)];
+    int64_t nxt = (int64_t)R * C;               // offset of the next word to fetch
+
+    // acc is biased by -lim so "fits" is the sign bit of acc + lo; dsum's
+    // vehicle counter starts at 2^B - K so exhausting the fleet sets bit 31.
+    // Every select below is a bitwise v_bfi on an arithmetic-shift mask:
+    // no lane masks, no VCC hazards, nothing the compiler can turn into a
+    // divergent branch.
+    uint32_t acc = 0u - lim, dsum = klim, dmax = 0;
+    auto bsel = [](uint32_t m, uint32_t x, uint32_t y) { return (x & m) | (y & ~m); };  // v_bfi
+    // sign mask via the bitfield-extract intrinsic: LLVM does not re-form it
+    // into a compare + select the way it does for (int)x >> 31
+    auto sgn = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_sbfe((int)x, 31u, 1u); };
+    auto step = [&](uint64_t e) {
+      const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);  // hi is pre-biased too
+      const uint32_t t = acc + lo;
+      const uint32_t fm = sgn(t);                                 // all ones: fits
+      const uint32_t rdm = bsel(fm, 0u, (acc & smask) | kinc);    // finished route, +1 vehicle
+      dsum += rdm;
+      dmax = max(dmax, rdm);
+      const uint32_t am = sgn(dsum);                              // all ones: fleet exhausted
+      acc = bsel(fm, t, bsel(am, deadacc, hi));
+    };
     uint32_t wd = ring[0];
-    uint32_t c3 = wd >> 24;
+    uint32_t c3 = wd >> 24, lastc = 0;
     uint64_t e0 = gat(0, wd & 0xffu), e1 = gat(wd & 0xffu, (wd >> 8) & 0xffu),
              e2 = gat((wd >> 8) & 0xffu, (wd >> 16) & 0xffu), e3 = gat((wd >> 16) & 0xffu, c3);
-    auto step = [&](uint64_t e) {
-      const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
-      const uint32_t t = acc + lo;
-      const bool f = t < lim || dead;
-      const uint32_t rd = f ? 0u : (acc & smask);
-      dsum += rd;
-      dmax = max(dmax, rd);
-      k += f ? 0u : 1u;
-      const bool die = !f && (k >= K || (OVS && hi >= lim));
-      dead = dead || die;
-      unv += dead ? 1u : 0u;
-      acc = f ? t : hi;
-    };
-    for (int w0 = 0; w0 < NWP; w0 += R) {
+    for (int b = 0; b < nblk; ++b) {
+      // only the last block's refills can run past the tour: clamp them there
+      const int64_t cap_off = b + 1 < nblk ? INT64_MAX : last_off;
 #pragma unroll
       for (int u = 0; u < R; ++u) {
-        const int w = w0 + u;
-        if (w < nw) {
-          // refill this slot with the word R slots ahead in the stream
-          const int wr = w + R;
-          if (wr < nw) ring[u] = W[(int64_t)wr * C + c];
-          else if (wr - NWP >= 0 && wr - NWP < nw && cn < C) ring[u] = W[(int64_t)(wr - NWP) * C + cn];
-          // gathers of the next word, issued before this word's split steps
-          const uint32_t wn = (w + 1 < nw) ? ring[(u + 1) % R] : 0u;
-          const uint32_t n0 = wn & 0xffu, n1 = (wn >> 8) & 0xffu, n2 = (wn >> 16) & 0xffu,
-                         n3 = wn >> 24;
-          const uint64_t f0 = gat(c3, n0), f1 = gat(n0, n1), f2 = gat(n1, n2), f3 = gat(n2, n3);
-          const int pos = 4 * w;
-          step(e0);
-          if (pos + 1 < n) step(e1);
-          if (pos + 2 < n) step(e2);
-          if (pos + 3 < n) step(e3);
-          c3 = n3;
-          e0 = f0;
-          e1 = f1;
-          e2 = f2;
-          e3 = f3;
-        } else {
-          // padding slot: refill with the next candidate's word, if any
-          const int wr = w + R - NWP;
-          if (wr >= 0 && wr < nw && cn < C) ring[u] = W[(int64_t)wr * C + cn];
-        }
+        ring[u] = Wc[min(nxt, cap_off)];  // word w + R
+        nxt += C;
+        // gathers of the next word, issued before this word's split steps
+        const uint32_t wn = ring[(u + 1) % R];
+        const uint32_t n0 = wn & 0xffu, n1 = (wn >> 8) & 0xffu, n2 = (wn >> 16) & 0xffu,
+                       n3 = wn >> 24;
+        const uint64_t f0 = gat(c3, n0), f1 = gat(n0, n1), f2 = gat(n1, n2), f3 = gat(n2, n3);
+        step(e0);
+        step(e1);
+        step(e2);
+        step(e3);
+        lastc = c3;  // last customer of the word just processed
+        c3 = n3;
+        e0 = f0;
+        e1 = f1;
+        e2 = f2;
+        e3 = f3;
       }
     }
-    if (!dead) {
-      const uint32_t rd = acc & smask;
-      dsum += rd;
-      dmax = max(dmax, rd);
+    // ragged tail (n not a multiple of 4R): plain per-word loads and gathers
+    uint32_t prev = lastc;  // last customer of the fast loop (depot if it ran no block)
+    for (int w = nblk * R; w < nw; ++w) {
+      const uint32_t x = Wc[(int64_t)w * C];
+      const int rem = min(4, n - 4 * w);
+      for (int q = 0; q < rem; ++q) {
+        const uint32_t cq = (x >> (8 * q)) & 0xffu;
+        step(gat(prev, cq));
+        prev = cq;
+      }
     }
-    a.keys[c] = cvrp_key(unv, dsum, dmax, a.objective);
-    if (a.sums) a.sums[c] = (int32_t)dsum;
-    if (a.maxs) a.maxs[c] = (int32_t)dmax;
+    const bool dead = (int32_t)dsum < 0;
+    const uint32_t count = (dsum >> a.ks) - (klim >> a.ks);  // vehicles closed (+ dead steps)
+    uint32_t s = dsum & lowmask, m = dmax >= kinc ? dmax - kinc : 0u;
+    uint32_t unv = 0;
+    if (dead) {
+      unv = count - (uint32_t)a.K + 1u;
+    } else if (n > 0) {
+      const uint32_t rd = acc & smask;  // close the last route
+      s += rd;
+      m = max(m, rd);
+    }
+    a.keys[c] = cvrp_key(unv, s, m, a.objective);
+    if (a.sums) a.sums[c] = (int32_t)s;
+    if (a.maxs) a.maxs[c] = (int32_t)m;
     if (a.unv) a.unv[c] = (int32_t)unv;
   }
 }
-
 // rows (uint8 [C][ld]) -> words (uint32 [ceil(n/4)][C]); one lane per (word, candidate)
 __global__ void rows_to_words_kernel(const uint8_t* __restrict__ rows, int64_t C, int n,
                                      int64_t ld, uint32_t* __restrict__ words) {
@@ -864,17 +884,42 @@ extern "C" int vrpms_eval_words(vrpms_ctx* ctx, const uint32_t* d_words, int64_t
   if (in.N > 256) return fail(VRPMS_EINVAL, "vrpms_eval_words: uint8 tours need N <= 256");
   VRPMS_HIP(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
-  if (words_fast_ok(ctx)) {
-    WordsArgs w{in.pack64p, in.N, in.K, in.pref_lim, in.pref_smask, d_words, C, n,
-                in.objective, d_keys, d_sum, d_max, d_unv};
+  // fast path conditions: every demand fits an empty vehicle, the vehicle
+  // counter fits above the duration sum in dsum, DEAD stays below 2^32
+  const int64_t sum_bound = (int64_t)(n + in.K + 1) * std::max(in.max_dur, 1);
+  int ks = 1;
+  while (ks < 31 && ((int64_t)1 << ks) <= sum_bound) ++ks;
+  const int B = 31 - ks;  // width of dsum's vehicle counter (bit 31 = exhausted)
+  const bool fits = words_fast_ok(ctx) && in.pack64w && in.max_dem <= in.cap0 && B >= 1 &&
+                    ((int64_t)1 << B) > std::max<int64_t>(in.K, n) &&
+                    (((int64_t)in.cap0 + in.max_dem + 3) << in.pref_S) <= ((int64_t)1 << 31);
+  if (fits) {
+    const uint32_t dsum0 = (uint32_t)((((int64_t)1 << B) - in.K) << ks);
+    WordsArgs w{in.pack64w, in.N, in.K, in.pref_lim, in.pref_smask, (uint32_t)ks, dsum0,
+                (uint32_t)1u << in.pref_S, d_words, C, n, in.objective, d_keys, d_sum, d_max,
+                d_unv};
     const size_t lds = ((size_t)in.N * in.N * 8 + 15) & ~(size_t)15;
     const int per_cu = std::max<int>(1, std::min<int>(2, (int)(ctx->max_lds / lds)));
     const int64_t blocks = (C + 1023) / 1024;
     const int grid = (int)std::min<int64_t>(blocks, (int64_t)ctx->num_cus * per_cu);
-    const bool ovs = in.max_dem > in.cap0;
-    auto kern = ovs ? eval_cvrp_words<8, true> : eval_cvrp_words<8, false>;
-    allow_lds(kern, lds);
-    kern<<<grid, 1024, lds, s>>>(w);
+    // ring depth: the R in [4, 8] that wastes the fewest slots on ceil(n/4) words
+    const int nw = (n + 3) / 4;
+    int R = 8, waste = 1 << 30;
+    for (int r = 8; r >= 4; --r) {
+      const int wst = (nw + r - 1) / r * r - nw;
+      if (wst < waste) { waste = wst; R = r; }
+    }
+    auto go = [&](auto kern) {
+      allow_lds(kern, lds);
+      kern<<<grid, 1024, lds, s>>>(w);
+    };
+    switch (R) {
+      case 4: go(eval_cvrp_words<4>); break;
+      case 5: go(eval_cvrp_words<5>); break;
+      case 6: go(eval_cvrp_words<6>); break;
+      case 7: go(eval_cvrp_words<7>); break;
+      default: go(eval_cvrp_words<8>); break;
+    }
     VRPMS_HIP(hipGetLastError());
     return VRPMS_OK;
   }
