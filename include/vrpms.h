@@ -120,6 +120,82 @@ int vrpms_decode(vrpms_ctx* ctx, const void* d_perm, int32_t perm_bytes, int32_t
 int vrpms_argmin(vrpms_ctx* ctx, const uint64_t* d_keys, int64_t C, uint64_t* d_out,
                  void* stream);
 
+/* ------------------------------------------------------------------------
+ * Search kernels: the algorithms behind api/{tsp,vrp}/{sa,ga,aco,bf}/index.py
+ * (each stops at `# TODO: Run algorithm` in the reference).  Tours here are
+ * uint16 rows [..][n] (n = N - 1 customers).  Every random choice is
+ * Philox4x32-10 keyed by `seed` with counters (step/generation/iteration,
+ * chain/island/ant, lane/stream), so oracle/spec.py replays them exactly.
+ * ---------------------------------------------------------------------- */
+
+/* Simulated annealing (api/{tsp,vrp}/sa/index.py; knobs: api/parameters.py:26-27
+ * declares none, so the front-end supplies defaults).  One wavefront per
+ * chain: every step the 64 lanes score 64 Philox-sampled moves (swap /
+ * 2-opt / relocate) of the chain's tour, the best (key, lane) is accepted if
+ * it is no worse or if (u >> 8) < floor(2^24 exp(-dp * invT)); invT is
+ * multiplied by inv_alpha after every step (geometric cooling). */
+typedef struct {
+  int32_t chains;   /* one wavefront each */
+  int32_t steps;    /* steps in this call */
+  float inv_t0;     /* 1 / temperature at the first step of this call */
+  float inv_alpha;  /* per-step factor on 1/T (1/alpha for T *= alpha) */
+  uint64_t seed;
+  uint64_t step0;   /* global index of the first step (Philox counter) */
+} vrpms_sa_params;
+
+/* d_cur [chains][n] in/out (cur_key out); d_best/d_best_key in/out (set
+ * d_best_key to UINT64_MAX before the first call). */
+int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* d_cur, uint64_t* d_cur_key,
+                 uint16_t* d_best, uint64_t* d_best_key, int32_t n, void* stream);
+
+/* Genetic algorithm (api/vrp/ga/index.py; randomPermutationCount -> pop,
+ * iterationCount -> generations, api/parameters.py:18-23).  Per generation:
+ * binary tournaments, OX1 crossover, Philox-gated mutation (one move),
+ * batched scoring, (mu + lambda) survivors per island. */
+typedef struct {
+  int32_t islands;
+  int32_t pop;          /* 2..4096 */
+  int32_t generations;  /* generations in this call */
+  uint32_t pmut;        /* mutate iff a Philox word < pmut (pmut/2^32 = probability) */
+  uint64_t seed;
+  uint64_t gen0;        /* global index of the first generation */
+} vrpms_ga_params;
+
+/* d_pop [islands][pop][n] and d_keys [islands][pop] in/out (keys must
+ * score d_pop on entry, e.g. by vrpms_eval). */
+int vrpms_ga_generation(vrpms_ctx* ctx, const vrpms_ga_params* p, uint16_t* d_pop,
+                        uint64_t* d_keys, int32_t n, void* stream);
+
+/* Ant colony (api/{tsp,vrp}/aco/index.py), integer pheromone so every
+ * update is exact and order-independent: w_ij = (tau_ij >> 8) * eta_ij,
+ * eta_ij = floor(2^24 / (1 + D_ij)^2); tau <- clamp(tau - tau >> evap_shift);
+ * the iteration-best ant deposits floor(2^30 / (1 + primary)) per edge. */
+typedef struct {
+  int32_t colonies;
+  int32_t ants;        /* per colony, one wavefront each */
+  int32_t evap_shift;  /* rho = 2^-evap_shift */
+  uint32_t tau_min, tau_max;  /* tau_max <= 2^31 */
+  uint64_t seed;
+  uint64_t iter;       /* global iteration index (Philox counter) */
+} vrpms_aco_params;
+
+/* d_tau [colonies][N][N] <- tau0, d_eta [N][N] <- floor(2^24 / (1 + D)^2). */
+int vrpms_aco_init(vrpms_ctx* ctx, int32_t colonies, uint32_t tau0, uint32_t* d_tau,
+                   uint32_t* d_eta, void* stream);
+
+/* One iteration: construct d_tours [colonies][ants][n] (n = N - 1), score
+ * them into d_keys, d_iter_best [colonies][2] = (key, ant), update tau. */
+int vrpms_aco_iteration(vrpms_ctx* ctx, const vrpms_aco_params* p, uint32_t* d_tau,
+                        const uint32_t* d_eta, uint16_t* d_tours, uint64_t* d_keys,
+                        uint64_t* d_iter_best, int32_t n, void* stream);
+
+/* Brute force (api/{tsp,vrp}/bf/index.py): lexicographic ranks
+ * [rank_begin, rank_end) of the permutations of customers 1..n (n <= 15);
+ * d_out[0] = min key, d_out[1] = smallest rank holding it (UINT64_MAX if
+ * the range is empty).  Multi-GPU: disjoint rank ranges + a min. */
+int vrpms_bf_run(vrpms_ctx* ctx, int32_t n, uint64_t rank_begin, uint64_t rank_end,
+                 uint64_t* d_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

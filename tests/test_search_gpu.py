@@ -1,0 +1,189 @@
+"""GPU parity of the search kernels against the CPU replay (oracle/search.py).
+
+Small instances: the whole trajectory must match exactly (tours, keys,
+best-so-far, pheromone matrices), because every random choice is a Philox
+word both sides compute and every cost is integer.  Larger instances: the
+invariants (tours stay permutations, reported keys == vrpms_eval of the
+reported tours, search improves on its start).
+"""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import search, spec
+from vrpms_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def torch_():
+    import torch
+    return torch
+
+
+def load(ctx, inst, objective=0):
+    from vrpms_amd.core import CVRP, TSP
+    if inst.problem == "tsp":
+        ctx.set_instance(TSP, inst.durations, start_times=inst.start_times, objective=objective)
+    else:
+        ctx.set_instance(CVRP, inst.durations, inst.demand, inst.capacities, inst.start_times,
+                         objective=objective)
+
+
+def scorer(inst, objective=0):
+    return search.Scorer(inst.durations, inst.demand, inst.capacities, inst.start_times,
+                         inst.problem, objective)
+
+
+def u64(t):
+    return [int(x) for x in t.cpu().numpy().view(np.uint64).reshape(-1)]
+
+
+SMALL = [
+    ("cvrp", lambda: synth.cvrp(12, 3, seed=1, slack=0.95)),
+    ("tsp", lambda: synth.Instance("tsp11", synth.tsp20(2).durations[:, :11, :11], None, None,
+                                   np.array([0]), "tsp")),
+    ("td", lambda: synth.td_cvrp(10, 2, seed=4)),
+]
+
+
+@pytest.mark.parametrize("name,maker", SMALL, ids=[s[0] for s in SMALL])
+def test_sa_trajectory_matches_oracle(ctx, name, maker):
+    torch = torch_()
+    inst = maker()
+    load(ctx, inst)
+    chains, n = 3, inst.n
+    P = synth.random_perms(chains, n, seed=7).astype(np.int16)
+    cur = torch.from_numpy(P).to(ctx.dev)
+    best = cur.clone()
+    ck = torch.empty(chains, dtype=torch.int64, device=ctx.dev)
+    bk = torch.full((chains,), -1, dtype=torch.int64, device=ctx.dev)   # UINT64_MAX
+    seed, inv_t0, inv_alpha = 12345, 1.0 / 200.0, 1.0 / 0.97
+    ctx.sa_run(cur, ck, best, bk, steps=20, inv_t0=inv_t0, inv_alpha=inv_alpha, seed=seed, step0=0)
+    ref = search.sa_run(scorer(inst), P.tolist(), P.tolist(), [2**64 - 1] * chains, seed, 0, 20,
+                        inv_t0, inv_alpha)
+    assert cur.cpu().numpy().tolist() == ref[0]
+    assert u64(ck) == ref[1]
+    assert best.cpu().numpy().tolist() == ref[2]
+    assert u64(bk) == ref[3]
+    # a second call continues the same streams (step0 = 20)
+    inv_t1 = np.float32(inv_t0)
+    for _ in range(20):
+        inv_t1 = np.float32(inv_t1 * np.float32(inv_alpha))
+    ctx.sa_run(cur, ck, best, bk, steps=10, inv_t0=float(inv_t1), inv_alpha=inv_alpha, seed=seed,
+               step0=20)
+    ref2 = search.sa_run(scorer(inst), ref[0], ref[2], ref[3], seed, 20, 10, float(inv_t1),
+                         inv_alpha)
+    assert cur.cpu().numpy().tolist() == ref2[0]
+    assert u64(bk) == ref2[3]
+
+
+def test_sa_large_invariants(ctx):
+    torch = torch_()
+    inst = synth.cvrp(100, 8, seed=0)
+    load(ctx, inst)
+    chains, n = 64, inst.n
+    P = synth.random_perms(chains, n, seed=3).astype(np.int16)
+    cur = torch.from_numpy(P).to(ctx.dev)
+    best = cur.clone()
+    ck = torch.empty(chains, dtype=torch.int64, device=ctx.dev)
+    bk = torch.full((chains,), -1, dtype=torch.int64, device=ctx.dev)
+    start = ctx.eval(cur, with_parts=False)
+    ctx.sa_run(cur, ck, best, bk, steps=300, inv_t0=1 / 50.0, inv_alpha=1 / 0.99, seed=1, step0=0)
+    B = best.cpu().numpy()
+    assert all(sorted(r) == list(range(1, n + 1)) for r in B)
+    assert u64(ctx.eval(best)) == u64(bk)
+    assert u64(ctx.eval(cur)) == u64(ck)
+    assert np.mean(u64(bk)) < 0.6 * np.mean(u64(start))
+
+
+@pytest.mark.parametrize("name,maker", SMALL[:2], ids=[s[0] for s in SMALL[:2]])
+def test_ga_generations_match_oracle(ctx, name, maker):
+    torch = torch_()
+    inst = maker()
+    load(ctx, inst)
+    islands, pop, n = 2, 16, inst.n
+    P = synth.random_perms(islands * pop, n, seed=5).astype(np.int16)
+    dpop = torch.from_numpy(P.reshape(islands, pop, n).copy()).to(ctx.dev)
+    keys = ctx.eval(dpop.view(islands * pop, n)).view(islands, pop)
+    sc = scorer(inst)
+    rpop = [[list(r) for r in P.reshape(islands, pop, n)[i]] for i in range(islands)]
+    rkeys = [[sc(t) for t in rpop[i]] for i in range(islands)]
+    assert u64(keys) == [k for ks in rkeys for k in ks]
+    seed, pmut = 99, 0.3
+    pm = min(int(round(pmut * 2**32)), 2**32 - 1)
+    for g in range(3):
+        rpop, rkeys = search.ga_generation(sc, rpop, rkeys, seed, g, pm)
+    ctx.ga_generation(dpop, keys, generations=3, pmut=pmut, seed=seed, gen0=0)
+    assert dpop.cpu().numpy().tolist() == rpop
+    assert u64(keys) == [k for ks in rkeys for k in ks]
+
+
+def test_ga_large_invariants(ctx):
+    torch = torch_()
+    inst = synth.cvrp(100, 8, seed=0)
+    load(ctx, inst)
+    islands, pop, n = 4, 128, inst.n
+    P = synth.random_perms(islands * pop, n, seed=8).astype(np.int16)
+    dpop = torch.from_numpy(P.reshape(islands, pop, n).copy()).to(ctx.dev)
+    keys = ctx.eval(dpop.view(-1, n)).view(islands, pop)
+    k0 = min(u64(keys))
+    ctx.ga_generation(dpop, keys, generations=30, pmut=0.2, seed=3, gen0=0)
+    flat = dpop.view(-1, n)
+    assert all(sorted(r) == list(range(1, n + 1)) for r in flat.cpu().numpy())
+    assert u64(ctx.eval(flat)) == u64(keys)
+    assert min(u64(keys)) < k0
+    ks = np.array(u64(keys), dtype=np.uint64).reshape(islands, pop)
+    assert (np.diff(ks.astype(np.float64), axis=1) >= 0).all()     # survivors sorted
+
+
+@pytest.mark.parametrize("name,maker", SMALL[:2], ids=[s[0] for s in SMALL[:2]])
+def test_aco_iterations_match_oracle(ctx, name, maker):
+    inst = maker()
+    load(ctx, inst)
+    colonies, ants, tau0 = 2, 8, 1 << 20
+    tau, eta = ctx.aco_init(colonies, tau0)
+    ref_eta = search.aco_eta(inst.durations[0])
+    assert (eta.cpu().numpy().astype(np.int64) & 0xFFFFFFFF).tolist() == ref_eta.tolist()
+    rtau = [np.full((inst.N, inst.N), tau0, dtype=np.int64) for _ in range(colonies)]
+    sc = scorer(inst)
+    for it in range(3):
+        tours, keys, ib = ctx.aco_iteration(tau, eta, ants, seed=7, it=it, evap_shift=3,
+                                            tau_min=1 << 10, tau_max=1 << 30)
+        rt, rk, rib = search.aco_iteration(sc, rtau, ref_eta, ants, inst.n, 7, it, 3, 1 << 10,
+                                           1 << 30)
+        assert tours.cpu().numpy().tolist() == rt
+        assert u64(keys) == [k for ks in rk for k in ks]
+        assert [(a & (2**64 - 1), b) for a, b in ib.cpu().tolist()] == rib
+        got_tau = tau.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+        assert all((got_tau[c] == rtau[c]).all() for c in range(colonies))
+
+
+@pytest.mark.parametrize("name,maker", SMALL, ids=[s[0] for s in SMALL])
+def test_bf_matches_oracle(ctx, name, maker):
+    inst = maker()
+    load(ctx, inst)
+    n = 7
+    sub = synth.Instance(inst.name, inst.durations[:, : n + 1, : n + 1],
+                         None if inst.demand is None else inst.demand[: n + 1],
+                         inst.capacities, inst.start_times, inst.problem)
+    load(ctx, sub)
+    best = ctx.bf_run(n, 0, math.factorial(n))
+    assert best == search.bf(scorer(sub), n)
+    # disjoint rank ranges (the multi-GPU split) reduce to the same optimum
+    parts = [ctx.bf_run(n, a, b) for a, b in [(0, 1000), (1000, 3333), (3333, 5040)]]
+    assert min(parts) == best
+    # the reported rank decodes to a tour with the reported key
+    tour = search.unrank(best[1], n)
+    assert scorer(sub)(tour) == best[0]
+
+
+def test_bf_n10_optimum_le_every_sampled_tour(ctx, coracle):
+    inst = synth.cvrp(10, 3, seed=9)
+    load(ctx, inst)
+    k, r = ctx.bf_run(10, 0, math.factorial(10))
+    P = synth.random_perms(20000, 10, seed=1)
+    keys = coracle.eval_batch(inst.durations, P, inst.demand, inst.capacities, inst.start_times)[0]
+    assert k <= int(keys.min())
+    assert scorer(inst)(search.unrank(r, 10)) == k

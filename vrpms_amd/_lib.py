@@ -34,6 +34,22 @@ _i32 = _c.c_int32
 _i64 = _c.c_int64
 _u64 = _c.c_uint64
 
+class SaParams(ctypes.Structure):
+    _fields_ = [("chains", _i32), ("steps", _i32), ("inv_t0", ctypes.c_float),
+                ("inv_alpha", ctypes.c_float), ("seed", _u64), ("step0", _u64)]
+
+
+class GaParams(ctypes.Structure):
+    _fields_ = [("islands", _i32), ("pop", _i32), ("generations", _i32),
+                ("pmut", ctypes.c_uint32), ("seed", _u64), ("gen0", _u64)]
+
+
+class AcoParams(ctypes.Structure):
+    _fields_ = [("colonies", _i32), ("ants", _i32), ("evap_shift", _i32),
+                ("tau_min", ctypes.c_uint32), ("tau_max", ctypes.c_uint32), ("seed", _u64),
+                ("iter", _u64)]
+
+
 # name -> (restype, argtypes); mirrors include/vrpms.h one-for-one.
 SIGNATURES = {
     "vrpms_version": (_c.c_int, []),
@@ -48,6 +64,12 @@ SIGNATURES = {
     "vrpms_set_option": (_c.c_int, [_vp, _i32, _i32]),
     "vrpms_decode": (_c.c_int, [_vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "vrpms_argmin": (_c.c_int, [_vp, _vp, _i64, _vp, _vp]),
+    "vrpms_sa_run": (_c.c_int, [_vp, _c.POINTER(SaParams), _vp, _vp, _vp, _vp, _i32, _vp]),
+    "vrpms_ga_generation": (_c.c_int, [_vp, _c.POINTER(GaParams), _vp, _vp, _i32, _vp]),
+    "vrpms_aco_init": (_c.c_int, [_vp, _i32, _c.c_uint32, _vp, _vp, _vp]),
+    "vrpms_aco_iteration": (_c.c_int, [_vp, _c.POINTER(AcoParams), _vp, _vp, _vp, _vp, _vp,
+                                       _i32, _vp]),
+    "vrpms_bf_run": (_c.c_int, [_vp, _i32, _u64, _u64, _vp, _vp]),
 }
 
 

@@ -190,6 +190,58 @@ class Context:
         return k & ((1 << 64) - 1), i
 
 
+    # -- search kernels (state lives in caller-owned device tensors) ----------
+    def sa_run(self, cur, cur_key, best, best_key, steps: int, inv_t0: float, inv_alpha: float,
+               seed: int, step0: int):
+        """Advance every chain (rows of the int16 [chains][n] tensor ``cur``)."""
+        chains, n = cur.shape
+        p = _lib.SaParams(chains, int(steps), float(inv_t0), float(inv_alpha),
+                          int(seed) & (2**64 - 1), int(step0))
+        check(self.lib.vrpms_sa_run(self._ctx, ctypes.byref(p), cur.data_ptr(),
+                                    cur_key.data_ptr(), best.data_ptr(), best_key.data_ptr(), n,
+                                    self.stream()))
+
+    def ga_generation(self, pop, keys, generations: int, pmut: float, seed: int, gen0: int):
+        """pop int16 [islands][P][n], keys int64 [islands][P] (must score pop)."""
+        islands, P, n = pop.shape
+        pm = min(int(round(float(pmut) * 2**32)), 2**32 - 1)
+        p = _lib.GaParams(islands, P, int(generations), pm, int(seed) & (2**64 - 1), int(gen0))
+        check(self.lib.vrpms_ga_generation(self._ctx, ctypes.byref(p), pop.data_ptr(),
+                                           keys.data_ptr(), n, self.stream()))
+
+    def aco_init(self, colonies: int, tau0: int):
+        torch = _torch()
+        tau = torch.empty((colonies, self.N, self.N), dtype=torch.int32, device=self.dev)
+        eta = torch.empty((self.N, self.N), dtype=torch.int32, device=self.dev)
+        check(self.lib.vrpms_aco_init(self._ctx, colonies, int(tau0), tau.data_ptr(),
+                                      eta.data_ptr(), self.stream()))
+        return tau, eta
+
+    def aco_iteration(self, tau, eta, ants: int, seed: int, it: int, evap_shift: int = 3,
+                      tau_min: int = 1 << 10, tau_max: int = 1 << 30):
+        torch = _torch()
+        colonies = tau.shape[0]
+        n = self.N - 1
+        tours = torch.empty((colonies, ants, n), dtype=torch.int16, device=self.dev)
+        keys = torch.empty((colonies, ants), dtype=torch.int64, device=self.dev)
+        ib = torch.empty((colonies, 2), dtype=torch.int64, device=self.dev)
+        p = _lib.AcoParams(colonies, ants, evap_shift, tau_min, tau_max,
+                           int(seed) & (2**64 - 1), int(it))
+        check(self.lib.vrpms_aco_iteration(self._ctx, ctypes.byref(p), tau.data_ptr(),
+                                           eta.data_ptr(), tours.data_ptr(), keys.data_ptr(),
+                                           ib.data_ptr(), n, self.stream()))
+        return tours, keys, ib
+
+    def bf_run(self, n: int, rank_begin: int, rank_end: int):
+        """(min key, smallest lexicographic rank) over ranks [begin, end)."""
+        torch = _torch()
+        out = torch.empty(2, dtype=torch.int64, device=self.dev)
+        check(self.lib.vrpms_bf_run(self._ctx, int(n), int(rank_begin), int(rank_end),
+                                    out.data_ptr(), self.stream()))
+        k, r = out.cpu().tolist()
+        return k & (2**64 - 1), r & (2**64 - 1)
+
+
 def keys_to_u64(keys) -> np.ndarray:
     """int64 tensor of A8 keys -> numpy uint64 (bit-identical view)."""
     return keys.cpu().numpy().view(np.uint64)

@@ -188,6 +188,7 @@ int vrpms_ctx_destroy(vrpms_ctx* ctx) {
   free_instance(ctx->inst);
   (void)hipFree(ctx->d_stats);
   (void)hipFree(ctx->d_scratch);
+  (void)hipFree(ctx->search_scratch);
   delete ctx;
   return VRPMS_OK;
 }

@@ -50,6 +50,8 @@ struct vrpms_ctx {
   int opt_split_mode = 0;       // VRPMS_OPT_SPLIT_MODE (0 auto, 2 force branchy)
   int32_t* d_stats = nullptr;   // scratch for set_instance validation
   uint64_t* d_scratch = nullptr;  // small reduction scratch
+  void* search_scratch = nullptr;  // GA children / BF block results (grown on demand)
+  size_t search_scratch_bytes = 0;
 };
 
 namespace vrpms {

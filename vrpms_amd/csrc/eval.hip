@@ -23,6 +23,7 @@
 
 #include "common.hpp"
 #include "ctx.hpp"
+#include "tour.hpp"
 
 namespace vrpms {
 
@@ -43,29 +44,15 @@ struct EvalArgs {
   int32_t* unv;
 };
 
-// A3: hour slice of an edge departing at minute t.  HM = 1 static,
-// HM = 24 hour-indexed (constant divisor), HM = 0 runtime H.
-template <int HM>
-VRPMS_DEV uint32_t hour_of(int t, int H) {
-  if constexpr (HM == 1) {
-    return 0;
-  } else if constexpr (HM == 24) {
-    return ((uint32_t)t / 60u) % 24u;
-  } else {
-    return ((uint32_t)t / 60u) % (uint32_t)H;
-  }
-}
-
-VRPMS_DEV void write_out(const EvalArgs& a, int64_t c, uint64_t key, int32_t s, int32_t m,
-                         int32_t u) {
-  a.keys[c] = key;
-  if (a.sums) a.sums[c] = s;
-  if (a.maxs) a.maxs[c] = m;
-  if (a.unv) a.unv[c] = u;
+VRPMS_DEV void write_out(const EvalArgs& a, int64_t c, const TourCost& r) {
+  a.keys[c] = r.key;
+  if (a.sums) a.sums[c] = r.sum;
+  if (a.maxs) a.maxs[c] = r.max;
+  if (a.unv) a.unv[c] = r.unv;
 }
 
 // ---------------------------------------------------------------------------
-// Generic lane-per-candidate evaluation (any tier / H / perm width).
+// Generic lane-per-candidate evaluation (any tier / H / perm width / layout).
 // ---------------------------------------------------------------------------
 // Tour element i of candidate c in either layout.
 template <typename PermT, bool WORDS>
@@ -73,88 +60,38 @@ struct TourAccess {
   const PermT* row;
   const uint32_t* w;
   int64_t C, c;
-  VRPMS_DEV uint32_t operator[](int i) const {
+  VRPMS_DEV uint32_t operator()(int i) const {
     if constexpr (WORDS) return (w[(int64_t)(i >> 2) * C + c] >> (8 * (i & 3))) & 0xffu;
     else return (uint32_t)row[i];
   }
 };
 
+// Copy `bytes` (a multiple of 2) from global to LDS with dword moves.
+VRPMS_DEV void stage_to_lds(unsigned char* dst, const void* src, uint32_t bytes) {
+  const uint32_t* s = static_cast<const uint32_t*>(src);
+  uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+  for (uint32_t i = threadIdx.x; i < bytes / 4; i += blockDim.x) d[i] = s[i];
+  if ((bytes & 2u) && threadIdx.x == 0)
+    reinterpret_cast<uint16_t*>(dst)[bytes / 2 - 1] = static_cast<const uint16_t*>(src)[bytes / 2 - 1];
+}
+
 template <typename MatT, bool LDS, bool CVRP, int HM, typename PermT, bool WORDS = false>
 __global__ __launch_bounds__(256) void eval_generic(EvalArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int N = a.N;
-  const uint32_t NN = (uint32_t)N * (uint32_t)N;
+  const uint32_t NN = (uint32_t)a.N * (uint32_t)a.N;
   const MatT* M = static_cast<const MatT*>(a.mat);
   if constexpr (LDS) {
-    const uint32_t bytes = NN * (uint32_t)a.H * sizeof(MatT);
-    const uint32_t words = bytes / 4;
-    const uint32_t* src = static_cast<const uint32_t*>(a.mat);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(smem);
-    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) dst[i] = src[i];
-    if ((bytes & 2u) && threadIdx.x == 0)
-      reinterpret_cast<uint16_t*>(smem)[bytes / 2 - 1] =
-          static_cast<const uint16_t*>(a.mat)[bytes / 2 - 1];
+    stage_to_lds(smem, a.mat, NN * (uint32_t)a.H * sizeof(MatT));
     __syncthreads();
     M = reinterpret_cast<const MatT*>(smem);
   }
+  const MatView<MatT, HM> D{M, (uint32_t)a.N, NN, a.H};
+  const SplitParams sp{a.dem, a.cap, a.start, a.K, a.objective};
   const PermT* P = static_cast<const PermT*>(a.perms);
-  const uint32_t Nm1 = (uint32_t)N - 1;
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < a.C;
        c += (int64_t)gridDim.x * blockDim.x) {
-    const TourAccess<PermT, WORDS> row{P + c * a.ld, static_cast<const uint32_t*>(a.perms), a.C, c};
-    if constexpr (!CVRP) {
-      const int t0 = a.start[0];
-      int t = t0;
-      uint32_t prev = 0;
-      for (int i = 0; i < a.n; ++i) {
-        const uint32_t cc = min((uint32_t)row[i], Nm1);
-        t += (int)M[hour_of<HM>(t, a.H) * NN + prev * N + cc];
-        prev = cc;
-      }
-      t += (int)M[hour_of<HM>(t, a.H) * NN + prev * N];
-      const int d = t - t0;
-      write_out(a, c, pack_key(0, (uint32_t)d, 0), d, d, 0);
-    } else {
-      const int K = a.K;
-      int k = 0, load = 0, t = a.start[0], capk = a.cap[0];
-      uint32_t prev = 0, unv = 0, dsum = 0, dmax = 0;
-      for (int i = 0; i < a.n; ++i) {
-        const uint32_t cc = min((uint32_t)row[i], Nm1);
-        const int dc = a.dem[cc];
-        if (k < K && load + dc > capk) {
-          do {
-            if (prev) {
-              t += (int)M[hour_of<HM>(t, a.H) * NN + prev * N];
-              const uint32_t rd = (uint32_t)(t - a.start[k]);
-              dsum += rd;
-              dmax = max(dmax, rd);
-            }
-            ++k;
-            if (k < K) {
-              load = 0;
-              t = a.start[k];
-              prev = 0;
-              capk = a.cap[k];
-            }
-          } while (k < K && load + dc > capk);
-        }
-        if (k < K) {
-          t += (int)M[hour_of<HM>(t, a.H) * NN + prev * N + cc];
-          load += dc;
-          prev = cc;
-        } else {
-          ++unv;
-        }
-      }
-      if (k < K && prev) {
-        t += (int)M[hour_of<HM>(t, a.H) * NN + prev * N];
-        const uint32_t rd = (uint32_t)(t - a.start[k]);
-        dsum += rd;
-        dmax = max(dmax, rd);
-      }
-      write_out(a, c, cvrp_key(unv, dsum, dmax, a.objective), (int32_t)dsum, (int32_t)dmax,
-                (int32_t)unv);
-    }
+    const TourAccess<PermT, WORDS> tour{P + c * a.ld, static_cast<const uint32_t*>(a.perms), a.C, c};
+    write_out(a, c, eval_tour<CVRP>(D, sp, tour, a.n));
   }
 }
 

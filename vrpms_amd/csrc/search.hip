@@ -1,0 +1,850 @@
+// The neighbourhood / search half of the vrpms hot path: the algorithms the
+// reference exposes as endpoints (api/{tsp,vrp}/{sa,ga,aco,bf}/index.py) but
+// never implements (each stops at `# TODO: Run algorithm`).  Every random
+// choice comes from Philox4x32-10 keyed by (seed) with counters naming
+// (step/generation, chain/island/child, lane, stream), so oracle/spec.py
+// replays the exact same trajectory on the CPU; every tour is scored by
+// eval_tour (tour.hpp), the same arithmetic vrpms_eval uses.
+//
+//   sa_kernel           one wavefront per SA chain; each step the 64 lanes
+//                       score 64 sampled moves of the chain's tour (LDS),
+//                       a wave argmin picks the best, Metropolis accepts.
+//   ga_breed_kernel     one wavefront per child: tournament selection,
+//                       wave-parallel OX crossover (ballot + popcount
+//                       compaction), Philox-gated mutation.
+//   ga_select_kernel    one workgroup per island: (mu + lambda) survivors by
+//                       a bitonic sort of (key, index) in LDS.
+//   aco_construct_kernel  one wavefront per ant: integer roulette over
+//                       tau * eta with a wave prefix scan (exact, so the
+//                       choice is order-independent and reproducible).
+//   aco_update_kernel   integer evaporation + iteration-best deposit.
+//   bf_kernel           lexicographic rank ranges of nibble-packed tours.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <vector>
+
+#include "common.hpp"
+#include "ctx.hpp"
+#include "tour.hpp"
+
+namespace vrpms {
+
+VRPMS_DEV void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+VRPMS_DEV int lane_id() { return (int)(threadIdx.x & 63u); }
+
+// Instance staged for a search kernel: matrix in LDS when it fits, else L2.
+struct SearchInst {
+  const void* mat;   // u16 or i32 [H][N][N] (global)
+  int N, H, K, problem, objective;
+  const int32_t* dem;
+  const int32_t* cap;
+  const int32_t* start;
+  int mat_lds;       // 1: stage the matrix into LDS
+  uint32_t mat_bytes;
+};
+
+static SearchInst search_inst(const vrpms_ctx* ctx) {
+  const Instance& in = ctx->inst;
+  SearchInst s;
+  s.mat = in.use16 ? static_cast<const void*>(in.mat16) : static_cast<const void*>(in.mat32);
+  s.N = in.N;
+  s.H = in.H;
+  s.K = in.K;
+  s.problem = in.problem;
+  s.objective = in.objective;
+  s.dem = in.dem;
+  s.cap = in.cap;
+  s.start = in.start;
+  s.mat_bytes = (uint32_t)((size_t)in.H * in.N * in.N * (in.use16 ? 2 : 4));
+  s.mat_lds = s.mat_bytes <= 64 * 1024 ? 1 : 0;
+  return s;
+}
+
+// LDS carve for the instance part: [matrix][dem N][cap K][start K], 16-B aligned.
+VRPMS_DEV uint32_t inst_lds_bytes(const SearchInst& si) {
+  const uint32_t m = si.mat_lds ? ((si.mat_bytes + 15u) & ~15u) : 0u;
+  return m + (((uint32_t)(si.N + 2 * si.K) * 4u + 15u) & ~15u);
+}
+
+static size_t inst_lds_bytes_host(const SearchInst& si) {
+  const size_t m = si.mat_lds ? ((si.mat_bytes + 15u) & ~(size_t)15u) : 0u;
+  return m + ((((size_t)si.N + 2 * si.K) * 4u + 15u) & ~(size_t)15u);
+}
+
+template <typename MatT, int HM>
+struct StagedInst {
+  MatView<MatT, HM> D;
+  SplitParams sp;
+};
+
+template <typename MatT, int HM>
+VRPMS_DEV StagedInst<MatT, HM> stage_inst(const SearchInst& si, unsigned char* smem) {
+  const uint32_t NN = (uint32_t)si.N * si.N;
+  const MatT* M = static_cast<const MatT*>(si.mat);
+  uint32_t off = 0;
+  if (si.mat_lds) {
+    const uint32_t* s = static_cast<const uint32_t*>(si.mat);
+    uint32_t* d = reinterpret_cast<uint32_t*>(smem);
+    for (uint32_t i = threadIdx.x; i < si.mat_bytes / 4; i += blockDim.x) d[i] = s[i];
+    if ((si.mat_bytes & 2u) && threadIdx.x == 0)
+      reinterpret_cast<uint16_t*>(smem)[si.mat_bytes / 2 - 1] =
+          static_cast<const uint16_t*>(si.mat)[si.mat_bytes / 2 - 1];
+    M = reinterpret_cast<const MatT*>(smem);
+    off = (si.mat_bytes + 15u) & ~15u;
+  }
+  int32_t* dem = reinterpret_cast<int32_t*>(smem + off);
+  int32_t* cap = dem + si.N;
+  int32_t* st = cap + si.K;
+  for (int i = threadIdx.x; i < si.N; i += blockDim.x) dem[i] = si.dem[i];
+  for (int i = threadIdx.x; i < si.K; i += blockDim.x) {
+    cap[i] = si.cap[i];
+    st[i] = si.start[i];
+  }
+  __syncthreads();
+  return {{M, (uint32_t)si.N, NN, si.H}, {dem, cap, st, si.K, si.objective}};
+}
+
+// ===========================================================================
+// Simulated annealing: one wavefront per chain.
+// ===========================================================================
+struct SaArgs {
+  SearchInst si;
+  int chains, n, steps;
+  float inv_t0, inv_alpha;
+  uint32_t seed_lo, seed_hi;
+  uint64_t step0;
+  uint16_t* cur;        // [chains][n]
+  uint64_t* cur_key;    // [chains]
+  uint16_t* best;       // [chains][n]
+  uint64_t* best_key;   // [chains]
+};
+
+template <typename MatT, int HM, bool CVRP>
+__global__ __launch_bounds__(256) void sa_kernel(SaArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const StagedInst<MatT, HM> I = stage_inst<MatT, HM>(a.si, smem);
+  const int n = a.n;
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  const int chain = blockIdx.x * 4 + wave;
+  const uint32_t npad = ((uint32_t)n + 7u) & ~7u;
+  uint16_t* buf = reinterpret_cast<uint16_t*>(smem + inst_lds_bytes(a.si)) + wave * 3 * npad;
+  if (chain >= a.chains) return;  // no block-wide barrier after this point
+  uint16_t* A = buf;              // current tour
+  uint16_t* B = buf + npad;       // scratch for the accepted move
+  uint16_t* Best = buf + 2 * npad;
+  const uint16_t* gcur = a.cur + (int64_t)chain * n;
+  for (int q = lane; q < n; q += 64) A[q] = gcur[q];
+  wave_sync();
+  auto cost_of = [&](const uint16_t* T) {
+    auto tour = [&](int i) { return (uint32_t)T[i]; };
+    return eval_tour<CVRP>(I.D, I.sp, tour, n).key;
+  };
+  uint64_t ck = cost_of(A);
+  uint64_t bk = a.best_key[chain];
+  bool best_in_lds = false;
+  if (ck < bk) {
+    bk = ck;
+    for (int q = lane; q < n; q += 64) Best[q] = A[q];
+    best_in_lds = true;
+  }
+  float invT = a.inv_t0;
+  for (int s = 0; s < a.steps && n >= 2; ++s) {
+    const uint64_t step = a.step0 + (uint64_t)s;
+    const u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)chain,
+                           (uint32_t)lane, a.seed_lo, a.seed_hi);
+    const Move m = decode_move(r.x, r.y, r.z, n);
+    auto moved = [&](int q) { return (uint32_t)A[moved_index(q, m)]; };
+    uint64_t k = eval_tour<CVRP>(I.D, I.sp, moved, n).key;
+    uint64_t who = (uint64_t)lane;
+    wave_argmin(k, who);
+    const int bl = (int)who;
+    bool accept = k <= ck;
+    if (!accept) {
+      const uint64_t d = (k >> 28) - (ck >> 28);
+      const uint32_t dp = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
+      const uint32_t u = __shfl(r.w, bl, 64) >> 8;
+      accept = u < accept_threshold(dp, invT);
+    }
+    if (accept) {
+      Move mb;
+      mb.typ = (uint32_t)__shfl((int)m.typ, bl, 64);
+      mb.i = __shfl(m.i, bl, 64);
+      mb.j = __shfl(m.j, bl, 64);
+      for (int q = lane; q < n; q += 64) B[q] = A[moved_index(q, mb)];
+      wave_sync();
+      uint16_t* t = A;
+      A = B;
+      B = t;
+      ck = k;
+      if (ck < bk) {
+        bk = ck;
+        for (int q = lane; q < n; q += 64) Best[q] = A[q];
+        best_in_lds = true;
+      }
+      wave_sync();
+    }
+    invT = invT * a.inv_alpha;
+  }
+  uint16_t* gout = a.cur + (int64_t)chain * n;
+  for (int q = lane; q < n; q += 64) gout[q] = A[q];
+  if (best_in_lds) {
+    uint16_t* gb = a.best + (int64_t)chain * n;
+    for (int q = lane; q < n; q += 64) gb[q] = Best[q];
+  }
+  if (lane == 0) {
+    a.cur_key[chain] = ck;
+    a.best_key[chain] = bk;
+  }
+}
+
+// ===========================================================================
+// Genetic algorithm: breed (one wavefront per child) + select (one block per island).
+// ===========================================================================
+struct GaBreedArgs {
+  int islands, pop, n, N;
+  uint32_t pmut;        // mutation iff philox word < pmut
+  uint32_t seed_lo, seed_hi;
+  uint64_t gen;
+  const uint16_t* pop_tours;  // [islands][pop][n]
+  const uint64_t* pop_keys;   // [islands][pop]
+  uint16_t* child;            // [islands][pop][n]
+};
+
+// Tournament of two: the lower (key, index) wins.
+VRPMS_DEV int tourney(const uint64_t* keys, int pop, uint32_t r0, uint32_t r1) {
+  const int x = (int)(r0 % (uint32_t)pop), y = (int)(r1 % (uint32_t)pop);
+  const uint64_t kx = keys[x], ky = keys[y];
+  return (ky < kx || (ky == kx && y < x)) ? y : x;
+}
+
+__global__ __launch_bounds__(256) void ga_breed_kernel(GaBreedArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  const int64_t gid = (int64_t)blockIdx.x * 4 + wave;  // child id = island * pop + i
+  const int n = a.n;
+  const uint32_t words = ((uint32_t)a.N + 31u) / 32u;
+  uint32_t* used = reinterpret_cast<uint32_t*>(smem) + wave * words;
+  if (gid >= (int64_t)a.islands * a.pop) return;
+  const int island = (int)(gid / a.pop), child = (int)(gid % a.pop);
+  const uint16_t* P = a.pop_tours + (int64_t)island * a.pop * n;
+  const uint64_t* Kk = a.pop_keys + (int64_t)island * a.pop;
+  uint16_t* out = a.child + gid * n;
+  const uint32_t cid = (uint32_t)(island * a.pop + child);
+  const u32x4 r = philox((uint32_t)a.gen, (uint32_t)(a.gen >> 32), cid, 0u, a.seed_lo, a.seed_hi);
+  const u32x4 r2 = philox((uint32_t)a.gen, (uint32_t)(a.gen >> 32), cid, 1u, a.seed_lo, a.seed_hi);
+  const int pa = tourney(Kk, a.pop, r.x, r.y), pb = tourney(Kk, a.pop, r.z, r.w);
+  const uint16_t* A = P + (int64_t)pa * n;
+  const uint16_t* B = P + (int64_t)pb * n;
+  if (n < 2) {
+    for (int q = lane; q < n; q += 64) out[q] = A[q];
+    return;
+  }
+  // OX1: child[lo..hi] = A[lo..hi]; the rest, in order from position hi+1
+  // (wrapping), are B's genes from B[hi+1] onwards (wrapping) not yet used.
+  int lo = (int)(r2.x % (uint32_t)n), hi = (int)(r2.y % (uint32_t)n);
+  if (lo > hi) {
+    const int t = lo;
+    lo = hi;
+    hi = t;
+  }
+  for (uint32_t w = lane; w < words; w += 64) used[w] = 0u;
+  wave_sync();
+  for (int q = lo + lane; q <= hi; q += 64) {
+    const uint32_t g = A[q];
+    out[q] = (uint16_t)g;
+    atomicOr(&used[g >> 5], 1u << (g & 31u));
+  }
+  wave_sync();
+  const int seg = hi - lo + 1, rest = n - seg;
+  int filled = 0;
+  for (int base = 0; base < n; base += 64) {
+    const int q = base + lane;
+    uint32_t g = 0;
+    bool keep = false;
+    if (q < n) {
+      g = B[(hi + 1 + q) % n];
+      keep = ((used[g >> 5] >> (g & 31u)) & 1u) == 0u;
+    }
+    const uint64_t ball = __ballot(keep);
+    const int before = __popcll(ball & ((1ull << lane) - 1ull));
+    if (keep) {
+      const int slot = filled + before;  // slot-th free position after hi
+      if (slot < rest) out[(hi + 1 + slot) % n] = (uint16_t)g;
+    }
+    filled += __popcll(ball);
+  }
+  wave_sync();
+  // mutation: one sampled move, applied by lane 0 (rare, O(n))
+  if (r2.z < a.pmut && lane == 0) {
+    const Move m = decode_move(r2.w, r.x ^ r2.x, r.y ^ r2.y, n);
+    if (m.typ == kMoveSwap) {
+      const uint16_t t = out[m.i];
+      out[m.i] = out[m.j];
+      out[m.j] = t;
+    } else if (m.typ == kMove2Opt) {
+      for (int x = m.i, y = m.j; x < y; ++x, --y) {
+        const uint16_t t = out[x];
+        out[x] = out[y];
+        out[y] = t;
+      }
+    } else if (m.i < m.j) {
+      const uint16_t v = out[m.i];
+      for (int x = m.i; x < m.j; ++x) out[x] = out[x + 1];
+      out[m.j] = v;
+    } else {
+      const uint16_t v = out[m.i];
+      for (int x = m.i; x > m.j; --x) out[x] = out[x - 1];
+      out[m.j] = v;
+    }
+  }
+}
+
+struct GaSelectArgs {
+  int islands, pop, n;
+  const uint16_t* pop_tours;   // [islands][pop][n]
+  const uint64_t* pop_keys;
+  const uint16_t* child;       // [islands][pop][n]
+  const uint64_t* child_keys;
+  uint16_t* out_tours;         // [islands][pop][n]
+  uint64_t* out_keys;
+};
+
+// (mu + lambda): the pop best of parents (index i) and children (index pop + i)
+// by (key, index); bitonic sort over the next power of two >= 2 * pop.
+__global__ __launch_bounds__(1024) void ga_select_kernel(GaSelectArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint64_t* sk = reinterpret_cast<uint64_t*>(smem);
+  const int island = blockIdx.x, pop = a.pop, n = a.n;
+  int M = 1;
+  while (M < 2 * pop) M <<= 1;
+  uint32_t* si = reinterpret_cast<uint32_t*>(sk + M);
+  const uint64_t* pk = a.pop_keys + (int64_t)island * pop;
+  const uint64_t* ck = a.child_keys + (int64_t)island * pop;
+  for (int i = threadIdx.x; i < M; i += blockDim.x) {
+    sk[i] = i < pop ? pk[i] : (i < 2 * pop ? ck[i - pop] : ~0ull);
+    si[i] = (uint32_t)i;
+  }
+  __syncthreads();
+  for (int size = 2; size <= M; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < M; i += blockDim.x) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool up = (i & size) == 0;
+          const uint64_t ki = sk[i], kj = sk[j];
+          const uint32_t ii = si[i], ij = si[j];
+          const bool gt = ki > kj || (ki == kj && ii > ij);
+          if (gt == up) {
+            sk[i] = kj;
+            sk[j] = ki;
+            si[i] = ij;
+            si[j] = ii;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const uint16_t* P = a.pop_tours + (int64_t)island * pop * n;
+  const uint16_t* Cc = a.child + (int64_t)island * pop * n;
+  uint16_t* O = a.out_tours + (int64_t)island * pop * n;
+  for (int i = threadIdx.x; i < pop; i += blockDim.x) a.out_keys[(int64_t)island * pop + i] = sk[i];
+  for (int64_t e = threadIdx.x; e < (int64_t)pop * n; e += blockDim.x) {
+    const int i = (int)(e / n), q = (int)(e % n);
+    const uint32_t src = si[i];
+    O[e] = src < (uint32_t)pop ? P[(int64_t)src * n + q] : Cc[(int64_t)(src - pop) * n + q];
+  }
+}
+
+// ===========================================================================
+// Integer ant colony: tau (uint32 fixed point) per colony, eta2 = floor(2^24 / (1 + d)^2).
+// ===========================================================================
+struct AcoArgs {
+  int colonies, ants, n, N;
+  uint32_t seed_lo, seed_hi;
+  uint64_t iter;
+  const uint32_t* tau;   // [colonies][N][N]
+  const uint32_t* eta;   // [N][N] (static part of the weight)
+  uint16_t* tours;       // [colonies][ants][n]
+};
+
+// Ant: starts at node 0; each step picks j among unvisited customers with
+// probability w_j / sum w, w_j = (tau[i][j] >> 8) * eta[i][j] (uint64, exact),
+// r = philox64 % sum, the smallest j (index order) whose prefix sum exceeds r.
+__global__ __launch_bounds__(256) void aco_construct_kernel(AcoArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  const int64_t gid = (int64_t)blockIdx.x * 4 + wave;
+  const int N = a.N, n = a.n;
+  const uint32_t words = ((uint32_t)N + 31u) / 32u;
+  uint32_t* vis = reinterpret_cast<uint32_t*>(smem) + wave * words;
+  if (gid >= (int64_t)a.colonies * a.ants) return;
+  const int colony = (int)(gid / a.ants), ant = (int)(gid % a.ants);
+  const uint32_t* T = a.tau + (int64_t)colony * N * N;
+  uint16_t* out = a.tours + gid * n;
+  for (uint32_t w = lane; w < words; w += 64) vis[w] = 0u;
+  wave_sync();
+  if (lane == 0) atomicOr(&vis[0], 1u);  // depot
+  wave_sync();
+  uint32_t cur = 0;
+  for (int s = 0; s < n; ++s) {
+    const u32x4 r = philox((uint32_t)a.iter, (uint32_t)(a.iter >> 32),
+                           (uint32_t)(colony * a.ants + ant), (uint32_t)s, a.seed_lo, a.seed_hi);
+    const uint32_t* Tr = T + (int64_t)cur * N;
+    const uint32_t* Er = a.eta + (int64_t)cur * N;
+    // pass 1: total weight (integer, so the order of summation is irrelevant)
+    uint64_t tot = 0;
+    int first_free = INT_MAX;
+    for (int j = lane; j < N; j += 64) {
+      if (!((vis[j >> 5] >> (j & 31)) & 1u)) {
+        tot += (uint64_t)(Tr[j] >> 8) * Er[j];
+        first_free = min(first_free, j);
+      }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      tot += __shfl_xor(tot, off, 64);
+      first_free = min(first_free, __shfl_xor(first_free, off, 64));
+    }
+    uint32_t pick;
+    if (tot == 0) {
+      pick = (uint32_t)first_free;
+    } else {
+      const uint64_t rr = (((uint64_t)r.y << 32) | r.x) % tot;
+      // pass 2: scan chunks of 64 consecutive j; lane-level inclusive prefix
+      uint64_t run = 0;
+      pick = 0xffffffffu;
+      for (int base = 0; base < N && pick == 0xffffffffu; base += 64) {
+        const int j = base + lane;
+        uint64_t w = 0;
+        if (j < N && !((vis[j >> 5] >> (j & 31)) & 1u)) w = (uint64_t)(Tr[j] >> 8) * Er[j];
+        uint64_t inc = w;
+        for (int off = 1; off < 64; off <<= 1) {
+          const uint64_t o = __shfl_up(inc, off, 64);
+          if (lane >= off) inc += o;
+        }
+        const bool hit = w > 0 && run + inc > rr;
+        const uint64_t ball = __ballot(hit);
+        if (ball) pick = (uint32_t)(base + __ffsll((long long)ball) - 1);
+        run += __shfl(inc, 63, 64);
+      }
+      if (pick == 0xffffffffu) pick = (uint32_t)first_free;  // unreachable: tot > rr
+    }
+    if (lane == 0) {
+      out[s] = (uint16_t)pick;
+      atomicOr(&vis[pick >> 5], 1u << (pick & 31u));
+    }
+    wave_sync();
+    cur = pick;
+  }
+}
+
+struct AcoUpdateArgs {
+  int colonies, ants, n, N;
+  uint32_t evap_shift, tau_min, tau_max;
+  uint32_t* tau;                 // [colonies][N][N]
+  const uint16_t* tours;         // [colonies][ants][n]
+  const uint64_t* ib;            // [colonies][2] iteration-best (key, ant)
+};
+
+__global__ void aco_evaporate_kernel(AcoUpdateArgs a) {
+  const int64_t total = (int64_t)a.colonies * a.N * a.N;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t t = a.tau[i];
+    a.tau[i] = min(a.tau_max, max(a.tau_min, t - (t >> a.evap_shift)));
+  }
+}
+
+// deposit floor(2^30 / (1 + primary)) on every edge of the iteration-best tour
+__global__ void aco_deposit_kernel(AcoUpdateArgs a) {
+  const int colony = blockIdx.x;
+  const uint64_t key = a.ib[2 * colony];
+  const int ant = (int)a.ib[2 * colony + 1];
+  const uint32_t primary = (uint32_t)((key >> 28) & ((1u << 28) - 1u));
+  const uint32_t dep = (uint32_t)((1u << 30) / (1ull + primary));
+  const uint16_t* t = a.tours + ((int64_t)colony * a.ants + ant) * a.n;
+  uint32_t* T = a.tau + (int64_t)colony * a.N * a.N;
+  for (int q = threadIdx.x; q <= a.n; q += blockDim.x) {
+    const uint32_t from = q == 0 ? 0u : t[q - 1];
+    const uint32_t to = q == a.n ? 0u : t[q];
+    const uint64_t idx = (uint64_t)from * a.N + to;
+    const uint32_t old = atomicAdd(&T[idx], dep);
+    (void)old;
+  }
+}
+
+// per-colony argmin over ant keys -> ib[2c] = key, ib[2c+1] = ant
+__global__ void segment_argmin_kernel(const uint64_t* __restrict__ keys, int seg, int nseg,
+                                      uint64_t* out) {
+  const int s = blockIdx.x;
+  if (s >= nseg) return;
+  uint64_t k = ~0ull, idx = ~0ull;
+  for (int i = threadIdx.x; i < seg; i += blockDim.x) {
+    const uint64_t v = keys[(int64_t)s * seg + i];
+    if (v < k || (v == k && (uint64_t)i < idx)) {
+      k = v;
+      idx = (uint64_t)i;
+    }
+  }
+  wave_argmin(k, idx);
+  __shared__ uint64_t wk[16], wi[16];
+  const int w = threadIdx.x >> 6;
+  if (lane_id() == 0) {
+    wk[w] = k;
+    wi[w] = idx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int x = 1; x < (int)(blockDim.x >> 6); ++x)
+      if (wk[x] < k || (wk[x] == k && wi[x] < idx)) {
+        k = wk[x];
+        idx = wi[x];
+      }
+    out[2 * s] = k;
+    out[2 * s + 1] = idx;
+  }
+}
+
+// ===========================================================================
+// Brute force: lexicographic ranks [r0, r1) of permutations of 1..n (n <= 15),
+// nibble-packed (element i in bits 4i..4i+3).
+// ===========================================================================
+struct BfArgs {
+  SearchInst si;
+  int n;
+  uint64_t r0, r1, chunk;
+  uint64_t* block_best;  // [gridDim.x][2] (key, rank)
+};
+
+VRPMS_DEV uint32_t nib(uint64_t p, int i) { return (uint32_t)(p >> (4 * i)) & 15u; }
+
+VRPMS_DEV uint64_t unrank(uint64_t r, int n) {
+  uint64_t fact[16];
+  fact[0] = 1;
+  for (int i = 1; i < 16; ++i) fact[i] = fact[i - 1] * (uint64_t)i;
+  uint32_t avail = (1u << n) - 1u;  // bit v-1 = value v available
+  uint64_t p = 0;
+  for (int i = 0; i < n; ++i) {
+    const uint64_t f = fact[n - 1 - i];
+    int d = (int)(r / f);
+    r %= f;
+    // d-th smallest available value
+    uint32_t m = avail;
+    for (int x = 0; x < d; ++x) m &= m - 1u;
+    const int v = __ffs((int)m);  // 1-based bit position = value
+    avail &= ~(1u << (v - 1));
+    p |= (uint64_t)v << (4 * i);
+  }
+  return p;
+}
+
+VRPMS_DEV uint64_t next_perm(uint64_t p, int n) {
+  int i = n - 2;
+  while (i >= 0 && nib(p, i) >= nib(p, i + 1)) --i;
+  if (i < 0) return p;
+  int j = n - 1;
+  while (nib(p, j) <= nib(p, i)) --j;
+  const uint64_t a = nib(p, i), b = nib(p, j);
+  p &= ~((15ull << (4 * i)) | (15ull << (4 * j)));
+  p |= (b << (4 * i)) | (a << (4 * j));
+  for (int x = i + 1, y = n - 1; x < y; ++x, --y) {
+    const uint64_t vx = nib(p, x), vy = nib(p, y);
+    p &= ~((15ull << (4 * x)) | (15ull << (4 * y)));
+    p |= (vy << (4 * x)) | (vx << (4 * y));
+  }
+  return p;
+}
+
+template <typename MatT, int HM, bool CVRP>
+__global__ __launch_bounds__(256) void bf_kernel(BfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const StagedInst<MatT, HM> I = stage_inst<MatT, HM>(a.si, smem);
+  const int n = a.n;
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t bk = ~0ull, br = ~0ull;
+  const uint64_t lo = a.r0 + tid * a.chunk;
+  if (lo < a.r1) {
+    const uint64_t hi = min(a.r1, lo + a.chunk);
+    uint64_t p = unrank(lo, n);
+    for (uint64_t rk = lo; rk < hi; ++rk) {
+      auto tour = [&](int i) { return nib(p, i); };
+      const uint64_t k = eval_tour<CVRP>(I.D, I.sp, tour, n).key;
+      if (k < bk) {
+        bk = k;
+        br = rk;
+      }
+      p = next_perm(p, n);
+    }
+  }
+  wave_argmin(bk, br);
+  __shared__ uint64_t wk[4], wr[4];
+  if (lane_id() == 0) {
+    wk[threadIdx.x >> 6] = bk;
+    wr[threadIdx.x >> 6] = br;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w)
+      if (wk[w] < bk || (wk[w] == bk && wr[w] < br)) {
+        bk = wk[w];
+        br = wr[w];
+      }
+    a.block_best[2 * blockIdx.x] = bk;
+    a.block_best[2 * blockIdx.x + 1] = br;
+  }
+}
+
+__global__ void reduce_pairs_kernel(const uint64_t* in, int count, uint64_t* out) {
+  uint64_t k = ~0ull, r = ~0ull;
+  for (int i = threadIdx.x; i < count; i += blockDim.x) {
+    const uint64_t kk = in[2 * i], rr = in[2 * i + 1];
+    if (kk < k || (kk == k && rr < r)) {
+      k = kk;
+      r = rr;
+    }
+  }
+  wave_argmin(k, r);
+  __shared__ uint64_t wk[16], wr[16];
+  if (lane_id() == 0) {
+    wk[threadIdx.x >> 6] = k;
+    wr[threadIdx.x >> 6] = r;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
+      if (wk[w] < k || (wk[w] == k && wr[w] < r)) {
+        k = wk[w];
+        r = wr[w];
+      }
+    out[0] = k;
+    out[1] = r;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// dispatch helpers: <MatT, HM, CVRP> from the loaded instance
+// ---------------------------------------------------------------------------
+template <template <typename, int, bool> class K, typename Args>
+static int launch_inst(const vrpms_ctx* ctx, dim3 grid, dim3 block, size_t lds, hipStream_t s,
+                       const Args& args) {
+  const Instance& in = ctx->inst;
+  const bool cvrp = in.problem == VRPMS_CVRP;
+  auto go = [&](auto kern) {
+    if (lds > 65536)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    kern<<<grid, block, lds, s>>>(args);
+  };
+#define VRPMS_SEL(MT)                                                            \
+  if (in.H == 1) {                                                               \
+    if (cvrp) go(K<MT, 1, true>::kernel()); else go(K<MT, 1, false>::kernel());  \
+  } else if (in.H == 24) {                                                       \
+    if (cvrp) go(K<MT, 24, true>::kernel()); else go(K<MT, 24, false>::kernel());\
+  } else {                                                                       \
+    if (cvrp) go(K<MT, 0, true>::kernel()); else go(K<MT, 0, false>::kernel());  \
+  }
+  if (in.use16) {
+    VRPMS_SEL(uint16_t)
+  } else {
+    VRPMS_SEL(int32_t)
+  }
+#undef VRPMS_SEL
+  VRPMS_HIP(hipGetLastError());
+  return VRPMS_OK;
+}
+
+template <typename MatT, int HM, bool CVRP>
+struct SaK {
+  static auto kernel() { return sa_kernel<MatT, HM, CVRP>; }
+};
+template <typename MatT, int HM, bool CVRP>
+struct BfK {
+  static auto kernel() { return bf_kernel<MatT, HM, CVRP>; }
+};
+
+static void ensure_scratch(vrpms_ctx* ctx, size_t bytes, int* err) {
+  if (ctx->search_scratch_bytes >= bytes) return;
+  (void)hipFree(ctx->search_scratch);
+  ctx->search_scratch = nullptr;
+  ctx->search_scratch_bytes = 0;
+  if (hipMalloc(&ctx->search_scratch, bytes) != hipSuccess) {
+    *err = fail(VRPMS_ENOMEM, "search scratch allocation failed");
+    return;
+  }
+  ctx->search_scratch_bytes = bytes;
+}
+
+}  // namespace vrpms
+
+using namespace vrpms;
+
+extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* d_cur,
+                            uint64_t* d_cur_key, uint16_t* d_best, uint64_t* d_best_key,
+                            int32_t n, void* stream) {
+  if (!ctx || !p) return fail(VRPMS_EINVAL, "vrpms_sa_run: NULL ctx/params");
+  if (!ctx->has_instance) return fail(VRPMS_ESTATE, "vrpms_sa_run: no instance loaded");
+  if (p->chains <= 0 || p->steps < 0 || n < 0 || n > ctx->inst.N - 1)
+    return fail(VRPMS_EINVAL, "vrpms_sa_run: need chains > 0, steps >= 0, 0 <= n <= N-1");
+  if (!d_cur || !d_cur_key || !d_best || !d_best_key)
+    return fail(VRPMS_EINVAL, "vrpms_sa_run: NULL state buffer");
+  VRPMS_HIP(hipSetDevice(ctx->device));
+  SaArgs a{search_inst(ctx), p->chains, n, p->steps, p->inv_t0, p->inv_alpha,
+           (uint32_t)p->seed, (uint32_t)(p->seed >> 32), p->step0, d_cur, d_cur_key, d_best,
+           d_best_key};
+  const size_t npad = ((size_t)n + 7) & ~(size_t)7;
+  size_t lds = inst_lds_bytes_host(a.si) + 4 * 3 * npad * 2;
+  if (lds > ctx->max_lds) {
+    a.si.mat_lds = 0;
+    lds = inst_lds_bytes_host(a.si) + 4 * 3 * npad * 2;
+  }
+  if (lds > ctx->max_lds) return fail(VRPMS_EINVAL, "vrpms_sa_run: tours too long for LDS");
+  return launch_inst<SaK>(ctx, dim3((p->chains + 3) / 4), dim3(256), lds, (hipStream_t)stream, a);
+}
+
+extern "C" int vrpms_ga_generation(vrpms_ctx* ctx, const vrpms_ga_params* p, uint16_t* d_pop,
+                                   uint64_t* d_keys, int32_t n, void* stream) {
+  if (!ctx || !p) return fail(VRPMS_EINVAL, "vrpms_ga_generation: NULL ctx/params");
+  if (!ctx->has_instance) return fail(VRPMS_ESTATE, "vrpms_ga_generation: no instance loaded");
+  if (p->islands <= 0 || p->pop <= 1 || p->pop > 4096 || n < 0 || n > ctx->inst.N - 1)
+    return fail(VRPMS_EINVAL, "vrpms_ga_generation: need islands > 0, 2 <= pop <= 4096, n <= N-1");
+  if (!d_pop || !d_keys) return fail(VRPMS_EINVAL, "vrpms_ga_generation: NULL population");
+  VRPMS_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t members = (int64_t)p->islands * p->pop;
+  const size_t tour_bytes = (size_t)members * n * 2;
+  const size_t need = 2 * tour_bytes + (size_t)members * 8 * 2 + 256;
+  int err = VRPMS_OK;
+  ensure_scratch(ctx, need, &err);
+  if (err) return err;
+  unsigned char* sp = static_cast<unsigned char*>(ctx->search_scratch);
+  uint16_t* child = reinterpret_cast<uint16_t*>(sp);
+  uint16_t* next = reinterpret_cast<uint16_t*>(sp + tour_bytes);
+  uint64_t* ckeys = reinterpret_cast<uint64_t*>(sp + 2 * tour_bytes);
+  uint64_t* nkeys = ckeys + members;
+  for (int g = 0; g < p->generations; ++g) {
+    const uint64_t gen = p->gen0 + (uint64_t)g;
+    GaBreedArgs b{p->islands, p->pop, n, ctx->inst.N, p->pmut, (uint32_t)p->seed, (uint32_t)(p->seed >> 32),
+                  gen, d_pop, d_keys, child};
+    const size_t lds_b = 4 * (((size_t)ctx->inst.N + 31) / 32) * 4;
+    ga_breed_kernel<<<(unsigned)((members + 3) / 4), 256, lds_b, s>>>(b);
+    VRPMS_HIP(hipGetLastError());
+    int rc = vrpms_eval(ctx, child, 2, members, n, n, ckeys, nullptr, nullptr, nullptr, stream);
+    if (rc) return rc;
+    int M = 1;
+    while (M < 2 * p->pop) M <<= 1;
+    GaSelectArgs sa{p->islands, p->pop, n, d_pop, d_keys, child, ckeys, next, nkeys};
+    if ((size_t)M * 12 > 65536)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ga_select_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)((size_t)M * 12));
+    ga_select_kernel<<<p->islands, 1024, (size_t)M * 12, s>>>(sa);
+    VRPMS_HIP(hipGetLastError());
+    VRPMS_HIP(hipMemcpyAsync(d_pop, next, tour_bytes, hipMemcpyDeviceToDevice, s));
+    VRPMS_HIP(hipMemcpyAsync(d_keys, nkeys, (size_t)members * 8, hipMemcpyDeviceToDevice, s));
+  }
+  return VRPMS_OK;
+}
+
+extern "C" int vrpms_aco_init(vrpms_ctx* ctx, int32_t colonies, uint32_t tau0, uint32_t* d_tau,
+                              uint32_t* d_eta, void* stream);
+
+extern "C" int vrpms_aco_iteration(vrpms_ctx* ctx, const vrpms_aco_params* p, uint32_t* d_tau,
+                                   const uint32_t* d_eta, uint16_t* d_tours, uint64_t* d_keys,
+                                   uint64_t* d_iter_best, int32_t n, void* stream) {
+  if (!ctx || !p) return fail(VRPMS_EINVAL, "vrpms_aco_iteration: NULL ctx/params");
+  if (!ctx->has_instance) return fail(VRPMS_ESTATE, "vrpms_aco_iteration: no instance loaded");
+  const Instance& in = ctx->inst;
+  if (p->colonies <= 0 || p->ants <= 0 || n != in.N - 1)
+    return fail(VRPMS_EINVAL, "vrpms_aco_iteration: need colonies, ants > 0 and n == N-1");
+  if (!d_tau || !d_eta || !d_tours || !d_keys || !d_iter_best)
+    return fail(VRPMS_EINVAL, "vrpms_aco_iteration: NULL buffer");
+  if (p->tau_max > (1u << 31) || p->tau_min > p->tau_max)
+    return fail(VRPMS_EINVAL, "vrpms_aco_iteration: need tau_min <= tau_max <= 2^31");
+  if (p->evap_shift < 1 || p->evap_shift > 31)
+    return fail(VRPMS_EINVAL, "vrpms_aco_iteration: evap_shift must be in [1, 31]");
+  VRPMS_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t ants = (int64_t)p->colonies * p->ants;
+  AcoArgs c{p->colonies, p->ants, n, in.N, (uint32_t)p->seed, (uint32_t)(p->seed >> 32), p->iter,
+            d_tau, d_eta, d_tours};
+  const size_t lds = 4 * (((size_t)in.N + 31) / 32) * 4;
+  aco_construct_kernel<<<(unsigned)((ants + 3) / 4), 256, lds, s>>>(c);
+  VRPMS_HIP(hipGetLastError());
+  int rc = vrpms_eval(ctx, d_tours, 2, ants, n, n, d_keys, nullptr, nullptr, nullptr, stream);
+  if (rc) return rc;
+  segment_argmin_kernel<<<p->colonies, 256, 0, s>>>(d_keys, p->ants, p->colonies, d_iter_best);
+  AcoUpdateArgs u{p->colonies, p->ants, n, in.N, (uint32_t)p->evap_shift, p->tau_min, p->tau_max,
+                  d_tau, d_tours, d_iter_best};
+  const int64_t total = (int64_t)p->colonies * in.N * in.N;
+  aco_evaporate_kernel<<<(unsigned)std::min<int64_t>((total + 255) / 256, ctx->num_cus * 8), 256, 0,
+                         s>>>(u);
+  aco_deposit_kernel<<<p->colonies, 256, 0, s>>>(u);
+  VRPMS_HIP(hipGetLastError());
+  return VRPMS_OK;
+}
+
+__global__ void aco_init_kernel(const int32_t* __restrict__ D, int N, int colonies, uint32_t tau0,
+                                uint32_t* tau, uint32_t* eta) {
+  const int64_t NN = (int64_t)N * N;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (int64_t)colonies * NN;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    tau[i] = tau0;
+    if (i < NN) {
+      const uint64_t d1 = 1ull + (uint64_t)(uint32_t)D[i];  // static slice (hour 0)
+      eta[i] = (uint32_t)((1ull << 24) / (d1 * d1));
+    }
+  }
+}
+
+extern "C" int vrpms_aco_init(vrpms_ctx* ctx, int32_t colonies, uint32_t tau0, uint32_t* d_tau,
+                              uint32_t* d_eta, void* stream) {
+  if (!ctx) return fail(VRPMS_EINVAL, "vrpms_aco_init: ctx is NULL");
+  if (!ctx->has_instance) return fail(VRPMS_ESTATE, "vrpms_aco_init: no instance loaded");
+  if (colonies <= 0 || !d_tau || !d_eta) return fail(VRPMS_EINVAL, "vrpms_aco_init: bad args");
+  VRPMS_HIP(hipSetDevice(ctx->device));
+  const Instance& in = ctx->inst;
+  const int64_t total = (int64_t)colonies * in.N * in.N;
+  aco_init_kernel<<<(unsigned)std::min<int64_t>((total + 255) / 256, ctx->num_cus * 8), 256, 0,
+                    (hipStream_t)stream>>>(in.mat32, in.N, colonies, tau0, d_tau, d_eta);
+  VRPMS_HIP(hipGetLastError());
+  return VRPMS_OK;
+}
+
+extern "C" int vrpms_bf_run(vrpms_ctx* ctx, int32_t n, uint64_t rank_begin, uint64_t rank_end,
+                            uint64_t* d_out, void* stream) {
+  if (!ctx) return fail(VRPMS_EINVAL, "vrpms_bf_run: ctx is NULL");
+  if (!ctx->has_instance) return fail(VRPMS_ESTATE, "vrpms_bf_run: no instance loaded");
+  if (n < 1 || n > 15 || n > ctx->inst.N - 1)
+    return fail(VRPMS_EINVAL, "vrpms_bf_run: brute force needs 1 <= n <= min(15, N-1)");
+  if (!d_out || rank_end < rank_begin) return fail(VRPMS_EINVAL, "vrpms_bf_run: bad range/out");
+  VRPMS_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = (hipStream_t)stream;
+  VRPMS_HIP(hipMemsetAsync(d_out, 0xff, 16, s));
+  const uint64_t count = rank_end - rank_begin;
+  if (count == 0) return VRPMS_OK;
+  const uint64_t threads_max = (uint64_t)ctx->num_cus * 8 * 256;
+  uint64_t chunk = std::max<uint64_t>(64, (count + threads_max - 1) / threads_max);
+  const uint64_t threads = (count + chunk - 1) / chunk;
+  const int blocks = (int)((threads + 255) / 256);
+  int err = VRPMS_OK;
+  ensure_scratch(ctx, (size_t)blocks * 16, &err);
+  if (err) return err;
+  BfArgs a{search_inst(ctx), n, rank_begin, rank_end, chunk,
+           static_cast<uint64_t*>(ctx->search_scratch)};
+  size_t lds = inst_lds_bytes_host(a.si);
+  if (lds > ctx->max_lds) {
+    a.si.mat_lds = 0;
+    lds = inst_lds_bytes_host(a.si);
+  }
+  int rc = launch_inst<BfK>(ctx, dim3(blocks), dim3(256), lds, s, a);
+  if (rc) return rc;
+  reduce_pairs_kernel<<<1, 1024, 0, s>>>(static_cast<uint64_t*>(ctx->search_scratch), blocks,
+                                         d_out);
+  VRPMS_HIP(hipGetLastError());
+  return VRPMS_OK;
+}

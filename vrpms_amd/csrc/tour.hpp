@@ -1,0 +1,175 @@
+// Single-tour evaluation (frozen in oracle/spec.py)
+// shared by the generic scoring kernel and every search kernel, so a tour
+// scored inside SA/GA/ACO/BF is bit-identical to vrpms_eval's score of it.
+#pragma once
+#include "common.hpp"
+
+namespace vrpms {
+
+// A3: hour slice of an edge departing at minute t.  HM = 1 static,
+// HM = 24 hour-indexed (constant divisor), HM = 0 runtime H.
+template <int HM>
+VRPMS_DEV uint32_t hour_of(int t, int H) {
+  if constexpr (HM == 1) {
+    return 0;
+  } else if constexpr (HM == 24) {
+    return ((uint32_t)t / 60u) % 24u;
+  } else {
+    return ((uint32_t)t / 60u) % (uint32_t)H;
+  }
+}
+
+// Duration matrix view (LDS or global), [H][N][N].
+template <typename MatT, int HM>
+struct MatView {
+  const MatT* M;
+  uint32_t N, NN;
+  int H;
+  VRPMS_DEV int operator()(int t, uint32_t a, uint32_t b) const {
+    return (int)M[hour_of<HM>(t, H) * NN + a * N + b];
+  }
+};
+
+struct SplitParams {
+  const int32_t* dem;
+  const int32_t* cap;
+  const int32_t* start;
+  int K;
+  int objective;
+};
+
+struct TourCost {
+  uint64_t key;
+  int32_t sum, max, unv;
+};
+
+// A4 (TSP) / A5-A7 (CVRP greedy split); `tour(i)` returns customer i
+// (values >= N are clamped to N-1 so a corrupt tour can never fault).
+template <bool CVRP, typename Mat, typename Tour>
+VRPMS_DEV TourCost eval_tour(const Mat& D, const SplitParams& sp, const Tour& tour, int n) {
+  const uint32_t Nm1 = D.N - 1;
+  if constexpr (!CVRP) {
+    const int t0 = sp.start[0];
+    int t = t0;
+    uint32_t prev = 0;
+    for (int i = 0; i < n; ++i) {
+      const uint32_t cc = min((uint32_t)tour(i), Nm1);
+      t += D(t, prev, cc);
+      prev = cc;
+    }
+    t += D(t, prev, 0);
+    const int d = t - t0;
+    return {pack_key(0, (uint32_t)d, 0), d, d, 0};
+  } else {
+    const int K = sp.K;
+    int k = 0, load = 0, t = sp.start[0], capk = sp.cap[0];
+    uint32_t prev = 0, unv = 0, dsum = 0, dmax = 0;
+    for (int i = 0; i < n; ++i) {
+      const uint32_t cc = min((uint32_t)tour(i), Nm1);
+      const int dc = sp.dem[cc];
+      if (k < K && load + dc > capk) {
+        do {
+          if (prev) {
+            t += D(t, prev, 0);
+            const uint32_t rd = (uint32_t)(t - sp.start[k]);
+            dsum += rd;
+            dmax = max(dmax, rd);
+          }
+          ++k;
+          if (k < K) {
+            load = 0;
+            t = sp.start[k];
+            prev = 0;
+            capk = sp.cap[k];
+          }
+        } while (k < K && load + dc > capk);
+      }
+      if (k < K) {
+        t += D(t, prev, cc);
+        load += dc;
+        prev = cc;
+      } else {
+        ++unv;
+      }
+    }
+    if (k < K && prev) {
+      t += D(t, prev, 0);
+      const uint32_t rd = (uint32_t)(t - sp.start[k]);
+      dsum += rd;
+      dmax = max(dmax, rd);
+    }
+    return {cvrp_key(unv, dsum, dmax, sp.objective), (int32_t)dsum, (int32_t)dmax, (int32_t)unv};
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Neighbourhood moves on a giant tour (oracle/spec.py decode_move / moved_index)
+// ---------------------------------------------------------------------------
+enum : uint32_t { kMoveSwap = 0, kMove2Opt = 1, kMoveRelocate = 2 };
+
+struct Move {
+  uint32_t typ;
+  int i, j;
+};
+
+VRPMS_DEV Move decode_move(uint32_t r0, uint32_t r1, uint32_t r2, int n) {
+  Move m;
+  m.typ = r0 % 3u;
+  m.i = (int)(r1 % (uint32_t)n);
+  int j = (int)(r2 % (uint32_t)(n - 1));
+  if (j >= m.i) ++j;
+  m.j = j;
+  if (m.typ != kMoveRelocate && m.i > m.j) {
+    const int x = m.i;
+    m.i = m.j;
+    m.j = x;
+  }
+  return m;
+}
+
+// Position in the ORIGINAL tour read at position q of the moved tour.
+VRPMS_DEV int moved_index(int q, const Move& m) {
+  const int i = m.i, j = m.j;
+  if (m.typ == kMoveSwap) return q == i ? j : (q == j ? i : q);
+  if (m.typ == kMove2Opt) return (q >= i && q <= j) ? i + j - q : q;
+  if (i < j) {
+    if (q < i || q > j) return q;
+    return q == j ? i : q + 1;
+  }
+  if (q < j || q > i) return q;
+  return q == j ? i : q - 1;
+}
+
+// ---------------------------------------------------------------------------
+// Deterministic SA acceptance threshold: floor(2^24 * exp(-dp * invT)) using
+// only IEEE fp32 multiply/add/sub (built with -ffp-contract=off) and exact
+// power-of-two scaling, so oracle/spec.py reproduces it bit for bit.
+// ---------------------------------------------------------------------------
+VRPMS_DEV uint32_t accept_threshold(uint32_t dp, float invT) {
+  if (dp == 0) return 1u << 24;
+  const float x = (float)dp * invT;           // >= 0
+  const float y = x * 0x1.715476p+0f;            // x * log2(e)
+  if (!(y < 24.0f)) return 0u;                // 2^-24 * 2^24 < 1
+  const float kf = floorf(y);
+  const float f = y - kf;                     // [0, 1)
+  // 2^-f = exp(-f ln2), degree-6 Taylor polynomial in g = f * ln2 (|err| < 2e-6)
+  const float g = f * 0x1.62e43p-1f;
+  float p = 0x1.6c16c2p-10f;                   // 1/720
+  p = p * g;
+  p = 0x1.111112p-7f - p;                     // 1/120
+  p = p * g;
+  p = 0x1.555556p-5f - p;                      // 1/24
+  p = p * g;
+  p = 0x1.555556p-3f - p;                       // 1/6
+  p = p * g;
+  p = 0.5f - p;
+  p = p * g;
+  p = 1.0f - p;
+  p = p * g;
+  p = 1.0f - p;                               // ~ e^-g
+  const int k = (int)kf;                      // 0..23
+  const float scaled = p * (float)(1u << (24 - k));  // exact power-of-two scaling
+  return (uint32_t)scaled;                    // truncation
+}
+
+}  // namespace vrpms
