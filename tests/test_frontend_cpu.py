@@ -1,0 +1,86 @@
+"""CPU tests of the front-end host logic, pinned by the reference's own
+behaviour captured in tests/golden/reference_fixtures.json."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from vrpms_amd import solver
+
+FX = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_fixtures.json")))
+
+
+@pytest.mark.parametrize("case", FX["remove_unused_locations"])
+def test_active_customers_match_remove_unused_locations(case):
+    """The solver's customer set is remove_unused_locations (api/helpers.py:11-13)
+    minus the depot row, which A1 always keeps."""
+    locs = case["locations"]
+    kept = [loc["id"] for loc in case["result"]]
+    ours = solver.active_customers(locs, case["ignored"], case["completed"])
+    assert [locs[i]["id"] for i in ours] == [x for x in kept if x != locs[0]["id"]]
+
+
+def test_calculate_duration_shape_and_stub_range():
+    ref = FX["calculate_duration"][0]
+    solver._LOOKUP = None
+    got = solver.calculate_duration("A", "B")
+    assert set(got) == set(ref) and got["units"] == "minutes"
+    assert 3 <= got["duration"] <= 320
+
+
+def test_calculate_duration_backed_by_matrix():
+    D = np.zeros((24, 3, 3), dtype=np.int64)
+    for h in range(24):
+        D[h] = h + 10
+    solver.set_duration_matrix(D, location_ids=["a", "b", "c"])
+    try:
+        assert solver.calculate_duration("a", "c", time_of_day=125)["duration"] == 12
+        assert solver.calculate_duration("b", "a", time_of_day=60 * 25)["duration"] == 11
+    finally:
+        solver._LOOKUP = None
+
+
+def test_compact_tsp_start_and_dedup():
+    D = np.arange(25).reshape(5, 5)
+    ci = solver.compact_tsp(D, [3, 1, 3, 4, 2], 2, 7)
+    assert ci.nodes == [2, 3, 1, 4]
+    assert ci.durations.shape == (1, 4, 4)
+    assert ci.durations[0, 0, 1] == D[2, 3]
+    assert ci.start_times.tolist() == [7]
+
+
+def test_compact_vrp_filters_and_demand_default():
+    D = np.ones((5, 5), dtype=np.int64)
+    locs = [{"id": 10}, {"id": 11, "demand": 4}, {"id": 12}, {"id": 13}, {"id": 14, "demand": 2}]
+    ci = solver.compact_vrp(D, locs, [5, 6], [0, 60], ignored_customers=[12],
+                            completed_customers=[13])
+    assert ci.nodes == [0, 1, 4]
+    assert ci.demand.tolist() == [0, 4, 2]
+
+
+@pytest.mark.parametrize("bad", [
+    {"durations": [[0, 1], [1]]},
+    {"durations": [[0, -1], [1, 0]]},
+    {"durations": [[0, 1.5], [1, 0]]},
+    {"durations": np.zeros((2, 3, 3))},
+])
+def test_bad_matrices_rejected(bad):
+    with pytest.raises(ValueError):
+        solver.compact_vrp(bad["durations"], [{"id": i} for i in range(3)], [1], [0])
+
+
+def test_vrp_shape_errors():
+    D = np.ones((3, 3))
+    with pytest.raises(ValueError, match="locations"):
+        solver.compact_vrp(D, [{"id": 0}], [1], [0])
+    with pytest.raises(ValueError, match="same length"):
+        solver.compact_vrp(D, [{"id": i} for i in range(3)], [1, 2], [0])
+    with pytest.raises(ValueError, match="startNode"):
+        solver.compact_tsp(D, [1], 9)
+
+
+def test_reference_stub_shape_fixture():
+    for r in FX["solve_vrp_problem"]:
+        assert set(r) == {"tour", "total_time", "unvisited", "date"}
+        assert r["tour"][0] == r["tour"][-1] == 0 and sorted(r["tour"][1:-1]) == list(range(1, 15))

@@ -211,7 +211,7 @@ int vrpms_set_instance(vrpms_ctx* ctx, int32_t problem, const int32_t* d_dur, in
   if (problem != VRPMS_TSP && problem != VRPMS_CVRP)
     return fail(VRPMS_EINVAL, "vrpms_set_instance: unknown problem " + std::to_string(problem));
   if (!d_dur || !d_start) return fail(VRPMS_EINVAL, "vrpms_set_instance: d_dur/d_start NULL");
-  if (N < 2 || N > 65535) return fail(VRPMS_EINVAL, "vrpms_set_instance: N must be in [2, 65535]");
+  if (N < 1 || N > 65535) return fail(VRPMS_EINVAL, "vrpms_set_instance: N must be in [1, 65535]");
   if (H < 1 || H > 1024) return fail(VRPMS_EINVAL, "vrpms_set_instance: H must be in [1, 1024]");
   if ((int64_t)H * N * N >= (1LL << 31))
     return fail(VRPMS_EINVAL, "vrpms_set_instance: H*N*N must stay below 2^31 elements");

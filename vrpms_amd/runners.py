@@ -1,0 +1,205 @@
+"""Epoch-driven search runners over the HIP kernels.
+
+Each runner owns its device state (tours, keys) as torch tensors, advances
+it with one C-ABI call per epoch, and exposes the three operations the
+island model and the front-end need:
+
+  epoch()            advance the search (GPU kernels only)
+  best()             (key, tour) of the best solution seen (device argmin)
+  elites(E) / inject(tours, keys)   migration hooks (islands.py)
+
+Defaults follow the reference's knobs where it has any
+(api/parameters.py:18-23: randomPermutationCount -> population,
+iterationCount -> generations); SA/ACO/BF endpoints declare no knobs
+(api/parameters.py:26-31, 47-56), so their defaults are build-defined.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from .core import Context
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def random_tours(ctx: Context, count: int, n: int, seed: int):
+    """count random permutations of 1..n as int16 rows, generated on the device."""
+    torch = _torch()
+    g = torch.Generator(device=ctx.dev)
+    g.manual_seed(int(seed) & (2**63 - 1))
+    r = torch.rand((count, n), generator=g, device=ctx.dev)
+    return (r.argsort(dim=1) + 1).to(torch.int16).contiguous()
+
+
+def typical_edge(durations) -> float:
+    D = np.asarray(durations, dtype=np.float64)
+    nz = D[D > 0]
+    return float(nz.mean()) if nz.size else 1.0
+
+
+class _Base:
+    def best(self):
+        keys, tours = self._keys_tours()
+        k, i = self.ctx.argmin(keys.reshape(-1))
+        return k, tours.reshape(-1, self.n)[i]
+
+    def elites(self, E: int):
+        torch = _torch()
+        keys, tours = self._keys_tours()
+        flat = keys.reshape(-1)
+        # uint64 order == int64 order after flipping the sign bit
+        order = torch.argsort(flat ^ torch.tensor(-(2**63), device=flat.device), stable=True)[:E]
+        return tours.reshape(-1, self.n)[order].clone(), flat[order].clone()
+
+
+class SARunner(_Base):
+    """Independent SA chains (one wavefront each), geometric cooling from
+    t0 to t_end over `total_steps` steps."""
+
+    def __init__(self, ctx: Context, n: int, chains: int = 1024, seed: int = 0,
+                 total_steps: int = 2000, steps_per_epoch: int = 250, t0: float | None = None,
+                 t_end: float | None = None, durations=None):
+        torch = _torch()
+        self.ctx, self.n, self.seed = ctx, n, seed
+        self.chains = chains
+        edge = typical_edge(durations) if durations is not None else 100.0
+        t0 = t0 if t0 is not None else 0.5 * edge
+        t_end = t_end if t_end is not None else 0.002 * edge
+        self.inv_alpha = np.float32((t0 / t_end) ** (1.0 / max(total_steps, 1)))
+        self.inv_t = np.float32(1.0 / t0)
+        self.steps_per_epoch = steps_per_epoch
+        self.step = 0
+        self.cur = random_tours(ctx, chains, n, seed)
+        self.best_t = self.cur.clone()
+        self.cur_key = torch.empty(chains, dtype=torch.int64, device=ctx.dev)
+        self.best_key = torch.full((chains,), -1, dtype=torch.int64, device=ctx.dev)
+
+    def epoch(self, steps: int | None = None):
+        s = self.steps_per_epoch if steps is None else steps
+        self.ctx.sa_run(self.cur, self.cur_key, self.best_t, self.best_key, s, float(self.inv_t),
+                        float(self.inv_alpha), self.seed, self.step)
+        for _ in range(s):      # same float32 recurrence as the kernel
+            self.inv_t = np.float32(self.inv_t * self.inv_alpha)
+        self.step += s
+
+    def _keys_tours(self):
+        return self.best_key, self.best_t
+
+    def inject(self, tours, keys):
+        """Restart the worst chains from migrant tours."""
+        torch = _torch()
+        E = tours.shape[0]
+        order = torch.argsort(self.cur_key ^ torch.tensor(-(2**63), device=self.cur_key.device),
+                              descending=True, stable=True)[:E]
+        self.cur[order] = tours.to(self.cur.dtype)
+        self.cur_key[order] = keys
+
+
+class GARunner(_Base):
+    """Island GA: `islands` populations of `pop` members."""
+
+    def __init__(self, ctx: Context, n: int, islands: int = 8, pop: int = 256, seed: int = 0,
+                 pmut: float = 0.2, gens_per_epoch: int = 20):
+        self.ctx, self.n, self.seed = ctx, n, seed
+        self.islands, self.pop, self.pmut = islands, pop, pmut
+        self.gens_per_epoch = gens_per_epoch
+        self.gen = 0
+        self.tours = random_tours(ctx, islands * pop, n, seed).view(islands, pop, n).contiguous()
+        self.keys = ctx.eval(self.tours.view(-1, n)).view(islands, pop)
+
+    def epoch(self, gens: int | None = None):
+        g = self.gens_per_epoch if gens is None else gens
+        self.ctx.ga_generation(self.tours, self.keys, g, self.pmut, self.seed, self.gen)
+        self.gen += g
+
+    def _keys_tours(self):
+        return self.keys, self.tours
+
+    def inject(self, tours, keys):
+        """Migrants replace the worst member of each island (round robin)."""
+        E = tours.shape[0]
+        for e in range(E):
+            isl = e % self.islands
+            slot = self.pop - 1 - (e // self.islands)
+            if slot < 0:
+                break
+            self.tours[isl, slot] = tours[e].to(self.tours.dtype)
+            self.keys[isl, slot] = keys[e]
+        # keep each island sorted by (key, index): the kernel's invariant
+        torch = _torch()
+        for isl in range(self.islands):
+            k = self.keys[isl]
+            order = torch.argsort(k ^ torch.tensor(-(2**63), device=k.device), stable=True)
+            self.keys[isl] = k[order]
+            self.tours[isl] = self.tours[isl][order]
+
+
+class ACORunner(_Base):
+    """Integer max-min ant colonies (one pheromone matrix per colony)."""
+
+    def __init__(self, ctx: Context, n: int, colonies: int = 4, ants: int = 64, seed: int = 0,
+                 iters_per_epoch: int = 5, evap_shift: int = 3):
+        torch = _torch()
+        if n != ctx.N - 1:
+            raise ValueError("ACO builds complete giant tours: n must be N - 1")
+        self.ctx, self.n, self.seed = ctx, n, seed
+        self.colonies, self.ants = colonies, ants
+        self.iters_per_epoch, self.evap_shift = iters_per_epoch, evap_shift
+        self.tau_max, self.tau_min = 1 << 30, 1 << 12
+        self.tau, self.eta = ctx.aco_init(colonies, 1 << 24)
+        self.it = 0
+        self.best_key = torch.full((colonies,), -1, dtype=torch.int64, device=ctx.dev)
+        self.best_t = torch.zeros((colonies, n), dtype=torch.int16, device=ctx.dev)
+
+    def epoch(self, iters: int | None = None):
+        torch = _torch()
+        for _ in range(self.iters_per_epoch if iters is None else iters):
+            tours, keys, ib = self.ctx.aco_iteration(self.tau, self.eta, self.ants, self.seed,
+                                                     self.it, self.evap_shift, self.tau_min,
+                                                     self.tau_max)
+            self.it += 1
+            k = ib[:, 0]
+            better = (k ^ torch.tensor(-(2**63), device=k.device)) < \
+                (self.best_key ^ torch.tensor(-(2**63), device=k.device))
+            idx = ib[:, 1].clamp(0, self.ants - 1)
+            cand = tours[torch.arange(self.colonies, device=k.device), idx]
+            self.best_key = torch.where(better, k, self.best_key)
+            self.best_t = torch.where(better[:, None], cand, self.best_t)
+
+    def _keys_tours(self):
+        return self.best_key, self.best_t
+
+    def inject(self, tours, keys):
+        """Migrant tours are deposited on every colony like an iteration-best."""
+        torch = _torch()
+        m = min(tours.shape[0], self.colonies)
+        k = keys[:m]
+        better = (k ^ torch.tensor(-(2**63), device=k.device)) < \
+            (self.best_key[:m] ^ torch.tensor(-(2**63), device=k.device))
+        self.best_key[:m] = torch.where(better, k, self.best_key[:m])
+        self.best_t[:m] = torch.where(better[:, None], tours[:m].to(self.best_t.dtype),
+                                      self.best_t[:m])
+
+
+def brute_force(ctx: Context, n: int, rank_begin: int = 0, rank_end: int | None = None):
+    """Exact optimum over lexicographic ranks [begin, end) -> (key, tour)."""
+    if rank_end is None:
+        rank_end = math.factorial(n)
+    key, rank = ctx.bf_run(n, rank_begin, rank_end)
+    return key, unrank(rank, n) if rank != 2**64 - 1 else None
+
+
+def unrank(rank: int, n: int):
+    """Lexicographic rank -> permutation of 1..n (host-side index arithmetic)."""
+    avail = list(range(1, n + 1))
+    out = []
+    for i in range(n):
+        f = math.factorial(n - 1 - i)
+        d, rank = divmod(rank, f)
+        out.append(avail.pop(d))
+    return out
