@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU work for the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--quality-seconds", type=float, default=5.0,
+                    help="wall time per side for the best-cost gap (0 disables)")
     return ap.parse_args()
 
 
@@ -79,6 +81,84 @@ def cpu_baseline(inst, perms_dev, seconds):
             "sample": f"{passes} pass(es) over the first {S} of the same CVRP-100 tours, C "
                       f"restatement oracle/oracle_c.c (OpenMP, {threads} threads), "
                       f"{dt:.2f} s"}, ref, S
+
+
+def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096):
+    """Best-cost gap at fixed wall time (the metric's second half): the same SA
+    (Philox streams, 64 sampled moves per step, geometric cooling from
+    0.5 to 0.002 x the mean edge) on the GPU -- `chains` wavefront chains with
+    elite migration every 5 epochs (across ranks when N > 1) -- and on the host
+    cores (oracle/oracle_c.c, one chain per OpenMP thread), each running as
+    many steps as fit in `seconds`.  gap = (gpu - cpu) / cpu on durationSum."""
+    import numpy as np
+    import torch
+    from vrpms_amd import islands, runners
+    n = inst.n
+    dev = ctx.dev
+    probe = runners.SARunner(ctx, n, chains=chains, total_steps=1000, durations=inst.durations)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    probe.epoch(100)
+    torch.cuda.synchronize(dev)
+    rate = 100 / (time.perf_counter() - t0)
+    del probe
+    total = max(1000, int(rate * seconds * 0.95))
+    per_epoch = max(50, total // 40)
+    r = runners.SARunner(ctx, n, chains=chains, seed=1000 + rank, total_steps=total,
+                         steps_per_epoch=per_epoch, durations=inst.durations)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    e = 0
+    while r.step < total and time.perf_counter() - t0 < seconds:
+        r.epoch()
+        e += 1
+        if e % 5 == 0:
+            if world > 1:
+                islands.exchange(r, 16)
+            else:
+                r.inject(*r.elites(16))
+        torch.cuda.synchronize(dev)
+    gpu_wall = time.perf_counter() - t0
+    key, tour = r.best()
+    if world > 1:
+        key, _ = islands.global_best(key, tour.cpu().tolist(), n, device=dev)
+    out = {"T_s": seconds, "algorithm": "sa", "instance": "cvrp100_k8 seed 0",
+           "gpu": {"chains_per_gpu": chains, "steps_per_chain": r.step, "wall_s": gpu_wall,
+                   "unvisited": key >> 56, "duration_sum": (key >> 28) & (2**28 - 1)}}
+    if with_cpu:
+        from oracle import coracle
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or coracle.max_threads()
+        cur = np.asarray(runners.random_tours(ctx, threads, n, 7).cpu().numpy()).view(np.uint16)
+        cur = cur.copy()
+        best = cur.copy()
+        bk = np.full(threads, 2**64 - 1, dtype=np.uint64)
+        t0 = time.perf_counter()
+        coracle.sa_run(inst.durations, cur.copy(), best.copy(), bk.copy(), 200, 1.0, 1.0, 1, 0,
+                       inst.demand, inst.capacities, inst.start_times, threads=threads)
+        crate = 200 / (time.perf_counter() - t0)
+        ctotal = max(1000, int(crate * seconds * 0.95))
+        edge = runners.typical_edge(inst.durations)
+        inv_a = np.float32((0.5 / 0.002) ** (1.0 / ctotal))
+        inv_t = np.float32(1.0 / (0.5 * edge))
+        step, t0 = 0, time.perf_counter()
+        chunk = max(50, ctotal // 40)
+        while step < ctotal and time.perf_counter() - t0 < seconds:
+            coracle.sa_run(inst.durations, cur, best, bk, chunk, float(inv_t), float(inv_a), 1,
+                           step, inst.demand, inst.capacities, inst.start_times, threads=threads)
+            for _ in range(chunk):
+                inv_t = np.float32(inv_t * inv_a)
+            step += chunk
+        cpu_wall = time.perf_counter() - t0
+        ck = int(bk.min())
+        out["cpu"] = {"chains": threads, "cores": threads, "steps_per_chain": step,
+                      "wall_s": cpu_wall, "unvisited": ck >> 56,
+                      "duration_sum": (ck >> 28) & (2**28 - 1),
+                      "kind": "port (oracle/oracle_c.c oracle_sa_run)"}
+        g, c = out["gpu"]["duration_sum"], out["cpu"]["duration_sum"]
+        out["gap"] = (g - c) / c if c else None
+        out["gap_sign"] = "negative = GPU better"
+    return out
 
 
 def pmc_traffic(kernel, grid):
@@ -154,6 +234,10 @@ def main():
     value = C * args.steps * world / wall
     rows_wall, rows_ms = timed(lambda: ctx.eval(perms, out=keys_rows), max(3, args.steps // 4),
                                1, False)
+    qual = None
+    if args.quality_seconds > 0:
+        qual = quality(ctx, inst, args.quality_seconds, world, rank, dist,
+                       with_cpu=(world == 1 and rank == 0 and not args.no_cpu_baseline))
 
     if rank == 0:
         nbytes = 4 * ((n + 3) // 4)
@@ -190,6 +274,8 @@ def main():
         import numpy as np
         same = bool(torch.equal(keys, keys_rows))
         out["rows_vs_words_identical"] = same
+        if qual is not None:
+            out["quality"] = qual
         if world == 1 and not args.no_cpu_baseline:
             cb, ref, S = cpu_baseline(inst, perms, args.cpu_seconds)
             got = keys[:S].cpu().numpy().view(np.uint64)

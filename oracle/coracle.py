@@ -30,6 +30,10 @@ def load():
         lib.oracle_eval_batch.argtypes = [i32, vp, i32, i32, vp, vp, vp, i32, i32, vp, vp, i64,
                                           i32, i64, vp, vp, vp, vp, i32]
         lib.oracle_max_threads.restype = ctypes.c_int
+        f32, u64 = ctypes.c_float, ctypes.c_uint64
+        lib.oracle_sa_run.restype = ctypes.c_int
+        lib.oracle_sa_run.argtypes = [i32, vp, i32, i32, vp, vp, vp, i32, i32, vp, vp, vp, vp, i32,
+                                      i32, i32, f32, f32, u64, u64, i32]
         _lib = lib
     return _lib
 
@@ -63,6 +67,28 @@ def eval_batch(durations, perms, demand=None, capacities=None, start_times=(0,),
     lib.oracle_eval_batch(problem, _p(D), H, N, _p(dem), _p(cap), _p(st), K, objective, _p(p8),
                           _p(p16), C, n, ld, _p(keys), _p(sums), _p(maxs), _p(unv), threads)
     return keys, sums, maxs, unv
+
+
+def sa_run(durations, cur, best, best_key, steps, inv_t0, inv_alpha, seed, step0,
+           demand=None, capacities=None, start_times=(0,), problem: int = 1, objective: int = 0,
+           threads: int = 0):
+    """C/OpenMP SA (same streams as vrpms_sa_run); cur/best uint16 [chains][n]
+    and best_key uint64 [chains] are updated in place; returns cur_key."""
+    lib = load()
+    D = np.ascontiguousarray(np.asarray(durations, dtype=np.int32).reshape(
+        (-1,) + np.asarray(durations).shape[-2:]))
+    H, N = D.shape[0], D.shape[1]
+    st = np.ascontiguousarray(np.asarray(start_times, dtype=np.int32).reshape(-1))
+    dem = None if demand is None else np.ascontiguousarray(np.asarray(demand, dtype=np.int32))
+    cap = None if capacities is None else np.ascontiguousarray(np.asarray(capacities, dtype=np.int32))
+    assert cur.dtype == np.uint16 and best.dtype == np.uint16 and best_key.dtype == np.uint64
+    chains, n = cur.shape
+    cur_key = np.empty(chains, dtype=np.uint64)
+    lib.oracle_sa_run(problem, _p(D), H, N, _p(dem), _p(cap), _p(st), st.shape[0], objective,
+                      _p(cur), _p(cur_key), _p(best), _p(best_key), chains, n, int(steps),
+                      float(inv_t0), float(inv_alpha), int(seed) & (2**64 - 1), int(step0),
+                      threads)
+    return cur_key
 
 
 def max_threads() -> int:

@@ -12,6 +12,7 @@
  * Arithmetic is int64 here (the spec uses unbounded ints); the A9 guard
  * keeps every value inside int32 for the device.
  */
+#include <math.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -113,6 +114,205 @@ int oracle_eval_batch(int problem, const int32_t* D, int H, int N, const int32_t
     if (sums) sums[c] = (int32_t)s;
     if (maxs) maxs[c] = (int32_t)m;
     if (unvs) unvs[c] = (int32_t)u;
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------------------
+ * SA restatement (oracle/search.py sa_run, SURVEY.md §8a' sa_chain_step):
+ * per chain and step, 64 Philox-sampled moves are scored, the best
+ * (key, lane) is accepted if no worse or if (u >> 8) < threshold(dp, invT).
+ * Used as the CPU solver at equal wall time (bench.py "quality") and as a
+ * large-size parity check of the GPU SA.  Build with -ffp-contract=off.
+ * ---------------------------------------------------------------------- */
+typedef struct {
+  uint32_t x, y, z, w;
+} u32x4;
+
+static u32x4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                    uint32_t k1) {
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c0 = n0;
+    c1 = (uint32_t)p1;
+    c2 = n2;
+    c3 = (uint32_t)p0;
+  }
+  u32x4 o = {c0, c1, c2, c3};
+  return o;
+}
+
+typedef struct {
+  int typ, i, j;
+} move_t;
+
+static move_t decode_move(uint32_t r0, uint32_t r1, uint32_t r2, int n) {
+  move_t m;
+  m.typ = (int)(r0 % 3u);
+  m.i = (int)(r1 % (uint32_t)n);
+  m.j = (int)(r2 % (uint32_t)(n - 1));
+  if (m.j >= m.i) ++m.j;
+  if (m.typ != 2 && m.i > m.j) {
+    int t = m.i;
+    m.i = m.j;
+    m.j = t;
+  }
+  return m;
+}
+
+static inline int moved_index(int q, const move_t* m) {
+  int i = m->i, j = m->j;
+  if (m->typ == 0) return q == i ? j : (q == j ? i : q);
+  if (m->typ == 1) return (q >= i && q <= j) ? i + j - q : q;
+  if (i < j) {
+    if (q < i || q > j) return q;
+    return q == j ? i : q + 1;
+  }
+  if (q < j || q > i) return q;
+  return q == j ? i : q - 1;
+}
+
+typedef struct {
+  int problem, H, N, K, objective;
+  const int32_t *D, *dem, *cap, *st;
+} inst_t;
+
+/* key of tour T read through move m (m == NULL: identity) */
+static uint64_t tour_key(const inst_t* I, const uint16_t* T, int n, const move_t* m) {
+  if (I->problem == 0) {
+    int64_t t = I->st[0];
+    int prev = 0;
+    for (int q = 0; q < n; ++q) {
+      int x = T[m ? moved_index(q, m) : q];
+      t += edge(I->D, I->H, I->N, t, prev, x);
+      prev = x;
+    }
+    t += edge(I->D, I->H, I->N, t, prev, 0);
+    return pack_key(0, t - I->st[0], 0);
+  }
+  int k = 0, prev = 0, K = I->K;
+  int64_t load = 0, t = K ? I->st[0] : 0, s = 0, mx = 0, u = 0;
+  for (int q = 0; q < n; ++q) {
+    int x = T[m ? moved_index(q, m) : q];
+    while (k < K && load + I->dem[x] > I->cap[k]) {
+      if (prev != 0) {
+        int64_t rd = t + edge(I->D, I->H, I->N, t, prev, 0) - I->st[k];
+        s += rd;
+        if (rd > mx) mx = rd;
+      }
+      ++k;
+      if (k < K) {
+        load = 0;
+        t = I->st[k];
+        prev = 0;
+      }
+    }
+    if (k >= K) {
+      ++u;
+      continue;
+    }
+    t += edge(I->D, I->H, I->N, t, prev, x);
+    load += I->dem[x];
+    prev = x;
+  }
+  if (k < K && prev != 0) {
+    int64_t rd = t + edge(I->D, I->H, I->N, t, prev, 0) - I->st[k];
+    s += rd;
+    if (rd > mx) mx = rd;
+  }
+  return I->objective ? pack_key(u, mx, s) : pack_key(u, s, mx);
+}
+
+static uint32_t accept_threshold(uint32_t dp, float invT) {
+  if (dp == 0) return 1u << 24;
+  float x = (float)dp * invT;
+  float y = x * 0x1.715476p+0f;
+  if (!(y < 24.0f)) return 0u;
+  float kf = floorf(y);
+  float f = y - kf;
+  float g = f * 0x1.62e43p-1f;
+  float p = 0x1.6c16c2p-10f;
+  p = p * g;
+  p = 0x1.111112p-7f - p;
+  p = p * g;
+  p = 0x1.555556p-5f - p;
+  p = p * g;
+  p = 0x1.555556p-3f - p;
+  p = p * g;
+  p = 0.5f - p;
+  p = p * g;
+  p = 1.0f - p;
+  p = p * g;
+  p = 1.0f - p;
+  int k = (int)kf;
+  float scaled = p * (float)(1u << (24 - k));
+  return (uint32_t)scaled;
+}
+
+int oracle_sa_run(int problem, const int32_t* D, int H, int N, const int32_t* dem,
+                  const int32_t* cap, const int32_t* st, int K, int objective, uint16_t* cur,
+                  uint64_t* cur_key, uint16_t* best, uint64_t* best_key, int chains, int n,
+                  int steps, float inv_t0, float inv_alpha, uint64_t seed, uint64_t step0,
+                  int threads) {
+  inst_t I = {problem, H, N, K, objective, D, dem, cap, st};
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+  for (int c = 0; c < chains; ++c) {
+    uint16_t* A = cur + (int64_t)c * n;
+    uint16_t* Bst = best + (int64_t)c * n;
+    uint16_t tmp[65536];
+    uint64_t ck = tour_key(&I, A, n, NULL), bk = best_key[c];
+    if (ck < bk) {
+      bk = ck;
+      memcpy(Bst, A, (size_t)n * 2);
+    }
+    float invT = inv_t0;
+    for (int s = 0; s < steps && n >= 2; ++s) {
+      uint64_t step = step0 + (uint64_t)s;
+      uint64_t kbest = ~0ull;
+      int lbest = 0;
+      move_t mbest = {0, 0, 0};
+      uint32_t wbest = 0;
+      for (int lane = 0; lane < 64; ++lane) {
+        u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)c, (uint32_t)lane, k0,
+                         k1);
+        move_t m = decode_move(r.x, r.y, r.z, n);
+        uint64_t kk = tour_key(&I, A, n, &m);
+        if (kk < kbest) {
+          kbest = kk;
+          lbest = lane;
+          mbest = m;
+          wbest = r.w;
+        }
+      }
+      (void)lbest;
+      int acc = kbest <= ck;
+      if (!acc) {
+        uint64_t d = (kbest >> 28) - (ck >> 28);
+        uint32_t dp = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
+        acc = (wbest >> 8) < accept_threshold(dp, invT);
+      }
+      if (acc) {
+        for (int q = 0; q < n; ++q) tmp[q] = A[moved_index(q, &mbest)];
+        memcpy(A, tmp, (size_t)n * 2);
+        ck = kbest;
+        if (ck < bk) {
+          bk = ck;
+          memcpy(Bst, A, (size_t)n * 2);
+        }
+      }
+      invT = invT * inv_alpha;
+    }
+    cur_key[c] = ck;
+    best_key[c] = bk;
   }
   return 0;
 }

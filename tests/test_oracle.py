@@ -125,6 +125,38 @@ def test_c_restatement_matches_python_spec(coracle):
                     assert (np.asarray(a).astype(np.int64) == np.asarray(b).astype(np.int64)).all()
 
 
+@pytest.mark.parametrize("kind", ["cvrp", "td", "tsp"])
+def test_c_sa_matches_python_replay(coracle, kind):
+    from oracle import search
+    inst = {"cvrp": synth.cvrp(11, 3, seed=2, slack=0.9), "td": synth.td_cvrp(9, 2, seed=3),
+            "tsp": synth.tsp20(4)}[kind]
+    if kind == "tsp":
+        inst = synth.Instance("t9", inst.durations[:, :10, :10], None, None, np.array([0]), "tsp")
+    P = synth.random_perms(2, inst.n, seed=11).astype(np.uint16)
+    cur, best = P.copy(), P.copy()
+    bk = np.full(2, 2**64 - 1, dtype=np.uint64)
+    ck = coracle.sa_run(inst.durations, cur, best, bk, 15, 1 / 150.0, 1 / 0.95, 77, 5,
+                        inst.demand, inst.capacities, inst.start_times,
+                        problem=0 if kind == "tsp" else 1)
+    sc = search.Scorer(inst.durations, inst.demand, inst.capacities, inst.start_times,
+                       inst.problem)
+    ref = search.sa_run(sc, P.tolist(), P.tolist(), [2**64 - 1] * 2, 77, 5, 15, 1 / 150.0,
+                        1 / 0.95)
+    assert cur.tolist() == ref[0] and [int(x) for x in ck] == ref[1]
+    assert best.tolist() == ref[2] and [int(x) for x in bk] == ref[3]
+
+
+def test_accept_threshold_tracks_exp():
+    from oracle import search
+    for dp in [1, 5, 37, 400, 2000]:
+        for invT in [1e-3, 0.01, 0.05, 0.2]:
+            want = int(2**24 * np.exp(-dp * np.float32(invT)))
+            got = search.accept_threshold(dp, np.float32(invT))
+            assert abs(got - want) <= 64 + want * 4e-6
+    assert search.accept_threshold(0, 1.0) == 2**24
+    assert search.accept_threshold(10**6, 1.0) == 0
+
+
 def test_brute_force_small_tsp_matches_itertools():
     inst = synth.tsp20(7)
     D = inst.durations[0][:7, :7]

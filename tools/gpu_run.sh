@@ -30,6 +30,7 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     benchq) run bench_quick 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
+    probe) run sa_probe 300 python tools/sa_probe.py ;;
     prof)
       cd /tmp
       run rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv \
