@@ -234,6 +234,7 @@ def main():
     value = C * args.steps * world / wall
     rows_wall, rows_ms = timed(lambda: ctx.eval(perms, out=keys_rows), max(3, args.steps // 4),
                                1, False)
+    r_gather = ctx.probe_lds_gather(slots=inst.N * inst.N) if rank == 0 else None
     qual = None
     if args.quality_seconds > 0:
         qual = quality(ctx, inst, args.quality_seconds, world, rank, dist,
@@ -271,6 +272,15 @@ def main():
             "rows_layout": {"kernel": "eval_cvrp_packed", "evals_per_s": C / (rows_ms * 1e-3),
                             "kernel_ms": rows_ms},
         }
+        # north-star roofline: random LDS gathers, G = n + K per eval,
+        # R_gather measured by vrpms_probe_lds_gather on this device
+        evals_s = C / (kernel_ms * 1e-3)
+        G = n + inst.K
+        out["lds_gather_roofline"] = {
+            "r_gather_measured": r_gather, "unit": "gathers/s", "G_per_eval": G,
+            "achieved": evals_s * G, "frac": evals_s * G / r_gather,
+            "issued_per_eval": n, "frac_issued": evals_s * n / r_gather,
+            "probe": "random ds_read_b64 over an N*N u64 LDS table, 1024-lane WGs, 2/CU"}
         import numpy as np
         same = bool(torch.equal(keys, keys_rows))
         out["rows_vs_words_identical"] = same

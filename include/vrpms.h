@@ -196,6 +196,12 @@ int vrpms_aco_iteration(vrpms_ctx* ctx, const vrpms_aco_params* p, uint32_t* d_t
 int vrpms_bf_run(vrpms_ctx* ctx, int32_t n, uint64_t rank_begin, uint64_t rank_end,
                  uint64_t* d_out, void* stream);
 
+/* Roofline probe (measurement only): `blocks` x 1024 lanes each issue
+ * 4 * iters random ds_read_b64 gathers over a `slots`-entry u64 table staged
+ * in LDS -- the measured random LDS-gather ceiling R_gather of SURVEY.md §8d. */
+int vrpms_probe_lds_gather(vrpms_ctx* ctx, const uint64_t* d_table, int32_t slots, int32_t iters,
+                           int32_t blocks, uint64_t* d_sink, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -70,6 +70,7 @@ SIGNATURES = {
     "vrpms_aco_iteration": (_c.c_int, [_vp, _c.POINTER(AcoParams), _vp, _vp, _vp, _vp, _vp,
                                        _i32, _vp]),
     "vrpms_bf_run": (_c.c_int, [_vp, _i32, _u64, _u64, _vp, _vp]),
+    "vrpms_probe_lds_gather": (_c.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp]),
 }
 
 

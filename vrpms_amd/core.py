@@ -242,6 +242,25 @@ class Context:
         return k & (2**64 - 1), r & (2**64 - 1)
 
 
+    def probe_lds_gather(self, slots: int = 101 * 101, iters: int = 4096, blocks: int | None = None,
+                         reps: int = 5):
+        """Measured random ds_read_b64 gather rate (gathers/s), best of `reps`."""
+        torch = _torch()
+        blocks = blocks or 2 * 256
+        table = torch.randint(0, 2**62, (slots,), dtype=torch.int64, device=self.dev)
+        sink = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        best = 0.0
+        for _ in range(reps + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            check(self.lib.vrpms_probe_lds_gather(self._ctx, table.data_ptr(), slots, iters,
+                                                  blocks, sink.data_ptr(), self.stream()))
+            e1.record()
+            torch.cuda.synchronize(self.dev)
+            best = max(best, blocks * 1024 * 4 * iters / (e0.elapsed_time(e1) * 1e-3))
+        return best
+
+
 def keys_to_u64(keys) -> np.ndarray:
     """int64 tensor of A8 keys -> numpy uint64 (bit-identical view)."""
     return keys.cpu().numpy().view(np.uint64)
