@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU work for the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-other-configs", action="store_true")
     ap.add_argument("--quality-seconds", type=float, default=5.0,
                     help="wall time per side for the best-cost gap (0 disables)")
     return ap.parse_args()
@@ -158,6 +159,59 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096):
         g, c = out["gpu"]["duration_sum"], out["cpu"]["duration_sum"]
         out["gap"] = (g - c) / c if c else None
         out["gap_sign"] = "negative = GPU better"
+    return out
+
+
+def other_configs(ctx, torch, dev, seed=0):
+    """Secondary lines for the other BASELINE.json configs (not the headline)."""
+    from vrpms_amd import synth
+    from vrpms_amd.core import CVRP
+    out = {}
+
+    def kernel_time(fn, reps=5):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(dev)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize(dev)
+        return e0.elapsed_time(e1) * 1e-3 / reps
+
+    # cfg 3: time-dependent VRP-200 x 24 h (4.0 MB int32 / 1.9 MB u16: L2-resident gathers)
+    td = synth.td_cvrp(200, 16, seed=seed)
+    ctx.set_instance(CVRP, td.durations, td.demand, td.capacities, td.start_times)
+    C = 1 << 21
+    perms = make_batch(torch, C, td.n, dev, seed + 11)
+    keys = torch.empty(C, dtype=torch.int64, device=dev)
+    t = kernel_time(lambda: ctx.eval(perms, out=keys))
+    out["cfg3_tdvrp200_h24"] = {"kernel": "eval_generic<u16, L2, H=24>", "evals_per_s": C / t,
+                                "candidates": C, "gathers_per_eval": td.n + td.K}
+    # cfg 4: X-style CVRP-1000 (uint16 tours, 2.0 MB u16 matrix: L2-resident)
+    x = synth.x_style(1000, seed=seed)
+    ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
+    C = 1 << 18
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed + 13)
+    p16 = torch.empty((C, x.n), dtype=torch.int16, device=dev)
+    for s in range(0, C, 1 << 15):
+        r = torch.rand((min(C, s + (1 << 15)) - s, x.n), generator=g, device=dev)
+        p16[s:s + r.shape[0]] = (r.argsort(dim=1) + 1).to(torch.int16)
+    keys = torch.empty(C, dtype=torch.int64, device=dev)
+    t = kernel_time(lambda: ctx.eval(p16, out=keys))
+    out["cfg4_x1000"] = {"kernel": "eval_generic<u16, L2>", "evals_per_s": C / t,
+                         "candidates": C, "vehicles": x.K, "gathers_per_eval": x.n + x.K}
+    # cfg 5: throughput mode, 10k concurrent TSP-50 requests, one workgroup per request
+    R, steps = 10000, 1000
+    rng = np.random.default_rng(seed)
+    mats = torch.tensor(np.stack([synth.random_symmetric(50, rng) for _ in range(R)]),
+                        dtype=torch.int32, device=dev)
+    t = kernel_time(lambda: ctx.tsp_batch_sa(mats, steps, 1 / 80.0, 1 / 0.995, 1), reps=3)
+    out["cfg5_tsp50_x10k"] = {"kernel": "tsp_batch_sa_kernel (1 WG / request, 4 chains)",
+                              "requests_per_s": R / t, "batch_latency_ms": t * 1e3,
+                              "sa_steps_per_chain": steps,
+                              "move_evals_per_s": R * 4 * steps * 64 / t}
     return out
 
 
@@ -291,6 +345,9 @@ def main():
             got = keys[:S].cpu().numpy().view(np.uint64)
             cb["parity_on_sample"] = bool((got == ref[0]).all())
             out["cpu_baseline"] = cb
+        if world == 1 and not args.no_other_configs:
+            del perms, words
+            out["other_configs"] = other_configs(ctx, torch, dev)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

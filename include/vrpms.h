@@ -196,6 +196,17 @@ int vrpms_aco_iteration(vrpms_ctx* ctx, const vrpms_aco_params* p, uint32_t* d_t
 int vrpms_bf_run(vrpms_ctx* ctx, int32_t n, uint64_t rank_begin, uint64_t rank_end,
                  uint64_t* d_out, void* stream);
 
+/* Throughput mode (BASELINE.json config 5: many concurrent TSP requests):
+ * R independent static TSP requests, each with its own int32 [N][N] matrix
+ * (d_mats [R][N][N], node 0 = start node), ONE WORKGROUP PER REQUEST: 4 SA
+ * chains per request from Philox Fisher-Yates starts, moves priced by exact
+ * O(1) integer deltas (2-opt re-prices the reversed segment when the matrix
+ * is asymmetric).  Uses p->steps, inv_t0, inv_alpha, seed (chains/step0
+ * ignored).  Out: d_best_tours [R][N-1], d_best_keys [R].  No instance needed. */
+int vrpms_tsp_batch_sa(vrpms_ctx* ctx, const int32_t* d_mats, int32_t R, int32_t N,
+                       const vrpms_sa_params* p, uint16_t* d_best_tours, uint64_t* d_best_keys,
+                       void* stream);
+
 /* Roofline probe (measurement only): `blocks` x 1024 lanes each issue
  * 4 * iters random ds_read_b64 gathers over a `slots`-entry u64 table staged
  * in LDS -- the measured random LDS-gather ceiling R_gather of SURVEY.md §8d. */

@@ -118,6 +118,53 @@ def sa_run(score: Scorer, cur_tours, best_tours, best_keys, seed: int, step0: in
     return cur_out, ck_out, best_out, bk_out
 
 
+def tsp_batch_sa(mats, steps: int, inv_t0: float, inv_alpha: float, seed: int):
+    """vrpms_tsp_batch_sa: per request 4 chains (Philox Fisher-Yates starts,
+    counters (0xffffffff, 0xffffffff, 4r + w, i)), SA steps with counters
+    (s, 0, 4r + w, lane); best (key, wave).  Costs by full re-evaluation --
+    the device prices moves by O(1) deltas, so equality checks the deltas."""
+    key = spec.seed_key(seed)
+    out_t, out_k = [], []
+    for r, D in enumerate(mats):
+        D = np.asarray(D)
+        n = D.shape[0] - 1
+        score = Scorer(D, problem="tsp")
+        best = None
+        for w in range(4):
+            cid = 4 * r + w
+            t = list(range(1, n + 1))
+            for i in range(n - 1, 0, -1):
+                x = spec.philox4x32_10((M32, M32, cid, i), key)
+                j = x[0] % (i + 1)
+                t[i], t[j] = t[j], t[i]
+            ck = score(t)
+            bk, bt = ck, t[:]
+            invT = _F(inv_t0)
+            if n >= 2:
+                for s in range(steps):
+                    cands = []
+                    for lane in range(64):
+                        rr = spec.philox4x32_10((s, 0, cid, lane), key)
+                        m = spec.decode_move(rr[0], rr[1], rr[2], n)
+                        cands.append((score(spec.apply_move(t, *m)), lane, m, rr[3]))
+                    kk, lane, m, r3 = min(cands, key=lambda c: (c[0], c[1]))
+                    acc = kk <= ck
+                    if not acc:
+                        dp = min((kk >> 28) - (ck >> 28), M32)
+                        acc = (r3 >> 8) < accept_threshold(dp, invT)
+                    if acc:
+                        t = spec.apply_move(t, *m)
+                        ck = kk
+                        if ck < bk:
+                            bk, bt = ck, t[:]
+                    invT = _F(invT * _F(inv_alpha))
+            if best is None or bk < best[0]:
+                best = (bk, bt)
+        out_k.append(best[0])
+        out_t.append(best[1])
+    return out_t, out_k
+
+
 # ---------------------------------------------------------------------------
 # GA: tournament(2) x 2, OX1, Philox-gated mutation, (mu + lambda) survivors
 # ---------------------------------------------------------------------------

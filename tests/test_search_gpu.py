@@ -103,6 +103,42 @@ def test_sa_cvrp100_matches_c_restatement(ctx, coracle):
     assert (best.cpu().numpy().view(np.uint16) == cbest).all()
 
 
+@pytest.mark.parametrize("symmetric", [True, False])
+def test_tsp_batch_matches_oracle(ctx, symmetric):
+    """Config-5 throughput kernel: O(1)-delta SA == full-evaluation replay."""
+    torch = torch_()
+    rng = np.random.default_rng(4)
+    mats = []
+    for r in range(3):
+        if symmetric:
+            mats.append(synth.random_symmetric(9, rng))
+        else:
+            m = rng.integers(3, 320, size=(9, 9))
+            np.fill_diagonal(m, 0)
+            mats.append(m)
+    M = torch.tensor(np.array(mats), dtype=torch.int32, device=ctx.dev)
+    tours, keys = ctx.tsp_batch_sa(M, steps=25, inv_t0=1 / 60.0, inv_alpha=1 / 0.97, seed=31)
+    rt, rk = search.tsp_batch_sa(mats, 25, 1 / 60.0, 1 / 0.97, 31)
+    assert tours.cpu().numpy().tolist() == rt
+    assert u64(keys) == rk
+
+
+def test_tsp_batch_tsp50_invariants(ctx):
+    torch = torch_()
+    rng = np.random.default_rng(0)
+    R = 300
+    mats = np.stack([synth.random_symmetric(50, rng) for _ in range(R)])
+    M = torch.tensor(mats, dtype=torch.int32, device=ctx.dev)
+    tours, keys = ctx.tsp_batch_sa(M, steps=400, inv_t0=1 / 80.0, inv_alpha=1 / 0.99, seed=2)
+    T = tours.cpu().numpy()
+    K = u64(keys)
+    for r in range(0, R, 37):
+        assert sorted(T[r]) == list(range(1, 50))
+        assert K[r] == spec.tsp_key(spec.eval_tsp(mats[r], T[r]))
+    rand = np.mean([spec.eval_tsp(mats[r], rng.permutation(np.arange(1, 50))) for r in range(20)])
+    assert np.mean([k >> 28 for k in K]) < 0.5 * rand
+
+
 def test_sa_large_invariants(ctx):
     torch = torch_()
     inst = synth.cvrp(100, 8, seed=0)

@@ -71,6 +71,8 @@ SIGNATURES = {
                                        _i32, _vp]),
     "vrpms_bf_run": (_c.c_int, [_vp, _i32, _u64, _u64, _vp, _vp]),
     "vrpms_probe_lds_gather": (_c.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp]),
+    "vrpms_tsp_batch_sa": (_c.c_int, [_vp, _vp, _i32, _i32, _c.POINTER(SaParams), _vp, _vp,
+                                      _vp]),
 }
 
 

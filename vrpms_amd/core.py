@@ -242,6 +242,19 @@ class Context:
         return k & (2**64 - 1), r & (2**64 - 1)
 
 
+    def tsp_batch_sa(self, mats, steps: int, inv_t0: float, inv_alpha: float, seed: int):
+        """One workgroup per request: mats int32 [R][N][N] on the device ->
+        (best tours int16 [R][N-1], best keys int64 [R])."""
+        torch = _torch()
+        R, N, _ = mats.shape
+        tours = torch.empty((R, max(N - 1, 1)), dtype=torch.int16, device=self.dev)
+        keys = torch.empty(R, dtype=torch.int64, device=self.dev)
+        p = _lib.SaParams(4 * R, int(steps), float(inv_t0), float(inv_alpha),
+                          int(seed) & (2**64 - 1), 0)
+        check(self.lib.vrpms_tsp_batch_sa(self._ctx, mats.data_ptr(), R, N, ctypes.byref(p),
+                                          tours.data_ptr(), keys.data_ptr(), self.stream()))
+        return tours, keys
+
     def probe_lds_gather(self, slots: int = 101 * 101, iters: int = 4096, blocks: int | None = None,
                          reps: int = 5):
         """Measured random ds_read_b64 gather rate (gathers/s), best of `reps`."""

@@ -627,6 +627,118 @@ __global__ void reduce_pairs_kernel(const uint64_t* in, int count, uint64_t* out
   }
 }
 
+// ===========================================================================
+// Throughput mode (BASELINE.json config 5): a batch of independent static TSP
+// requests, each with its own matrix, ONE WORKGROUP PER REQUEST.  The
+// request's matrix is staged in LDS; its 4 wavefronts run 4 SA chains from
+// Philox Fisher-Yates starts; candidate moves are priced by the exact O(1)
+// integer delta (tsp_move_delta), so a step costs ~8 LDS gathers per lane
+// instead of n; the best (key, wave) of the 4 chains is the answer.
+// ===========================================================================
+struct TspBatchArgs {
+  const int32_t* mats;   // [R][N][N]
+  int R, N, steps;
+  float inv_t0, inv_alpha;
+  uint32_t seed_lo, seed_hi;
+  uint16_t* best_tours;  // [R][N-1]
+  uint64_t* best_keys;   // [R]
+};
+
+__global__ __launch_bounds__(256) void tsp_batch_sa_kernel(TspBatchArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int N = a.N, n = N - 1, r = blockIdx.x;
+  const uint32_t NN = (uint32_t)N * N;
+  int32_t* D = reinterpret_cast<int32_t*>(smem);
+  const int32_t* src = a.mats + (int64_t)r * NN;
+  for (uint32_t i = threadIdx.x; i < NN; i += blockDim.x) D[i] = src[i];
+  __syncthreads();
+  int asym = 0;
+  for (uint32_t i = threadIdx.x; i < NN; i += blockDim.x) {
+    const uint32_t x = i / N, y = i % N;
+    asym |= D[i] != D[y * N + x];
+  }
+  const bool symmetric = __syncthreads_or(asym) == 0;
+  const uint32_t npad = ((uint32_t)n + 7u) & ~7u;
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  uint16_t* buf = reinterpret_cast<uint16_t*>(smem + ((NN * 4 + 15u) & ~15u)) + wave * 3 * npad;
+  uint64_t* wbest = reinterpret_cast<uint64_t*>(smem + ((NN * 4 + 15u) & ~15u) + 4 * 3 * npad * 2);
+  uint16_t* A = buf;
+  uint16_t* B = buf + npad;
+  uint16_t* Best = buf + 2 * npad;
+  const uint32_t cid = (uint32_t)(r * 4 + wave);
+  // Philox Fisher-Yates start (lane 0): for i = n-1..1 swap t[i], t[x % (i+1)]
+  for (int q = lane; q < n; q += 64) A[q] = (uint16_t)(q + 1);
+  wave_sync();
+  if (lane == 0)
+    for (int i = n - 1; i >= 1; --i) {
+      const u32x4 x = philox(0xffffffffu, 0xffffffffu, cid, (uint32_t)i, a.seed_lo, a.seed_hi);
+      const int j = (int)(x.x % (uint32_t)(i + 1));
+      const uint16_t t = A[i];
+      A[i] = A[j];
+      A[j] = t;
+    }
+  wave_sync();
+  auto dist = [&](uint32_t x, uint32_t y) { return D[x * (uint32_t)N + y]; };
+  auto full = [&](const uint16_t* T) {
+    int s = 0;
+    uint32_t prev = 0;
+    for (int q = 0; q < n; ++q) {
+      s += dist(prev, T[q]);
+      prev = T[q];
+    }
+    return s + dist(prev, 0);
+  };
+  int dur = full(A);
+  uint64_t ck = pack_key(0, (uint32_t)dur, 0), bk = ck;
+  for (int q = lane; q < n; q += 64) Best[q] = A[q];
+  float invT = a.inv_t0;
+  for (int s = 0; s < a.steps && n >= 2; ++s) {
+    const u32x4 rr = philox((uint32_t)s, 0u, cid, (uint32_t)lane, a.seed_lo, a.seed_hi);
+    const Move m = decode_move(rr.x, rr.y, rr.z, n);
+    auto tourA = [&](int q) { return (uint32_t)A[q]; };
+    const int nd = dur + tsp_move_delta(dist, tourA, n, m, symmetric);
+    uint64_t k = pack_key(0, (uint32_t)nd, 0);
+    uint64_t who = (uint64_t)lane;
+    wave_argmin(k, who);
+    const int bl = (int)who;
+    bool accept = k <= ck;
+    if (!accept) {
+      const uint64_t d = (k >> 28) - (ck >> 28);
+      const uint32_t dp = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
+      accept = (__shfl(rr.w, bl, 64) >> 8) < accept_threshold(dp, invT);
+    }
+    if (accept) {
+      Move mb;
+      mb.typ = (uint32_t)__shfl((int)m.typ, bl, 64);
+      mb.i = __shfl(m.i, bl, 64);
+      mb.j = __shfl(m.j, bl, 64);
+      dur = __shfl(nd, bl, 64);
+      for (int q = lane; q < n; q += 64) B[q] = A[moved_index(q, mb)];
+      wave_sync();
+      uint16_t* t = A;
+      A = B;
+      B = t;
+      ck = k;
+      if (ck < bk) {
+        bk = ck;
+        for (int q = lane; q < n; q += 64) Best[q] = A[q];
+      }
+      wave_sync();
+    }
+    invT = invT * a.inv_alpha;
+  }
+  if (lane == 0) wbest[wave] = bk;
+  __syncthreads();
+  int bw = 0;
+  for (int w = 1; w < 4; ++w)
+    if (wbest[w] < wbest[bw]) bw = w;
+  if (wave == bw) {
+    uint16_t* out = a.best_tours + (int64_t)r * n;
+    for (int q = lane; q < n; q += 64) out[q] = Best[q];
+    if (lane == 0) a.best_keys[r] = bk;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // dispatch helpers: <MatT, HM, CVRP> from the loaded instance
 // ---------------------------------------------------------------------------
@@ -845,6 +957,28 @@ extern "C" int vrpms_bf_run(vrpms_ctx* ctx, int32_t n, uint64_t rank_begin, uint
   if (rc) return rc;
   reduce_pairs_kernel<<<1, 1024, 0, s>>>(static_cast<uint64_t*>(ctx->search_scratch), blocks,
                                          d_out);
+  VRPMS_HIP(hipGetLastError());
+  return VRPMS_OK;
+}
+
+extern "C" int vrpms_tsp_batch_sa(vrpms_ctx* ctx, const int32_t* d_mats, int32_t R, int32_t N,
+                                  const vrpms_sa_params* p, uint16_t* d_best_tours,
+                                  uint64_t* d_best_keys, void* stream) {
+  if (!ctx || !p) return fail(VRPMS_EINVAL, "vrpms_tsp_batch_sa: NULL ctx/params");
+  if (R < 0 || N < 2 || p->steps < 0) return fail(VRPMS_EINVAL, "vrpms_tsp_batch_sa: bad shape");
+  if (R == 0) return VRPMS_OK;
+  if (!d_mats || !d_best_tours || !d_best_keys)
+    return fail(VRPMS_EINVAL, "vrpms_tsp_batch_sa: NULL buffer");
+  const size_t npad = ((size_t)N - 1 + 7) & ~(size_t)7;
+  const size_t lds = (((size_t)N * N * 4 + 15) & ~(size_t)15) + 4 * 3 * npad * 2 + 4 * 8;
+  if (lds > ctx->max_lds) return fail(VRPMS_EINVAL, "vrpms_tsp_batch_sa: request too large for LDS");
+  VRPMS_HIP(hipSetDevice(ctx->device));
+  TspBatchArgs a{d_mats, R, N, p->steps, p->inv_t0, p->inv_alpha, (uint32_t)p->seed,
+                 (uint32_t)(p->seed >> 32), d_best_tours, d_best_keys};
+  if (lds > 65536)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(tsp_batch_sa_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  tsp_batch_sa_kernel<<<R, 256, lds, (hipStream_t)stream>>>(a);
   VRPMS_HIP(hipGetLastError());
   return VRPMS_OK;
 }

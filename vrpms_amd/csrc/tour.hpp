@@ -140,6 +140,36 @@ VRPMS_DEV int moved_index(int q, const Move& m) {
   return q == j ? i : q - 1;
 }
 
+// Exact duration change of the static closed tour 0 -> T[0..n-1] -> 0 under
+// move m (integer, so duration + delta == a full re-evaluation).  Swap and
+// relocate touch at most 8 edges; 2-opt touches 4 on a symmetric matrix and
+// additionally re-prices the reversed segment otherwise.  `d(a, b)` is D[a][b].
+template <typename Dist, typename Tour>
+VRPMS_DEV int tsp_move_delta(const Dist& d, const Tour& T, int n, const Move& m, bool symmetric) {
+  auto at = [&](int q) -> uint32_t { return (q < 0 || q >= n) ? 0u : (uint32_t)T(q); };
+  const int i = m.i, j = m.j;
+  if (m.typ == kMoveSwap) {  // i < j
+    const uint32_t a = at(i - 1), pi = at(i), pj = at(j), b = at(j + 1);
+    if (j == i + 1) return d(a, pj) + d(pj, pi) + d(pi, b) - d(a, pi) - d(pi, pj) - d(pj, b);
+    const uint32_t x = at(i + 1), y = at(j - 1);
+    return d(a, pj) + d(pj, x) + d(y, pi) + d(pi, b) - d(a, pi) - d(pi, x) - d(y, pj) - d(pj, b);
+  }
+  if (m.typ == kMove2Opt) {  // reverse T[i..j], i < j
+    const uint32_t a = at(i - 1), pi = at(i), pj = at(j), b = at(j + 1);
+    int delta = d(a, pj) + d(pi, b) - d(a, pi) - d(pj, b);
+    if (!symmetric)
+      for (int q = i; q < j; ++q) delta += d(at(q + 1), at(q)) - d(at(q), at(q + 1));
+    return delta;
+  }
+  if (i < j) {  // relocate T[i] to position j (later)
+    const uint32_t a = at(i - 1), pi = at(i), x = at(i + 1), pj = at(j), b = at(j + 1);
+    return d(a, x) + d(pj, pi) + d(pi, b) - d(a, pi) - d(pi, x) - d(pj, b);
+  }
+  // relocate T[i] to position j (earlier)
+  const uint32_t a = at(j - 1), pj = at(j), y = at(i - 1), pi = at(i), b = at(i + 1);
+  return d(a, pi) + d(pi, pj) + d(y, b) - d(a, pj) - d(y, pi) - d(pi, b);
+}
+
 // ---------------------------------------------------------------------------
 // Deterministic SA acceptance threshold: floor(2^24 * exp(-dp * invT)) using
 // only IEEE fp32 multiply/add/sub (built with -ffp-contract=off) and exact
