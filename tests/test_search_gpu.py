@@ -45,6 +45,9 @@ SMALL = [
     ("tsp", lambda: synth.Instance("tsp11", synth.tsp20(2).durations[:, :11, :11], None, None,
                                    np.array([0]), "tsp")),
     ("td", lambda: synth.td_cvrp(10, 2, seed=4)),
+    ("tsp_asym", lambda: synth.Instance(
+        "tsp10a", np.array([np.where(np.eye(10, dtype=bool), 0, np.random.default_rng(8).integers(
+            3, 320, size=(10, 10)))]), None, None, np.array([0]), "tsp")),
 ]
 
 
@@ -77,6 +80,35 @@ def test_sa_trajectory_matches_oracle(ctx, name, maker):
                          inv_alpha)
     assert cur.cpu().numpy().tolist() == ref2[0]
     assert u64(bk) == ref2[3]
+
+
+@pytest.mark.parametrize("split_mode", [0, 2], ids=["branchfree", "branchy"])
+@pytest.mark.parametrize("n_cust", [1, 2, 3, 5, 8, 13])
+def test_sa_split_paths_match_oracle(ctx, split_mode, n_cust):
+    """CVRP SA through the packed branch-free kernel (mode 0) and the generic
+    split (mode 2): identical trajectories, ragged and tiny tours included,
+    tight capacity so some candidates leave customers unvisited."""
+    torch = torch_()
+    inst = synth.cvrp(n_cust, 2, seed=n_cust, slack=0.8)
+    load(ctx, inst)
+    ctx.set_split_mode(split_mode)
+    try:
+        chains = 5
+        P = synth.random_perms(chains, n_cust, seed=n_cust).astype(np.int16)
+        cur = torch.from_numpy(P).to(ctx.dev)
+        best = cur.clone()
+        ck = torch.empty(chains, dtype=torch.int64, device=ctx.dev)
+        bk = torch.full((chains,), -1, dtype=torch.int64, device=ctx.dev)
+        ctx.sa_run(cur, ck, best, bk, steps=12, inv_t0=1 / 40.0, inv_alpha=1 / 0.97, seed=77,
+                   step0=5)
+        ref = search.sa_run(scorer(inst), P.tolist(), P.tolist(), [2**64 - 1] * chains, 77, 5,
+                            12, 1 / 40.0, 1 / 0.97)
+    finally:
+        ctx.set_split_mode(0)
+    assert cur.cpu().numpy().tolist() == ref[0]
+    assert u64(ck) == ref[1]
+    assert best.cpu().numpy().tolist() == ref[2]
+    assert u64(bk) == ref[3]
 
 
 def test_sa_cvrp100_matches_c_restatement(ctx, coracle):

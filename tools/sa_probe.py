@@ -11,16 +11,16 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from vrpms_amd import runners, synth  # noqa: E402
-from vrpms_amd.core import CVRP, Context  # noqa: E402
+from vrpms_amd.core import CVRP, TSP, Context  # noqa: E402
 
 
 def main():
     inst = synth.cvrp(100, 8, seed=0)
     ctx = Context(0)
     ctx.set_instance(CVRP, inst.durations, inst.demand, inst.capacities, inst.start_times)
-    for chains in (256, 1024, 4096, 16384):
-        r = runners.SARunner(ctx, inst.n, chains=chains, total_steps=400, steps_per_epoch=200,
-                             durations=inst.durations)
+    def sa(label, c, n, chains, durations):
+        r = runners.SARunner(c, n, chains=chains, total_steps=400, steps_per_epoch=200,
+                             durations=durations)
         r.epoch(20)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -28,9 +28,20 @@ def main():
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         k, _ = r.best()
-        print(json.dumps({"algo": "sa", "chains": chains, "steps_per_s": 200 / dt,
-                          "evals_per_s": chains * 64 * 200 / dt, "best": (k >> 28) & (2**28 - 1)}),
-              flush=True)
+        print(json.dumps({"algo": "sa", "instance": label, "chains": chains,
+                          "steps_per_s": 200 / dt, "evals_per_s": chains * 64 * 200 / dt,
+                          "best": (k >> 28) & (2**28 - 1)}), flush=True)
+
+    for chains in (256, 1024, 4096, 16384):
+        sa("cvrp100", ctx, inst.n, chains, inst.durations)
+    ctx.set_split_mode(2)  # generic split kernel, for comparison
+    sa("cvrp100 (generic split)", ctx, inst.n, 4096, inst.durations)
+    ctx.set_split_mode(0)
+    tsp = synth.tsp50(0)
+    tctx = Context(0)
+    tctx.set_instance(TSP, tsp.durations, start_times=tsp.start_times)
+    for chains in (1024, 4096):
+        sa("tsp50 (O(1) deltas)", tctx, tsp.n, chains, tsp.durations)
     for islands, pop in ((8, 256), (64, 256), (256, 256)):
         g = runners.GARunner(ctx, inst.n, islands=islands, pop=pop)
         g.epoch(2)

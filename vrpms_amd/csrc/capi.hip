@@ -27,9 +27,22 @@ int hip_fail(hipError_t e, const char* what) {
 }
 
 // stats layout: 0 min_dur 1 max_dur 2 min_dem 3 max_dem 4 min_cap 5 max_cap
-//               6 min_start 7 max_start
+//               6 min_start 7 max_start 8 asymmetric (slice 0)
 __global__ void stats_init_kernel(int32_t* s) {
   if (threadIdx.x < 8) s[threadIdx.x] = (threadIdx.x & 1) ? INT_MIN : INT_MAX;
+  if (threadIdx.x == 8) s[8] = 0;
+}
+
+// s[8] |= any D[a][b] != D[b][a] in hour slice 0 (selects the O(1) 2-opt delta).
+__global__ void asym_kernel(const int32_t* __restrict__ D, int N, int32_t* s) {
+  const int64_t total = (int64_t)N * N;
+  int asym = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t a = i / N, b = i - a * N;
+    asym |= D[i] != D[b * N + a];
+  }
+  if (__any(asym) && (threadIdx.x & 63) == 0) atomicOr(s + 8, 1);
 }
 
 __device__ __forceinline__ void block_minmax_commit(int vmin, int vmax, int32_t* smin,
@@ -254,7 +267,9 @@ int vrpms_set_instance(vrpms_ctx* ctx, int32_t problem, const int32_t* d_dur, in
                                     problem == VRPMS_CVRP ? in.cap : nullptr, in.start, K,
                                     ctx->d_stats);
   VRPMS_HIP(hipGetLastError());
-  int32_t st[8];
+  asym_kernel<<<grid, 256, 0, s>>>(in.mat32, N, ctx->d_stats);
+  VRPMS_HIP(hipGetLastError());
+  int32_t st[9];
   std::vector<int32_t> caps(K);
   VRPMS_HIP(hipMemcpyAsync(st, ctx->d_stats, sizeof(st), hipMemcpyDeviceToHost, s));
   VRPMS_HIP(hipMemcpyAsync(caps.data(), in.cap, (size_t)K * 4, hipMemcpyDeviceToHost, s));
@@ -270,6 +285,7 @@ int vrpms_set_instance(vrpms_ctx* ctx, int32_t problem, const int32_t* d_dur, in
   in.min_cap = problem == VRPMS_CVRP ? st[4] : INT_MAX;
   in.max_cap = problem == VRPMS_CVRP ? st[5] : INT_MAX;
   in.max_start = st[7];
+  in.symmetric = st[8] == 0;
   in.cap0 = caps[0];
   in.uniform_cap = std::all_of(caps.begin(), caps.end(), [&](int32_t c) { return c == caps[0]; });
   const long double bound = (long double)in.max_start + (long double)(N + K + 1) * in.max_dur;

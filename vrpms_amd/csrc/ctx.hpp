@@ -20,6 +20,7 @@ struct Instance {
   int H = 1, N = 0, K = 1, objective = VRPMS_OBJ_SUM;
   int max_dur = 0, max_dem = 0, max_start = 0, min_cap = 0, max_cap = 0;
   bool uniform_cap = true;
+  bool symmetric = false;      // hour slice 0 is symmetric (O(1) 2-opt delta for static TSP)
   int cap0 = 0;
   // device copies owned by the context
   int32_t* mat32 = nullptr;    // [H][N][N]

@@ -23,6 +23,7 @@
 
 #include "common.hpp"
 #include "ctx.hpp"
+#include "split.hpp"
 #include "tour.hpp"
 
 namespace vrpms {
@@ -333,31 +334,16 @@ __global__ __launch_bounds__(BLOCK) void eval_cvrp_packed(PackedArgs a) {
 // from HBM to registers: no LDS tile, the LDS holds only the matrix and a
 // workgroup can be 1024 lanes (16 waves per CU instead of 8).
 //
-// Split arithmetic (prefix-ret layout, uniform fleet, every demand fits an
-// empty vehicle), per customer, branch-free:
-//   t    = acc + lo                     load << S | (cur + ret(prev)) grows
-//   f    = t < lim                      capacity test
-//   rd'  = (acc & smask) | 1 << KS      finished route, vehicle count above KS
-//   dsum += f ? 0 : rd';  dmax = max(dmax, f ? 0 : rd')
-//   acc  = f ? t : (dsum >= K << KS ? DEAD : hi)
-// The vehicle counter lives in dsum's high bits; once it reaches K the
-// accumulator is parked at DEAD = (cap + 2) << S, which never fits again and
-// contributes 0 duration, so every later customer adds exactly one count:
-// unvisited = count - K + 1.  No per-lane flags, no divergent branches.
-//
+// Split arithmetic: split.hpp (SplitAcc over the biased prefix-ret matrix).
 // Each lane walks its candidates through an R-deep ring of tour words
 // (R divides the word count when possible, so no slot is wasted); ring slot
 // indices are compile-time constants.
 // ---------------------------------------------------------------------------
 struct WordsArgs {
-  const uint64_t* pack;
-  int N, K;
-  uint32_t lim, smask;
-  uint32_t ks, klim, dead;  // 1 << ks counts vehicles; klim = initial dsum; dead = biased DEAD
+  FastSplit f;
   const uint32_t* words;
   int64_t C;
   int n;
-  int objective;
   uint64_t* keys;
   int32_t* sums;
   int32_t* maxs;
@@ -367,14 +353,14 @@ struct WordsArgs {
 template <int R>
 __global__ __launch_bounds__(1024) void eval_cvrp_words(WordsArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int N = a.N;
+  const int N = a.f.N;
   {
     const uint32_t ebytes = (uint32_t)N * N * 8;
-    const v4u* src = reinterpret_cast<const v4u*>(a.pack);
+    const v4u* src = reinterpret_cast<const v4u*>(a.f.pack);
     v4u* dst = reinterpret_cast<v4u*>(smem);
     for (uint32_t i = threadIdx.x; i < ebytes / 16; i += blockDim.x) dst[i] = src[i];
     if ((ebytes & 8u) && threadIdx.x == 0)
-      reinterpret_cast<uint64_t*>(smem)[ebytes / 8 - 1] = a.pack[ebytes / 8 - 1];
+      reinterpret_cast<uint64_t*>(smem)[ebytes / 8 - 1] = a.f.pack[ebytes / 8 - 1];
   }
   __syncthreads();
   const unsigned char* Eb = smem;
@@ -384,8 +370,7 @@ __global__ __launch_bounds__(1024) void eval_cvrp_words(WordsArgs a) {
   };
   const int64_t C = a.C;
   const int n = a.n, nw = (n + 3) >> 2, nfull = n >> 2;
-  const uint32_t lim = a.lim, smask = a.smask, kinc = 1u << a.ks, klim = a.klim;
-  const uint32_t deadacc = a.dead, lowmask = kinc - 1u;
+  const uint32_t smask = a.f.smask, kinc = 1u << a.f.ks, deadacc = a.f.dead;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
 
   const int nblk = nfull / R;                 // blocks of R full words: the fast loop
@@ -400,26 +385,9 @@ __global__ __launch_bounds__(1024) void eval_cvrp_words(WordsArgs a) {
     for (int u = 0; u < R; ++u) ring[u] = Wc[min((int64_t)u * C, last_off)];
     int64_t nxt = (int64_t)R * C;               // offset of the next word to fetch
 
-    // acc is biased by -lim so "fits" is the sign bit of acc + lo; dsum's
-    // vehicle counter starts at 2^B - K so exhausting the fleet sets bit 31.
-    // Every select below is a bitwise v_bfi on an arithmetic-shift mask:
-    // no lane masks, no VCC hazards, nothing the compiler can turn into a
-    // divergent branch.
-    uint32_t acc = 0u - lim, dsum = klim, dmax = 0;
-    auto bsel = [](uint32_t m, uint32_t x, uint32_t y) { return (x & m) | (y & ~m); };  // v_bfi
-    // sign mask via the bitfield-extract intrinsic: LLVM does not re-form it
-    // into a compare + select the way it does for (int)x >> 31
-    auto sgn = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_sbfe((int)x, 31u, 1u); };
-    auto step = [&](uint64_t e) {
-      const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);  // hi is pre-biased too
-      const uint32_t t = acc + lo;
-      const uint32_t fm = sgn(t);                                 // all ones: fits
-      const uint32_t rdm = bsel(fm, 0u, (acc & smask) | kinc);    // finished route, +1 vehicle
-      dsum += rdm;
-      dmax = max(dmax, rdm);
-      const uint32_t am = sgn(dsum);                              // all ones: fleet exhausted
-      acc = bsel(fm, t, bsel(am, deadacc, hi));
-    };
+    SplitAcc sa;
+    sa.init(a.f);
+    auto step = [&](uint64_t e) { sa.step(e, smask, kinc, deadacc); };
     uint32_t wd = ring[0];
     uint32_t c3 = wd >> 24, lastc = 0;
     uint64_t e0 = gat(0, wd & 0xffu), e1 = gat(wd & 0xffu, (wd >> 8) & 0xffu),
@@ -459,21 +427,11 @@ __global__ __launch_bounds__(1024) void eval_cvrp_words(WordsArgs a) {
         prev = cq;
       }
     }
-    const bool dead = (int32_t)dsum < 0;
-    const uint32_t count = (dsum >> a.ks) - (klim >> a.ks);  // vehicles closed (+ dead steps)
-    uint32_t s = dsum & lowmask, m = dmax >= kinc ? dmax - kinc : 0u;
-    uint32_t unv = 0;
-    if (dead) {
-      unv = count - (uint32_t)a.K + 1u;
-    } else if (n > 0) {
-      const uint32_t rd = acc & smask;  // close the last route
-      s += rd;
-      m = max(m, rd);
-    }
-    a.keys[c] = cvrp_key(unv, s, m, a.objective);
-    if (a.sums) a.sums[c] = (int32_t)s;
-    if (a.maxs) a.maxs[c] = (int32_t)m;
-    if (a.unv) a.unv[c] = (int32_t)unv;
+    const TourCost tc = sa.finish(a.f, n);
+    a.keys[c] = tc.key;
+    if (a.sums) a.sums[c] = tc.sum;
+    if (a.maxs) a.maxs[c] = tc.max;
+    if (a.unv) a.unv[c] = tc.unv;
   }
 }
 // rows (uint8 [C][ld]) -> words (uint32 [ceil(n/4)][C]); one lane per (word, candidate)
@@ -699,6 +657,30 @@ static bool words_fast_ok(const vrpms_ctx* ctx) {
          (size_t)in.N * in.N * 8 <= ctx->max_lds;
 }
 
+// Exactness conditions of the branch-free split (split.hpp): every demand fits
+// an empty vehicle, the vehicle counter fits above the duration sum in dsum,
+// and DEAD stays below 2^32.
+bool fast_split_params(const vrpms_ctx* ctx, int n, FastSplit* out) {
+  const Instance& in = ctx->inst;
+  if (!words_fast_ok(ctx) || !in.pack64w || in.max_dem > in.cap0) return false;
+  const int64_t sum_bound = (int64_t)(n + in.K + 1) * std::max(in.max_dur, 1);
+  int ks = 1;
+  while (ks < 31 && ((int64_t)1 << ks) <= sum_bound) ++ks;
+  const int B = 31 - ks;  // width of dsum's vehicle counter (bit 31 = exhausted)
+  if (B < 1 || ((int64_t)1 << B) <= std::max<int64_t>(in.K, n)) return false;
+  if ((((int64_t)in.cap0 + in.max_dem + 3) << in.pref_S) > ((int64_t)1 << 31)) return false;
+  out->pack = in.pack64w;
+  out->N = in.N;
+  out->K = in.K;
+  out->objective = in.objective;
+  out->lim = in.pref_lim;
+  out->smask = in.pref_smask;
+  out->ks = (uint32_t)ks;
+  out->klim = (uint32_t)((((int64_t)1 << B) - in.K) << ks);
+  out->dead = (uint32_t)1u << in.pref_S;
+  return true;
+}
+
 template <int NV>
 static int launch_packed(const PackedArgs& p, bool big, int mode, int grid, size_t lds,
                          hipStream_t s) {
@@ -821,20 +803,9 @@ extern "C" int vrpms_eval_words(vrpms_ctx* ctx, const uint32_t* d_words, int64_t
   if (in.N > 256) return fail(VRPMS_EINVAL, "vrpms_eval_words: uint8 tours need N <= 256");
   VRPMS_HIP(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
-  // fast path conditions: every demand fits an empty vehicle, the vehicle
-  // counter fits above the duration sum in dsum, DEAD stays below 2^32
-  const int64_t sum_bound = (int64_t)(n + in.K + 1) * std::max(in.max_dur, 1);
-  int ks = 1;
-  while (ks < 31 && ((int64_t)1 << ks) <= sum_bound) ++ks;
-  const int B = 31 - ks;  // width of dsum's vehicle counter (bit 31 = exhausted)
-  const bool fits = words_fast_ok(ctx) && in.pack64w && in.max_dem <= in.cap0 && B >= 1 &&
-                    ((int64_t)1 << B) > std::max<int64_t>(in.K, n) &&
-                    (((int64_t)in.cap0 + in.max_dem + 3) << in.pref_S) <= ((int64_t)1 << 31);
-  if (fits) {
-    const uint32_t dsum0 = (uint32_t)((((int64_t)1 << B) - in.K) << ks);
-    WordsArgs w{in.pack64w, in.N, in.K, in.pref_lim, in.pref_smask, (uint32_t)ks, dsum0,
-                (uint32_t)1u << in.pref_S, d_words, C, n, in.objective, d_keys, d_sum, d_max,
-                d_unv};
+  FastSplit f;
+  if (fast_split_params(ctx, n, &f)) {
+    WordsArgs w{f, d_words, C, n, d_keys, d_sum, d_max, d_unv};
     const size_t lds = ((size_t)in.N * in.N * 8 + 15) & ~(size_t)15;
     const int per_cu = std::max<int>(1, std::min<int>(2, (int)(ctx->max_lds / lds)));
     const int64_t blocks = (C + 1023) / 1024;

@@ -27,6 +27,7 @@
 
 #include "common.hpp"
 #include "ctx.hpp"
+#include "split.hpp"
 #include "tour.hpp"
 
 namespace vrpms {
@@ -47,6 +48,7 @@ struct SearchInst {
   const int32_t* start;
   int mat_lds;       // 1: stage the matrix into LDS
   uint32_t mat_bytes;
+  int symmetric;     // hour slice 0 symmetric (O(1) 2-opt delta)
 };
 
 static SearchInst search_inst(const vrpms_ctx* ctx) {
@@ -63,6 +65,7 @@ static SearchInst search_inst(const vrpms_ctx* ctx) {
   s.start = in.start;
   s.mat_bytes = (uint32_t)((size_t)in.H * in.N * in.N * (in.use16 ? 2 : 4));
   s.mat_lds = s.mat_bytes <= 64 * 1024 ? 1 : 0;
+  s.symmetric = in.symmetric ? 1 : 0;
   return s;
 }
 
@@ -141,11 +144,19 @@ __global__ __launch_bounds__(256) void sa_kernel(SaArgs a) {
   const uint16_t* gcur = a.cur + (int64_t)chain * n;
   for (int q = lane; q < n; q += 64) A[q] = gcur[q];
   wave_sync();
-  auto cost_of = [&](const uint16_t* T) {
-    auto tour = [&](int i) { return (uint32_t)T[i]; };
-    return eval_tour<CVRP>(I.D, I.sp, tour, n).key;
-  };
-  uint64_t ck = cost_of(A);
+  // Static TSP prices a move by its exact O(1) integer delta (tsp_move_delta);
+  // everything else re-evaluates the moved tour (the split / departure-time
+  // dependence makes a CVRP or time-dependent delta non-local).
+  constexpr bool kDelta = !CVRP && HM == 1;
+  const uint32_t Nm1 = (uint32_t)a.si.N - 1;
+  int dur;
+  uint64_t ck;
+  {
+    auto tour = [&](int i) { return (uint32_t)A[i]; };
+    const TourCost c0 = eval_tour<CVRP>(I.D, I.sp, tour, n);
+    ck = c0.key;
+    dur = c0.sum;
+  }
   uint64_t bk = a.best_key[chain];
   bool best_in_lds = false;
   if (ck < bk) {
@@ -159,8 +170,17 @@ __global__ __launch_bounds__(256) void sa_kernel(SaArgs a) {
     const u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)chain,
                            (uint32_t)lane, a.seed_lo, a.seed_hi);
     const Move m = decode_move(r.x, r.y, r.z, n);
-    auto moved = [&](int q) { return (uint32_t)A[moved_index(q, m)]; };
-    uint64_t k = eval_tour<CVRP>(I.D, I.sp, moved, n).key;
+    uint64_t k;
+    int nd = 0;
+    if constexpr (kDelta) {
+      auto dist = [&](uint32_t x, uint32_t y) { return I.D(0, x, y); };
+      auto tourA = [&](int q) { return min((uint32_t)A[q], Nm1); };
+      nd = dur + tsp_move_delta(dist, tourA, n, m, a.si.symmetric != 0);
+      k = pack_key(0, (uint32_t)nd, 0);
+    } else {
+      auto moved = [&](int q) { return (uint32_t)A[moved_index(q, m)]; };
+      k = eval_tour<CVRP>(I.D, I.sp, moved, n).key;
+    }
     uint64_t who = (uint64_t)lane;
     wave_argmin(k, who);
     const int bl = (int)who;
@@ -176,9 +196,166 @@ __global__ __launch_bounds__(256) void sa_kernel(SaArgs a) {
       mb.typ = (uint32_t)__shfl((int)m.typ, bl, 64);
       mb.i = __shfl(m.i, bl, 64);
       mb.j = __shfl(m.j, bl, 64);
+      if constexpr (kDelta) dur = __shfl(nd, bl, 64);
       for (int q = lane; q < n; q += 64) B[q] = A[moved_index(q, mb)];
       wave_sync();
       uint16_t* t = A;
+      A = B;
+      B = t;
+      ck = k;
+      if (ck < bk) {
+        bk = ck;
+        for (int q = lane; q < n; q += 64) Best[q] = A[q];
+        best_in_lds = true;
+      }
+      wave_sync();
+    }
+    invT = invT * a.inv_alpha;
+  }
+  uint16_t* gout = a.cur + (int64_t)chain * n;
+  for (int q = lane; q < n; q += 64) gout[q] = A[q];
+  if (best_in_lds) {
+    uint16_t* gb = a.best + (int64_t)chain * n;
+    for (int q = lane; q < n; q += 64) gb[q] = Best[q];
+  }
+  if (lane == 0) {
+    a.cur_key[chain] = ck;
+    a.best_key[chain] = bk;
+  }
+}
+
+// ===========================================================================
+// SA fast path (static CVRP, uniform fleet, every demand fits an empty
+// vehicle): the same chain, moves and acceptance as sa_kernel, but each
+// candidate is priced with the branch-free split of split.hpp over the
+// biased prefix-ret matrix (one ds_read_b64 per customer carries the edge,
+// the demand and both depot legs).  One 1024-lane workgroup = 16 chains
+// share the LDS-resident matrix; tours are u8 in LDS.  Each lane reads its
+// moved tour through the select-chain map (move_map), software-pipelined two
+// blocks of 4 customers ahead: tour bytes of block b+2 and matrix gathers of
+// block b+1 are in flight while block b's split steps run.
+// ===========================================================================
+constexpr int kSaPackedWaves = 16;
+
+struct SaPackedArgs {
+  FastSplit f;
+  int chains, n, steps;
+  float inv_t0, inv_alpha;
+  uint32_t seed_lo, seed_hi;
+  uint64_t step0;
+  uint32_t tb;          // bytes per LDS tour buffer (>= n + 12, zero padded)
+  uint16_t* cur;
+  uint64_t* cur_key;
+  uint16_t* best;
+  uint64_t* best_key;
+};
+
+// Key of tour T (u8, LDS, zero padded to n + 12) read through map mm.
+VRPMS_DEV uint64_t eval_mapped(const FastSplit& f, const unsigned char* E, uint32_t N8,
+                               const uint8_t* T, int n, const MoveMap& mm) {
+  auto gat = [&](uint32_t x, uint32_t y) {
+    return *reinterpret_cast<const uint64_t*>(E + (__umul24(x, N8) + (y << 3)));
+  };
+  auto rd = [&](int q) { return (uint32_t)T[map_src(mm, q)]; };
+  const uint32_t smask = f.smask, kinc = 1u << f.ks, deadacc = f.dead;
+  SplitAcc sa;
+  sa.init(f);
+  const int nfull = n >> 2;
+  uint32_t b0 = rd(4), b1 = rd(5), b2 = rd(6), b3 = rd(7);
+  uint32_t last;
+  uint64_t e0, e1, e2, e3;
+  {
+    const uint32_t a0 = rd(0), a1 = rd(1), a2 = rd(2), a3 = rd(3);
+    e0 = gat(0, a0);
+    e1 = gat(a0, a1);
+    e2 = gat(a1, a2);
+    e3 = gat(a2, a3);
+    last = a3;
+  }
+  for (int b = 0; b < nfull; ++b) {
+    const int q = 4 * b + 8;
+    const uint32_t c0 = rd(q), c1 = rd(q + 1), c2 = rd(q + 2), c3 = rd(q + 3);
+    const uint64_t f0 = gat(last, b0), f1 = gat(b0, b1), f2 = gat(b1, b2), f3 = gat(b2, b3);
+    sa.step(e0, smask, kinc, deadacc);
+    sa.step(e1, smask, kinc, deadacc);
+    sa.step(e2, smask, kinc, deadacc);
+    sa.step(e3, smask, kinc, deadacc);
+    last = b3;
+    b0 = c0;
+    b1 = c1;
+    b2 = c2;
+    b3 = c3;
+    e0 = f0;
+    e1 = f1;
+    e2 = f2;
+    e3 = f3;
+  }
+  const int rem = n & 3;  // e0..e(rem-1): the ragged last block
+  if (rem > 0) sa.step(e0, smask, kinc, deadacc);
+  if (rem > 1) sa.step(e1, smask, kinc, deadacc);
+  if (rem > 2) sa.step(e2, smask, kinc, deadacc);
+  return sa.finish(f, n).key;
+}
+
+__global__ __launch_bounds__(1024) void sa_packed_kernel(SaPackedArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int N = a.f.N;
+  const uint32_t ebytes = (uint32_t)N * N * 8;
+  {
+    const v4u* src = reinterpret_cast<const v4u*>(a.f.pack);
+    v4u* dst = reinterpret_cast<v4u*>(smem);
+    for (uint32_t i = threadIdx.x; i < ebytes / 16; i += blockDim.x) dst[i] = src[i];
+    if ((ebytes & 8u) && threadIdx.x == 0)
+      reinterpret_cast<uint64_t*>(smem)[ebytes / 8 - 1] = a.f.pack[ebytes / 8 - 1];
+  }
+  __syncthreads();
+  const int n = a.n;
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  const int chain = blockIdx.x * kSaPackedWaves + wave;
+  if (chain >= a.chains) return;  // no block-wide barrier after this point
+  const uint32_t N8 = 8u * (uint32_t)N, tb = a.tb;
+  uint8_t* A = smem + ((ebytes + 15u) & ~15u) + (uint32_t)wave * 3u * tb;
+  uint8_t* B = A + tb;
+  uint8_t* Best = B + tb;
+  const uint16_t* gcur = a.cur + (int64_t)chain * n;
+  for (uint32_t q = lane; q < tb; q += 64) {
+    A[q] = q < (uint32_t)n ? (uint8_t)min((uint32_t)gcur[q], (uint32_t)N - 1) : 0;
+    B[q] = 0;
+  }
+  wave_sync();
+  uint64_t ck = eval_mapped(a.f, smem, N8, A, n, identity_map());
+  uint64_t bk = a.best_key[chain];
+  bool best_in_lds = false;
+  if (ck < bk) {
+    bk = ck;
+    for (int q = lane; q < n; q += 64) Best[q] = A[q];
+    best_in_lds = true;
+  }
+  float invT = a.inv_t0;
+  for (int s = 0; s < a.steps && n >= 2; ++s) {
+    const uint64_t step = a.step0 + (uint64_t)s;
+    const u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)chain,
+                           (uint32_t)lane, a.seed_lo, a.seed_hi);
+    const Move m = decode_move(r.x, r.y, r.z, n);
+    uint64_t k = eval_mapped(a.f, smem, N8, A, n, move_map(m));
+    uint64_t who = (uint64_t)lane;
+    wave_argmin(k, who);
+    const int bl = (int)who;
+    bool accept = k <= ck;
+    if (!accept) {
+      const uint64_t d = (k >> 28) - (ck >> 28);
+      const uint32_t dp = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
+      accept = (__shfl(r.w, bl, 64) >> 8) < accept_threshold(dp, invT);
+    }
+    if (accept) {
+      Move mb;
+      mb.typ = (uint32_t)__shfl((int)m.typ, bl, 64);
+      mb.i = __shfl(m.i, bl, 64);
+      mb.j = __shfl(m.j, bl, 64);
+      const MoveMap mm = move_map(mb);
+      for (int q = lane; q < n; q += 64) B[q] = A[map_src(mm, q)];
+      wave_sync();
+      uint8_t* t = A;
       A = B;
       B = t;
       ck = k;
@@ -806,6 +983,24 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
   if (!d_cur || !d_cur_key || !d_best || !d_best_key)
     return fail(VRPMS_EINVAL, "vrpms_sa_run: NULL state buffer");
   VRPMS_HIP(hipSetDevice(ctx->device));
+  FastSplit f;
+  if (ctx->inst.H == 1 && fast_split_params(ctx, n, &f)) {
+    const uint32_t tb = ((uint32_t)n + 12u + 15u) & ~15u;
+    const size_t lds = (((size_t)f.N * f.N * 8 + 15) & ~(size_t)15) +
+                       (size_t)kSaPackedWaves * 3 * tb;
+    if (lds <= ctx->max_lds) {
+      SaPackedArgs pa{f, p->chains, n, p->steps, p->inv_t0, p->inv_alpha, (uint32_t)p->seed,
+                      (uint32_t)(p->seed >> 32), p->step0, tb, d_cur, d_cur_key, d_best,
+                      d_best_key};
+      if (lds > 65536)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(sa_packed_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      const int grid = (p->chains + kSaPackedWaves - 1) / kSaPackedWaves;
+      sa_packed_kernel<<<grid, 64 * kSaPackedWaves, lds, (hipStream_t)stream>>>(pa);
+      VRPMS_HIP(hipGetLastError());
+      return VRPMS_OK;
+    }
+  }
   SaArgs a{search_inst(ctx), p->chains, n, p->steps, p->inv_t0, p->inv_alpha,
            (uint32_t)p->seed, (uint32_t)(p->seed >> 32), p->step0, d_cur, d_cur_key, d_best,
            d_best_key};

@@ -1,0 +1,82 @@
+// Branch-free greedy split over the prefix-ret
+// packed matrix, shared by the headline scoring kernel (eval_cvrp_words) and
+// the CVRP SA chain kernel (sa_packed_kernel) so both produce the same key
+// for the same tour, bit for bit, as oracle/spec.py eval_cvrp.
+//
+// Layout (capi.hip pack_prefix_kernel + bias_hi_kernel), uniform fleet:
+//   E[a][b].lo = dem(b) << S + dur(a,b) + ret(b) - ret(a)       (mod 2^32)
+//   E[a][b].hi = (out(b) + ret(b) | dem(b) << S) - lim,  lim = (cap + 1) << S
+// A route's accumulator is acc = (load << S | cur + ret(last)) - lim, so a
+// customer fits iff acc + lo is negative (sign bit), and the finished
+// route's duration is acc & smask.
+//   rd'  = (acc & smask) | 1 << KS      finished route, vehicle count above KS
+//   dsum += f ? 0 : rd';  dmax = max(dmax, f ? 0 : rd')
+//   acc  = f ? t : (dsum >= K << KS ? DEAD : hi)
+// The vehicle counter lives in dsum's high bits, starting at 2^B - K so that
+// exhausting the fleet sets bit 31; the accumulator is then parked at DEAD,
+// which never fits again and adds no duration, so every later customer adds
+// exactly one count: unvisited = count - K + 1.  No per-lane flags and no
+// divergent branches.
+#pragma once
+#include "common.hpp"
+#include "ctx.hpp"
+#include "tour.hpp"
+
+namespace vrpms {
+
+struct FastSplit {
+  const uint64_t* pack;     // biased prefix-ret matrix [N][N] (Instance::pack64w)
+  int N, K, objective;
+  uint32_t lim, smask;
+  uint32_t ks, klim, dead;  // 1 << ks counts vehicles; klim = initial dsum; dead = biased DEAD
+};
+
+// Host: constants of the branch-free split for tours of n customers, or
+// false when the instance is outside its exactness conditions (the caller
+// then uses the generic split).  Defined in eval.hip.
+bool fast_split_params(const vrpms_ctx* ctx, int n, FastSplit* out);
+
+struct SplitAcc {
+  uint32_t acc, dsum, dmax;
+
+  VRPMS_DEV void init(const FastSplit& f) {
+    acc = 0u - f.lim;
+    dsum = f.klim;
+    dmax = 0;
+  }
+
+  // One customer: `e` is the packed entry of (previous customer, customer).
+  // Every select is a bitwise v_bfi on an arithmetic-shift mask; the sign
+  // mask comes from the bitfield-extract intrinsic, which LLVM does not
+  // re-form into a compare + select the way it does for (int)x >> 31.
+  VRPMS_DEV void step(uint64_t e, uint32_t smask, uint32_t kinc, uint32_t deadacc) {
+    auto bsel = [](uint32_t m, uint32_t x, uint32_t y) { return (x & m) | (y & ~m); };
+    auto sgn = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_sbfe((int)x, 31u, 1u); };
+    const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);  // hi is pre-biased too
+    const uint32_t t = acc + lo;
+    const uint32_t fm = sgn(t);                                 // all ones: fits
+    const uint32_t rdm = bsel(fm, 0u, (acc & smask) | kinc);    // finished route, +1 vehicle
+    dsum += rdm;
+    dmax = max(dmax, rdm);
+    const uint32_t am = sgn(dsum);                              // all ones: fleet exhausted
+    acc = bsel(fm, t, bsel(am, deadacc, hi));
+  }
+
+  VRPMS_DEV TourCost finish(const FastSplit& f, int n) const {
+    const uint32_t kinc = 1u << f.ks;
+    const bool dead = (int32_t)dsum < 0;
+    const uint32_t count = (dsum >> f.ks) - (f.klim >> f.ks);  // vehicles closed (+ dead steps)
+    uint32_t s = dsum & (kinc - 1u), m = dmax >= kinc ? dmax - kinc : 0u;
+    uint32_t unv = 0;
+    if (dead) {
+      unv = count - (uint32_t)f.K + 1u;
+    } else if (n > 0) {
+      const uint32_t rd = acc & f.smask;  // close the last route
+      s += rd;
+      m = max(m, rd);
+    }
+    return {cvrp_key(unv, s, m, f.objective), (int32_t)s, (int32_t)m, (int32_t)unv};
+  }
+};
+
+}  // namespace vrpms

@@ -140,6 +140,30 @@ VRPMS_DEV int moved_index(int q, const Move& m) {
   return q == j ? i : q - 1;
 }
 
+// moved_index as a select chain with no divergent branches: one window of
+// positions read at a + s*q (2-opt reversal, relocate shift) plus up to two
+// pinned positions (swap ends, relocate target).  src(q) == moved_index(q, m)
+// for every q; positions outside [0, n) map to themselves.
+struct MoveMap {
+  int lo, len, a, s, p1, v1, p2, v2;
+};
+
+VRPMS_DEV MoveMap move_map(const Move& m) {
+  const int i = m.i, j = m.j;
+  if (m.typ == kMoveSwap) return {0, 0, 0, 1, i, j, j, i};
+  if (m.typ == kMove2Opt) return {i, j - i + 1, i + j, -1, -1, 0, -1, 0};
+  if (i < j) return {i, j - i, 1, 1, j, i, -1, 0};
+  return {j + 1, i - j, -1, 1, j, i, -1, 0};
+}
+
+VRPMS_DEV MoveMap identity_map() { return {0, 0, 0, 1, -1, 0, -1, 0}; }
+
+VRPMS_DEV int map_src(const MoveMap& mm, int q) {
+  int r = (uint32_t)(q - mm.lo) < (uint32_t)mm.len ? mm.a + mm.s * q : q;
+  r = q == mm.p1 ? mm.v1 : r;
+  return q == mm.p2 ? mm.v2 : r;
+}
+
 // Exact duration change of the static closed tour 0 -> T[0..n-1] -> 0 under
 // move m (integer, so duration + delta == a full re-evaluation).  Swap and
 // relocate touch at most 8 edges; 2-opt touches 4 on a symmetric matrix and
