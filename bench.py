@@ -170,6 +170,10 @@ def other_configs(ctx, torch, dev, seed=0):
     from vrpms_amd import synth
     from vrpms_amd.core import CVRP
     out = {}
+    # measured L2-gather ceiling (random 2-byte loads over a uint16 table the
+    # size of each matrix; vrpms_probe_l2_gather) -- the staged kernels' roofline
+    r_td = ctx.probe_l2_gather(slots=24 * 201 * 201)
+    r_x = ctx.probe_l2_gather(slots=1001 * 1001)
 
     def kernel_time(fn, reps=5):
         fn()
@@ -189,8 +193,11 @@ def other_configs(ctx, torch, dev, seed=0):
     perms = make_batch(torch, C, td.n, dev, seed + 11)
     keys = torch.empty(C, dtype=torch.int64, device=dev)
     t = kernel_time(lambda: ctx.eval(perms, out=keys))
-    out["cfg3_tdvrp200_h24"] = {"kernel": "eval_generic<u16, L2, H=24>", "evals_per_s": C / t,
-                                "candidates": C, "gathers_per_eval": td.n + td.K}
+    out["cfg3_tdvrp200_h24"] = {"kernel": "eval_staged<u16 L2, H=24, u8 tours>",
+                                "evals_per_s": C / t, "candidates": C,
+                                "gathers_per_eval": td.n + td.K, "l2_gathers_per_eval": td.n,
+                                "l2_roofline": {"r_gather_measured": r_td, "unit": "gathers/s",
+                                                "frac": C / t * td.n / r_td}}
     # cfg 4: X-style CVRP-1000 (uint16 tours, 2.0 MB u16 matrix: L2-resident)
     x = synth.x_style(1000, seed=seed)
     ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
@@ -203,8 +210,11 @@ def other_configs(ctx, torch, dev, seed=0):
         p16[s:s + r.shape[0]] = (r.argsort(dim=1) + 1).to(torch.int16)
     keys = torch.empty(C, dtype=torch.int64, device=dev)
     t = kernel_time(lambda: ctx.eval(p16, out=keys))
-    out["cfg4_x1000"] = {"kernel": "eval_generic<u16, L2>", "evals_per_s": C / t,
-                         "candidates": C, "vehicles": x.K, "gathers_per_eval": x.n + x.K}
+    out["cfg4_x1000"] = {"kernel": "eval_staged<u16 L2, H=1, u16 tours>", "evals_per_s": C / t,
+                         "candidates": C, "vehicles": x.K, "gathers_per_eval": x.n + x.K,
+                         "l2_gathers_per_eval": x.n,
+                         "l2_roofline": {"r_gather_measured": r_x, "unit": "gathers/s",
+                                         "frac": C / t * x.n / r_x}}
     # cfg 5: throughput mode, 10k concurrent TSP-50 requests, one workgroup per request
     R, steps = 10000, 1000
     rng = np.random.default_rng(seed)

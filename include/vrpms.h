@@ -100,13 +100,18 @@ int vrpms_rows_to_words(vrpms_ctx* ctx, const uint8_t* d_rows, int64_t C, int32_
 
 /* Which scoring kernel vrpms_eval picks for these tour buffers:
  * 0 = eval_cvrp_packed (LDS packed matrix + LDS-staged tiles),
- * 1 = eval_tsp_staged, 2 = eval_generic; -1 = no instance. */
+ * 1 = eval_tsp_staged, 2 = eval_staged (LDS-staged tours, L2-resident or
+ * LDS matrix, depot legs in LDS tables; eval_generic when its tables do not
+ * fit the LDS); -1 = no instance. */
 int vrpms_eval_path(vrpms_ctx* ctx, int32_t perm_bytes, int64_t ld, const void* d_perms);
 
 /* Context options (kernel-variant overrides for A/B tests and profiling).
  *   VRPMS_OPT_SPLIT_MODE: 0 = auto (branch-free prefix-ret split whenever its
  *   packed layout fits), 2 = force the branchy split in eval_cvrp_packed. */
 #define VRPMS_OPT_SPLIT_MODE 1
+/*   VRPMS_OPT_STAGED_M: candidates interleaved per lane in eval_staged
+ *   (0 = auto: 2 for hour-indexed matrices, 1 for static; 1 or 2 force). */
+#define VRPMS_OPT_STAGED_M 2
 int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value);
 
 /* Decode ONE giant tour into the result dict of api/vrp/ga/index.py:49-53
@@ -212,6 +217,12 @@ int vrpms_tsp_batch_sa(vrpms_ctx* ctx, const int32_t* d_mats, int32_t R, int32_t
  * in LDS -- the measured random LDS-gather ceiling R_gather of SURVEY.md §8d. */
 int vrpms_probe_lds_gather(vrpms_ctx* ctx, const uint64_t* d_table, int32_t slots, int32_t iters,
                            int32_t blocks, uint64_t* d_sink, void* stream);
+
+/* Roofline probe (measurement only): `blocks` x 256 lanes each issue
+ * 8 * iters random 2-byte global loads over a `slots`-entry uint16 table --
+ * the measured L2-gather ceiling of the staged kernels (cfg 3 / cfg 4). */
+int vrpms_probe_l2_gather(vrpms_ctx* ctx, const uint16_t* d_table, int32_t slots, int32_t iters,
+                          int32_t blocks, uint64_t* d_sink, void* stream);
 
 #ifdef __cplusplus
 }

@@ -25,6 +25,7 @@ VRPMS_ENOMEM = -5
 TSP = 0
 CVRP = 1
 OPT_SPLIT_MODE = 1
+OPT_STAGED_M = 2
 OBJ_SUM = 0
 OBJ_MAX = 1
 
@@ -71,6 +72,7 @@ SIGNATURES = {
                                        _i32, _vp]),
     "vrpms_bf_run": (_c.c_int, [_vp, _i32, _u64, _u64, _vp, _vp]),
     "vrpms_probe_lds_gather": (_c.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp]),
+    "vrpms_probe_l2_gather": (_c.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp]),
     "vrpms_tsp_batch_sa": (_c.c_int, [_vp, _vp, _i32, _i32, _c.POINTER(SaParams), _vp, _vp,
                                       _vp]),
 }

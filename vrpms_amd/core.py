@@ -165,6 +165,10 @@ class Context:
         """0 = auto (branch-free prefix-ret split when it fits), 2 = branchy."""
         check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_SPLIT_MODE, int(mode)))
 
+    def set_staged_m(self, m: int):
+        """Candidates per lane in eval_staged: 0 = auto, 1 or 2 force."""
+        check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_STAGED_M, int(m)))
+
     def eval_path(self, perms) -> int:
         return self.lib.vrpms_eval_path(self._ctx, perm_dtype_bytes(perms), perms.shape[-1],
                                         perms.data_ptr())
@@ -271,6 +275,25 @@ class Context:
             e1.record()
             torch.cuda.synchronize(self.dev)
             best = max(best, blocks * 1024 * 4 * iters / (e0.elapsed_time(e1) * 1e-3))
+        return best
+
+    def probe_l2_gather(self, slots: int = 24 * 201 * 201, iters: int = 256,
+                        blocks: int | None = None, reps: int = 5):
+        """Measured random 2-byte global-load gather rate (gathers/s) over an
+        L2-resident uint16 table of `slots` entries, best of `reps`."""
+        torch = _torch()
+        blocks = blocks or 8 * 256 * 4
+        table = torch.randint(0, 2**15, (slots,), dtype=torch.int16, device=self.dev)
+        sink = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        best = 0.0
+        for _ in range(reps + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            check(self.lib.vrpms_probe_l2_gather(self._ctx, table.data_ptr(), slots, iters,
+                                                 blocks, sink.data_ptr(), self.stream()))
+            e1.record()
+            torch.cuda.synchronize(self.dev)
+            best = max(best, blocks * 256 * 8 * iters / (e0.elapsed_time(e1) * 1e-3))
         return best
 
 

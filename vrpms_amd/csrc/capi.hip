@@ -214,6 +214,12 @@ int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value) {
     ctx->opt_split_mode = value;
     return VRPMS_OK;
   }
+  if (option == VRPMS_OPT_STAGED_M) {
+    if (value < 0 || value > 2)
+      return fail(VRPMS_EINVAL, "vrpms_set_option: staged M must be 0 (auto), 1 or 2");
+    ctx->opt_staged_m = value;
+    return VRPMS_OK;
+  }
   return fail(VRPMS_EINVAL, "vrpms_set_option: unknown option " + std::to_string(option));
 }
 

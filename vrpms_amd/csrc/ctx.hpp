@@ -49,6 +49,7 @@ struct vrpms_ctx {
   int num_cus = 256;
   size_t max_lds = 160 * 1024;
   int opt_split_mode = 0;       // VRPMS_OPT_SPLIT_MODE (0 auto, 2 force branchy)
+  int opt_staged_m = 0;         // VRPMS_OPT_STAGED_M (0 auto, 1 or 2)
   int32_t* d_stats = nullptr;   // scratch for set_instance validation
   uint64_t* d_scratch = nullptr;  // small reduction scratch
   void* search_scratch = nullptr;  // GA children / BF block results (grown on demand)

@@ -24,6 +24,7 @@
 #include "common.hpp"
 #include "ctx.hpp"
 #include "split.hpp"
+#include "staged.hpp"
 #include "tour.hpp"
 
 namespace vrpms {
@@ -786,6 +787,8 @@ extern "C" int vrpms_eval(vrpms_ctx* ctx, const void* d_perms, int32_t perm_byte
     VRPMS_HIP(hipGetLastError());
     return VRPMS_OK;
   }
+  if (staged_fits(ctx))
+    return launch_staged(ctx, d_perms, perm_bytes, C, n, ld, d_keys, d_sum, d_max, d_unv, s);
   EvalArgs a{nullptr, in.N, in.H, in.K, in.dem, in.cap, in.start, d_perms, C, n, ld,
              in.objective, d_keys, d_sum, d_max, d_unv};
   return perm_bytes == 1 ? launch_generic<uint8_t>(ctx, a, s) : launch_generic<uint16_t>(ctx, a, s);

@@ -37,9 +37,44 @@ __global__ __launch_bounds__(1024) void lds_gather_probe(const uint64_t* __restr
   if (acc == 0x123456789abcdefull) sink[0] = acc;  // keeps the gathers live
 }
 
+// L2-gather ceiling for the staged kernels (cfg 3 / cfg 4): every lane
+// issues random 2-byte loads into a uint16 table of `slots` entries (the
+// 1.94 MB hour-indexed TD-200 matrix / the 2.0 MB X-1000 matrix stay L2
+// resident per XCD).  Eight independent LCG streams per lane keep eight
+// loads in flight; full occupancy (2048 lanes per CU).
+__global__ __launch_bounds__(256) void l2_gather_probe(const uint16_t* __restrict__ table,
+                                                       uint32_t slots, int iters,
+                                                       uint64_t* __restrict__ sink) {
+  uint32_t s[8];
+  s[0] = (blockIdx.x * 256u + threadIdx.x) * 2654435761u + 1u;
+#pragma unroll
+  for (int i = 1; i < 8; ++i) s[i] = s[i - 1] * 747796405u + 2891336453u;
+  uint32_t acc = 0;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      s[i] = s[i] * 1664525u + 1013904223u;
+      acc += table[__umulhi(s[i], slots)];
+    }
+  }
+  if (acc == 0x9abcdefu) sink[0] = acc;  // keeps the gathers live
+}
+
 }  // namespace vrpms
 
 using namespace vrpms;
+
+extern "C" int vrpms_probe_l2_gather(vrpms_ctx* ctx, const uint16_t* d_table, int32_t slots,
+                                     int32_t iters, int32_t blocks, uint64_t* d_sink,
+                                     void* stream) {
+  if (!ctx || !d_table || !d_sink || slots <= 0 || iters <= 0 || blocks <= 0)
+    return fail(VRPMS_EINVAL, "vrpms_probe_l2_gather: bad arguments");
+  VRPMS_HIP(hipSetDevice(ctx->device));
+  l2_gather_probe<<<blocks, 256, 0, (hipStream_t)stream>>>(d_table, (uint32_t)slots, iters,
+                                                           d_sink);
+  VRPMS_HIP(hipGetLastError());
+  return VRPMS_OK;
+}
 
 extern "C" int vrpms_probe_lds_gather(vrpms_ctx* ctx, const uint64_t* d_table, int32_t slots,
                                       int32_t iters, int32_t blocks, uint64_t* d_sink,
