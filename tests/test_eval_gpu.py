@@ -107,6 +107,39 @@ def test_cvrp_asymmetric_matrix_prefix_ret(ctx, coracle, split_mode):
     check_batch(ctx, coracle, inst, P, n=inst.n, expect_path=0)
 
 
+@pytest.fixture
+def words_gen(ctx):
+    """Reset the LDS-packed kernel generation after a test forces one."""
+    yield ctx
+    ctx.set_words_kernel(0)
+    ctx.set_words_ilp(0)
+
+
+# eval_cvrp_rows2 (row-major tiles staged through LDS) against the first
+# generation eval_cvrp_packed and the oracle: CW = 8 (N <= 101), CW = 4
+# (N = 111), ragged tiles, short tours, and N = 121 where no tile fits next
+# to the matrix (falls back to eval_cvrp_packed).
+@pytest.mark.parametrize("n,K,ld,C", [(100, 8, 100, 20037), (97, 7, 100, 5000), (30, 3, 32, 4099),
+                                      (5, 2, 8, 3000), (110, 9, 112, 5000), (120, 10, 120, 6000)])
+def test_rows2_matches_packed_and_oracle(words_gen, coracle, n, K, ld, C):
+    ctx = words_gen
+    inst = synth.cvrp(n, K, seed=n)
+    P = synth.random_perms(C, inst.n, seed=K, ld=ld)
+    got = {}
+    for gen in (0, 1):
+        ctx.set_words_kernel(gen)
+        got[gen] = check_batch(ctx, coracle, inst, P, n=inst.n, objective=n % 2, expect_path=0)
+    np.testing.assert_array_equal(got[0], got[1])
+
+
+@pytest.mark.parametrize("ilp", [1, 2])
+def test_words2_ilp_variants(words_gen, coracle, ilp):
+    ctx = words_gen
+    ctx.set_words_ilp(ilp)
+    inst = synth.cvrp(100, 8, seed=11)
+    check_words(ctx, coracle, inst, synth.random_perms(4097, inst.n, seed=ilp), inst.n)
+
+
 def check_words(ctx, coracle, inst, P, n, objective=0):
     """Same tours through the word-interleaved layout (vrpms_eval_words)."""
     load(ctx, inst, objective)

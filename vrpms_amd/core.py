@@ -165,6 +165,15 @@ class Context:
         """0 = auto (branch-free prefix-ret split when it fits), 2 = branchy."""
         check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_SPLIT_MODE, int(mode)))
 
+    def set_words_kernel(self, gen: int):
+        """LDS-packed kernels: 0 = auto (eval_cvrp_words2 / eval_cvrp_rows2),
+        1 = first generation (eval_cvrp_words / eval_cvrp_packed)."""
+        check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_WORDS_KERNEL, int(gen)))
+
+    def set_words_ilp(self, ilp: int):
+        """Candidates per lane in eval_cvrp_words2: 0 = auto (2), 1 or 2 force."""
+        check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_WORDS_ILP, int(ilp)))
+
     def set_staged_m(self, m: int):
         """Candidates per lane in eval_staged: 0 = auto, 1 or 2 force."""
         check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_STAGED_M, int(m)))

@@ -25,6 +25,7 @@
 #include "ctx.hpp"
 #include "split.hpp"
 #include "staged.hpp"
+#include "words.hpp"
 #include "tour.hpp"
 
 namespace vrpms {
@@ -340,17 +341,6 @@ __global__ __launch_bounds__(BLOCK) void eval_cvrp_packed(PackedArgs a) {
 // (R divides the word count when possible, so no slot is wasted); ring slot
 // indices are compile-time constants.
 // ---------------------------------------------------------------------------
-struct WordsArgs {
-  FastSplit f;
-  const uint32_t* words;
-  int64_t C;
-  int n;
-  uint64_t* keys;
-  int32_t* sums;
-  int32_t* maxs;
-  int32_t* unv;
-};
-
 template <int R>
 __global__ __launch_bounds__(1024) void eval_cvrp_words(WordsArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -750,6 +740,13 @@ extern "C" int vrpms_eval(vrpms_ctx* ctx, const void* d_perms, int32_t perm_byte
   hipStream_t s = (hipStream_t)stream;
   const int path = vrpms_eval_path(ctx, perm_bytes, ld, d_perms);
   if (path == 0) {
+    FastSplit f;
+    if (ctx->opt_words_kernel != 1 && fast_split_params(ctx, n, &f) &&
+        rows2_chunk_words(ctx, f) > 0) {
+      RowsArgs r{f, static_cast<const unsigned char*>(d_perms), C, n, (int)ld,
+                 d_keys, d_sum, d_max, d_unv};
+      return launch_rows2(ctx, r, s);
+    }
     const int mode = packed_mode(ctx);
     PackedArgs p{mode == 1 ? in.pack64p : in.pack64, in.N, in.K, in.pack_w,
                  in.uniform_cap ? 1 : 0, in.cap0, in.pref_lim, in.pref_smask, in.cap,
@@ -820,6 +817,7 @@ extern "C" int vrpms_eval_words(vrpms_ctx* ctx, const uint32_t* d_words, int64_t
       const int wst = (nw + r - 1) / r * r - nw;
       if (wst < waste) { waste = wst; R = r; }
     }
+    if (ctx->opt_words_kernel != 1) return launch_words2(ctx, w, R, s);
     auto go = [&](auto kern) {
       allow_lds(kern, lds);
       kern<<<grid, 1024, lds, s>>>(w);

@@ -1,0 +1,435 @@
+// Headline scoring kernels, second generation: eval_cvrp_words2 (word-
+// interleaved tours) and eval_cvrp_rows2 (the API's row-major uint8 tours).
+//
+// Same contract as eval_cvrp_words (eval.hip): uniform-fleet CVRP with the
+// biased prefix-ret matrix E (u64 [N][N], split.hpp) resident in LDS, one
+// lane per candidate, bit-exact keys.  What changes is the instruction
+// budget per customer (the kernels are LDS-gather / VALU issue bound,
+// DESIGN.md §4):
+//
+//   * gather address in 2 VALU: v_perm_b32 lays the customer pair (a, b) out
+//     as two u16 halves, v_dot2_u32_u16 against (8N, 8) gives the byte
+//     offset a*8N + 8b directly -- the cross-word pair (last of the previous
+//     word, first of this one) costs the same because v_perm takes two words
+//     (was: byte extract, 24-bit multiply, shift, add);
+//   * route closure in 2 VALU: v_and_or_b32 builds (acc & smask) | kinc with
+//     smask held in a VGPR (gfx9 VOP3 reads one SGPR), then one cndmask;
+//   * two candidates per lane (ILP = 2): two independent split chains hide
+//     each other's gather latency, one 1024-lane workgroup per CU;
+//   * the next word's address math is interleaved into the current word's
+//     split chain (sched_group_barrier), so ds_reads issue well before use.
+//
+// eval_cvrp_rows2 reads the row-major layout directly: a 2048-row tile is
+// staged through LDS CW words at a time (coalesced 32-byte row segments,
+// register prefetch of the next chunk), and each lane then walks its two
+// rows out of LDS with conflict-free ds_read_b32 (odd row stride CW + 1).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "common.hpp"
+#include "ctx.hpp"
+#include "split.hpp"
+#include "words.hpp"
+
+namespace vrpms {
+
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) const uint64_t lds_u64;
+typedef __attribute__((address_space(3))) unsigned char lds_uc;
+
+// v_perm selectors: bytes (x, 0, y, 0) of the 8-byte value {hi_word, lo_word}
+constexpr uint32_t kSel01 = 0x0c010c00u;  // (c0, c1) of one word
+constexpr uint32_t kSel12 = 0x0c020c01u;
+constexpr uint32_t kSel23 = 0x0c030c02u;
+constexpr uint32_t kSel30 = 0x0c040c03u;  // (c3 of lo_word = previous, c0 of hi_word = current)
+
+// One customer of the branch-free split (split.hpp SplitAcc::step), with the
+// route-closure value formed by v_and_or_b32 on a VGPR-resident smask.
+// (A v_ashrrev/v_bfi form with VGPR lane masks was measured 1-9 % slower:
+// inline asm makes LLVM pad every use with s_nop.)
+VRPMS_DEV void split_step(SplitAcc& s, uint64_t e, uint32_t vsmask, uint32_t kinc,
+                          uint32_t deadacc) {
+  const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
+  const uint32_t t = s.acc + lo;
+  const bool fits = (int32_t)t < 0;
+  const uint32_t rdm = fits ? 0u : ((s.acc & vsmask) | kinc);
+  s.dsum += rdm;
+  s.dmax = max(s.dmax, rdm);
+  const bool exhausted = (int32_t)s.dsum < 0;
+  s.acc = fits ? t : (exhausted ? deadacc : hi);
+}
+
+// Copy the packed matrix E into LDS (16-byte vectors + an 8-byte tail).
+VRPMS_DEV void stage_table(const uint64_t* pack, int N, unsigned char* smem) {
+  const uint32_t ebytes = (uint32_t)N * N * 8;
+  const v4u* src = reinterpret_cast<const v4u*>(pack);
+  v4u* dst = reinterpret_cast<v4u*>(smem);
+  for (uint32_t i = threadIdx.x; i < ebytes / 16; i += blockDim.x) dst[i] = src[i];
+  if ((ebytes & 8u) && threadIdx.x == 0)
+    reinterpret_cast<uint64_t*>(smem)[ebytes / 8 - 1] = pack[ebytes / 8 - 1];
+  __syncthreads();
+}
+
+// ILP independent split chains of one lane, fed four customers (one word)
+// at a time.
+template <int ILP>
+struct WordChains {
+  SplitAcc sa[ILP];
+  uint32_t wprev[ILP];  // previous word (its byte 3 is the depot before the first word)
+  uint32_t vsmask, kinc, deadacc, ebase;
+  us2 w8;
+
+  VRPMS_DEV void setup(const FastSplit& f, unsigned char* smem) {
+    ebase = (uint32_t)(uintptr_t)(lds_uc*)smem;
+    w8 = {(unsigned short)(8 * f.N), (unsigned short)8};
+    kinc = 1u << f.ks;
+    deadacc = f.dead;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(vsmask) : "s"(f.smask));
+  }
+  VRPMS_DEV void reset(const FastSplit& f) {
+#pragma unroll
+    for (int i = 0; i < ILP; ++i) {
+      sa[i].init(f);
+      wprev[i] = 0;
+    }
+  }
+  // E entry of the customer pair v_perm laid out as u16 halves; the table's
+  // LDS base rides in the dot's accumulator, so the read needs no add.
+  VRPMS_DEV uint64_t gat(uint32_t pair) const {
+    const uint32_t addr = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, pair), w8, ebase, false);
+    return *(lds_u64*)(uintptr_t)addr;
+  }
+  // the four gathers of word wd (wp = the word before it)
+  VRPMS_DEV void issue(uint64_t (&g)[ILP][4], const uint32_t (&wd)[ILP],
+                       const uint32_t (&wp)[ILP]) const {
+#pragma unroll
+    for (int i = 0; i < ILP; ++i) {
+      g[i][0] = gat(__builtin_amdgcn_perm(wd[i], wp[i], kSel30));
+      g[i][1] = gat(__builtin_amdgcn_perm(wd[i], wd[i], kSel01));
+      g[i][2] = gat(__builtin_amdgcn_perm(wd[i], wd[i], kSel12));
+      g[i][3] = gat(__builtin_amdgcn_perm(wd[i], wd[i], kSel23));
+    }
+  }
+  VRPMS_DEV void steps(const uint64_t (&g)[ILP][4]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < ILP; ++i) split_step(sa[i], g[i][q], vsmask, kinc, deadacc);
+  }
+  // next word's address math (perm + dot2) interleaved into this word's
+  // split chain, each ds_read well after its dot2
+  VRPMS_DEV static void interleave() {
+#pragma unroll
+    for (int q = 0; q < 4 * ILP; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x2, 10, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+  }
+  // a partial last word of rem (1..3) customers
+  VRPMS_DEV void partial(const uint32_t (&x)[ILP], int rem) {
+#pragma unroll
+    for (int i = 0; i < ILP; ++i) {
+      const uint32_t sel[3] = {kSel30, kSel01, kSel12};
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        if (q < rem)
+          split_step(sa[i], gat(__builtin_amdgcn_perm(x[i], q ? x[i] : wprev[i], sel[q])), vsmask,
+                     kinc, deadacc);
+      wprev[i] = x[i];
+    }
+  }
+};
+
+VRPMS_DEV void store_cost(const FastSplit& f, const SplitAcc& s, int n, int64_t c,
+                          uint64_t* keys, int32_t* sums, int32_t* maxs, int32_t* unv) {
+  const TourCost tc = s.finish(f, n);
+  keys[c] = tc.key;
+  if (sums) sums[c] = tc.sum;
+  if (maxs) maxs[c] = tc.max;
+  if (unv) unv[c] = tc.unv;
+}
+
+template <int R, int ILP>
+__global__ __launch_bounds__(1024) void eval_cvrp_words2(WordsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  stage_table(a.f.pack, a.f.N, smem);
+  WordChains<ILP> ch;
+  ch.setup(a.f, smem);
+  const int64_t C = a.C;
+  const int n = a.n, nw = (n + 3) >> 2, nfull = n >> 2;
+  constexpr int SPAN = 1024 * ILP;  // candidates per workgroup pass
+  const int64_t stride = (int64_t)gridDim.x * SPAN;
+  const int nblk = nfull / R;  // blocks of R full words: the fast loop
+
+  for (int64_t c0 = blockIdx.x * (int64_t)SPAN; c0 < C; c0 += stride) {
+    // a lane's i-th candidate is c0 + tid + 1024 i (re-pointed at its first
+    // one when past the end: computed, never stored).  Word w of every
+    // candidate of this pass lives at row(w) = words + w*C + c0 (uniform,
+    // SGPR) plus the lane's 32-bit offset.
+    uint32_t lane[ILP];
+    bool live[ILP];
+#pragma unroll
+    for (int i = 0; i < ILP; ++i) {
+      live[i] = c0 + threadIdx.x + 1024 * i < C;
+      lane[i] = live[i] ? threadIdx.x + 1024u * i : threadIdx.x;
+    }
+    if (!live[0]) continue;
+    const uint32_t* row = a.words + c0;
+    uint32_t ring[ILP][R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+#pragma unroll
+      for (int i = 0; i < ILP; ++i) ring[i][u] = u < nw ? row[lane[i]] : 0u;
+      row += C;
+    }
+    ch.reset(a.f);
+    // software pipeline: the gathers of word w + 1 are issued before the
+    // split steps of word w consume theirs
+    uint64_t e[ILP][4];
+    if (nblk > 0) {
+      uint32_t w0[ILP];
+#pragma unroll
+      for (int i = 0; i < ILP; ++i) w0[i] = ring[i][0];
+      ch.issue(e, w0, ch.wprev);
+    }
+    // one word: refill its ring slot, issue the next word's gathers, step
+    auto word = [&](int u, bool refill, bool has_next) {
+      uint32_t wd[ILP], wn[ILP];
+#pragma unroll
+      for (int i = 0; i < ILP; ++i) {
+        wd[i] = ring[i][u];
+        if (refill) ring[i][u] = row[lane[i]];  // word w + R
+      }
+      if (refill) row += C;
+      uint64_t f[ILP][4];
+      if (has_next) {
+#pragma unroll
+        for (int i = 0; i < ILP; ++i) wn[i] = ring[i][(u + 1) % R];
+        ch.issue(f, wn, wd);
+      }
+      ch.interleave();
+      ch.steps(e);
+#pragma unroll
+      for (int i = 0; i < ILP; ++i) {
+        ch.wprev[i] = wd[i];
+        if (has_next)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) e[i][q] = f[i][q];
+      }
+    };
+    for (int b = 0; b + 1 < nblk; ++b) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) word(u, true, true);
+    }
+    if (nblk > 0) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) word(u, false, u + 1 < R);  // last block: no refills
+    }
+    // ragged tail (n not a multiple of 4R): word by word, the last one partial
+    for (int w = nblk * R; w < nw; ++w) {
+      const int rem = min(4, n - 4 * w);  // uniform
+      const uint32_t* rw = a.words + c0 + (int64_t)w * C;
+      uint32_t x[ILP];
+#pragma unroll
+      for (int i = 0; i < ILP; ++i) x[i] = rw[lane[i]];
+      if (rem == 4) {
+        ch.issue(e, x, ch.wprev);
+        ch.steps(e);
+#pragma unroll
+        for (int i = 0; i < ILP; ++i) ch.wprev[i] = x[i];
+      } else {
+        ch.partial(x, rem);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < ILP; ++i)
+      if (live[i])
+        store_cost(a.f, ch.sa[i], n, c0 + threadIdx.x + 1024 * i, a.keys, a.sums, a.maxs, a.unv);
+  }
+}
+
+// Row-major tours: 2048-row tiles, 128 rows per wave (rows l and l + 64 of
+// the wave's slice on lane l), staged through a wave-private LDS slice CW
+// words per row at a time.  Wave-private staging needs no workgroup
+// barrier: the 16 waves drift apart, so one wave's chunk transition
+// (prefetch wait, LDS store, pipeline refill) overlaps the others' gathers.
+template <int CW>
+__global__ __launch_bounds__(1024) void eval_cvrp_rows2(RowsArgs a) {
+  constexpr int RS = CW + 1;     // LDS row stride in dwords: odd, so b32 reads are conflict-free
+  constexpr int TR = 2048;       // rows per tile
+  constexpr int WR = 128;        // rows per wave
+  constexpr int LPT = 2 * CW;    // staging dwords per lane per chunk
+  constexpr int RPJ = 64 / CW;   // wave-slice rows per staging step
+  static_assert(64 % CW == 0, "CW must divide 64");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int N = a.f.N;
+  stage_table(a.f.pack, N, smem);
+  const uint32_t e16 = ((uint32_t)N * N * 8 + 15u) & ~15u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63u;
+  uint32_t* T = reinterpret_cast<uint32_t*>(smem + e16) + wave * WR * RS;
+  WordChains<2> ch;
+  ch.setup(a.f, smem);
+  const int64_t C = a.C;
+  const int n = a.n, nw = (n + 3) >> 2, nfull = n >> 2;
+  const int nchunks = (nw + CW - 1) / CW;
+  const int fullch = nfull / CW;  // chunks made of full words only
+  const uint32_t ldw = (uint32_t)a.ld >> 2;
+  // staging map: dword l + 64 j of a chunk is word l % CW of slice row
+  // l / CW + j * RPJ; CW consecutive lanes read one 4*CW-byte row segment.
+  // Addresses are a uniform (SGPR) base per j plus one 32-bit lane offset.
+  const uint32_t r0 = l / CW, wl = l % CW;
+  const int64_t tstride = (int64_t)gridDim.x * TR;
+  uint32_t pf[LPT];
+  // Chunk k of the wave's slice starting at row t, through a buffer
+  // resource bounded at row C: rows past C (ragged last tile) read as 0 with
+  // no fault and no branch; words past the tour are never used.
+  const uint32_t lane_off = (r0 * ldw + wl) * 4;
+  auto load_chunk = [&](int64_t t, int k) {
+    // (wave-uniform values only: readfirstlane keeps the descriptor in SGPRs)
+    const int64_t rows = t < C ? C - t : 0;
+    const int nrec = __builtin_amdgcn_readfirstlane(rows < WR ? (int)rows * a.ld : WR * a.ld);
+    const int64_t tb = t < C ? t : 0;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned char*>(a.perms) + tb * (int64_t)a.ld, (short)0, nrec, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < LPT; ++j)
+      pf[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(
+          rs, lane_off + (uint32_t)(k * CW * 4 + j * RPJ * a.ld), 0, 0);
+  };
+  const uint32_t toff = (uint32_t)(uintptr_t)(lds_uc*)T + l * RS * 4;
+  typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+  // word j of the lane's row i of the staged chunk (conflict-free ds_read_b32)
+  auto tw = [&](int i, int j) {
+    return *(lds_u32*)(uintptr_t)(toff + (uint32_t)(i * 64 * RS * 4 + 4 * j));
+  };
+  // pf holds chunk k of the current tile: store it into the wave's slice
+  // and prefetch what follows (the next chunk, or the next tile's first).
+  // One wave owns the slice, and LDS keeps a wave's order, so its reads of
+  // the previous chunk precede these stores and the stores precede the
+  // reads after them; wave_barrier only pins the compiler's order.
+  int64_t t0 = blockIdx.x * (int64_t)TR;
+  if (t0 < C && nchunks > 0) load_chunk(t0 + wave * WR, 0);  // n == 0: no tour words at all
+  for (; t0 < C; t0 += tstride) {
+    ch.reset(a.f);
+    for (int k = 0; k < nchunks; ++k) {
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int j = 0; j < LPT; ++j) T[(r0 + j * RPJ) * RS + wl] = pf[j];
+      __builtin_amdgcn_wave_barrier();
+      // in flight during the steps below
+      if (k + 1 < nchunks) load_chunk(t0 + wave * WR, k + 1);
+      else if (t0 + tstride < C) load_chunk(t0 + tstride + wave * WR, 0);
+      if (k < fullch) {
+        // software pipeline: the gathers of word j + 1 are issued before
+        // the split steps of word j consume theirs
+        uint64_t e[2][4];
+        uint32_t cur[2] = {tw(0, 0), tw(1, 0)};
+        ch.issue(e, cur, ch.wprev);
+#pragma unroll
+        for (int j = 0; j < CW; ++j) {
+          uint64_t f[2][4];
+          uint32_t nx[2];
+          if (j + 1 < CW) {
+            nx[0] = tw(0, j + 1);
+            nx[1] = tw(1, j + 1);
+            ch.issue(f, nx, cur);
+          }
+          ch.steps(e);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            ch.wprev[i] = cur[i];
+            if (j + 1 < CW) {
+              cur[i] = nx[i];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) e[i][q] = f[i][q];
+            }
+          }
+        }
+      } else {
+        // last chunk: full words, then the partial one (uniform guards)
+#pragma unroll
+        for (int j = 0; j < CW; ++j) {
+          const int w = k * CW + j;
+          const uint32_t cur[2] = {w < nw ? tw(0, j) : 0u, w < nw ? tw(1, j) : 0u};
+          if (w < nfull) {
+            uint64_t g[2][4];
+            ch.issue(g, cur, ch.wprev);
+            ch.steps(g);
+            ch.wprev[0] = cur[0];
+            ch.wprev[1] = cur[1];
+          } else if (w < nw) {
+            ch.partial(cur, n - 4 * w);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t c = t0 + wave * WR + l + 64 * i;
+      if (c < C) store_cost(a.f, ch.sa[i], n, c, a.keys, a.sums, a.maxs, a.unv);
+    }
+  }
+}
+
+int launch_words2(const vrpms_ctx* ctx, const WordsArgs& w, int R, hipStream_t s) {
+  const int ilp = ctx->opt_words_ilp == 1 ? 1 : 2;  // auto: two chains per lane
+  const Instance& in = ctx->inst;
+  const size_t lds = ((size_t)in.N * in.N * 8 + 15) & ~(size_t)15;
+  // ILP2 needs > 64 VGPRs: one 1024-lane workgroup per CU; ILP1 fits two
+  const int per_cu = ilp == 2 ? 1 : std::max<int>(1, std::min<int>(2, (int)(ctx->max_lds / lds)));
+  const int64_t blocks = (w.C + 1024 * ilp - 1) / (1024 * ilp);
+  const int grid = (int)std::min<int64_t>(blocks, (int64_t)ctx->num_cus * per_cu);
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    kern<<<grid, 1024, lds, s>>>(w);
+  };
+  if (ilp == 2) {
+    switch (R) {
+      case 4: go(eval_cvrp_words2<4, 2>); break;
+      case 5: go(eval_cvrp_words2<5, 2>); break;
+      case 6: go(eval_cvrp_words2<6, 2>); break;
+      case 7: go(eval_cvrp_words2<7, 2>); break;
+      default: go(eval_cvrp_words2<8, 2>); break;
+    }
+  } else {
+    switch (R) {
+      case 4: go(eval_cvrp_words2<4, 1>); break;
+      case 5: go(eval_cvrp_words2<5, 1>); break;
+      case 6: go(eval_cvrp_words2<6, 1>); break;
+      case 7: go(eval_cvrp_words2<7, 1>); break;
+      default: go(eval_cvrp_words2<8, 1>); break;
+    }
+  }
+  VRPMS_HIP(hipGetLastError());
+  return VRPMS_OK;
+}
+
+int rows2_chunk_words(const vrpms_ctx* ctx, const FastSplit& f) {
+  const size_t e16 = ((size_t)f.N * f.N * 8 + 15) & ~(size_t)15;
+  if (e16 + 2048 * (8 + 1) * 4 <= ctx->max_lds) return 8;
+  if (e16 + 2048 * (4 + 1) * 4 <= ctx->max_lds) return 4;
+  return 0;
+}
+
+int launch_rows2(const vrpms_ctx* ctx, const RowsArgs& r, hipStream_t s) {
+  const int cw = rows2_chunk_words(ctx, r.f);
+  if (cw == 0 || (r.ld & 3) != 0 || ((uintptr_t)r.perms & 3u) != 0)
+    return fail(VRPMS_EINVAL, "launch_rows2: tile does not fit LDS or rows unaligned");
+  const size_t e16 = ((size_t)r.f.N * r.f.N * 8 + 15) & ~(size_t)15;
+  const size_t lds = e16 + (size_t)2048 * (cw + 1) * 4;
+  const int64_t tiles = (r.C + 2047) / 2048;
+  const int grid = (int)std::min<int64_t>(tiles, (int64_t)ctx->num_cus);
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    kern<<<grid, 1024, lds, s>>>(r);
+  };
+  if (cw == 8) go(eval_cvrp_rows2<8>);
+  else go(eval_cvrp_rows2<4>);
+  VRPMS_HIP(hipGetLastError());
+  return VRPMS_OK;
+}
+
+}  // namespace vrpms

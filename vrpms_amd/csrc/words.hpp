@@ -1,0 +1,51 @@
+// LDS-packed scoring family: shared argument blocks of eval_cvrp_words
+// (eval.hip), eval_cvrp_words2 and eval_cvrp_rows2 (eval_words.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ctx.hpp"
+#include "split.hpp"
+
+namespace vrpms {
+
+// Word-interleaved tours (VRPMS_LAYOUT_WORDS): word w of candidate c holds
+// tour positions 4w..4w+3 as bytes, at words[w * C + c].
+struct WordsArgs {
+  FastSplit f;
+  const uint32_t* words;  // uint32 [ceil(n/4)][C]
+  int64_t C;
+  int n;
+  uint64_t* keys;
+  int32_t* sums;
+  int32_t* maxs;
+  int32_t* unv;
+};
+
+// Row-major uint8 tours (the vrpms_eval layout, perm_bytes == 1): candidate
+// c at perms[c * ld .. c * ld + n), ld % 4 == 0, perms 16-byte aligned.
+// eval_cvrp_rows2 stages 2048-row tiles through LDS in chunks of CW words,
+// so the API layout needs no transpose.
+struct RowsArgs {
+  FastSplit f;
+  const unsigned char* perms;
+  int64_t C;
+  int n;
+  int ld;
+  uint64_t* keys;
+  int32_t* sums;
+  int32_t* maxs;
+  int32_t* unv;
+};
+
+// Launch eval_cvrp_words2 with ring depth R (4..8) on stream s.
+int launch_words2(const vrpms_ctx* ctx, const WordsArgs& w, int R, hipStream_t s);
+
+// Words per row per LDS stage eval_cvrp_rows2 can use beside the packed
+// matrix: 8, 4, or 0 when no tile fits the LDS budget.
+int rows2_chunk_words(const vrpms_ctx* ctx, const FastSplit& f);
+
+// Launch eval_cvrp_rows2 on stream s (caller checked rows2_chunk_words > 0).
+int launch_rows2(const vrpms_ctx* ctx, const RowsArgs& r, hipStream_t s);
+
+}  // namespace vrpms
