@@ -11,9 +11,13 @@ collective in the data path) -> weak scaling; the driver launches one
 process per GPU via torch.distributed.run.
 
 Reported beside the value:
-  roofline      the dominant kernel (eval_cvrp_packed) timed with HIP events
-                on the stream it runs on; achieved = algorithmic HBM bytes per
-                launch (C x (100 B tour + 8 B key)) / mean launch time.
+  roofline      the dominant kernel (eval_cvrp_words2, word-interleaved
+                tours) timed with HIP events on the stream it runs on;
+                achieved = algorithmic HBM bytes per launch (C x (100 B tour +
+                8 B key)) / mean launch time.  The kernel is LDS-gather bound:
+                lds_gather_roofline prices it against the measured random
+                ds_read_b64 rate.  rows_layout times the same batch in the
+                API's row-major layout (eval_cvrp_rows2).
   cpu_baseline  the C restatement of the spec (oracle/oracle_c.c, OpenMP)
                 on a bounded sample of the same workload, rank 0 only.
 """
@@ -314,6 +318,7 @@ def main():
             qual = {"error": traceback.format_exc(limit=3)}
 
     if rank == 0:
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
         nbytes = 4 * ((n + 3) // 4)
         bytes_per_launch = C * (nbytes + 8)
         achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
@@ -336,13 +341,13 @@ def main():
                        "parallelism": f"islands{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": pmc_traffic("eval_cvrp_words",
-                                                min((C + 1023) // 1024, 512) * 1024),
+                         "traffic": pmc_traffic("eval_cvrp_words2",
+                                                min((C + 2047) // 2048, cus) * 1024),
                          "traffic_unit": "bytes/launch (PMC, profiles/pmc_traffic.json)",
-                         "kernel": "eval_cvrp_words", "kernel_ms": kernel_ms,
+                         "kernel": "eval_cvrp_words2", "kernel_ms": kernel_ms,
                          "bytes_per_launch": bytes_per_launch,
                          "lds_gathers_per_s": C * n / (kernel_ms * 1e-3)},
-            "rows_layout": {"kernel": "eval_cvrp_packed", "evals_per_s": C / (rows_ms * 1e-3),
+            "rows_layout": {"kernel": "eval_cvrp_rows2", "evals_per_s": C / (rows_ms * 1e-3),
                             "kernel_ms": rows_ms},
         }
         # north-star roofline: random LDS gathers, G = n + K per eval,

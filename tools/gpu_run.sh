@@ -38,7 +38,7 @@ for step in "$@"; do
       cd "$ROOT" ;;
     pmc)
       cd /tmp
-      B="python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline"
+      B="python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --quality-seconds 0 --no-other-configs"
       run pmc_a 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS \
           --output-format csv -d "$OUT/pmc_a" -o run -- $B
       run pmc_b 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_SCA \
