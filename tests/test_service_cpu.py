@@ -1,0 +1,199 @@
+"""HTTP host (vrpms_amd/service.py) against the reference's wire contract.
+
+Every byte the reference's handlers emit without running an algorithm --
+GET banners, the VRP GA preflight, missing-parameter and missing-record
+error lists, the zero-result responses and the save payload -- is pinned by
+tests/golden/reference_fixtures.json (captured from the reference's own
+handler classes).  The solver is injected here (the zero result the
+reference's TODO slot returns); tests/test_service_gpu.py runs the real one.
+"""
+import io
+import json
+import os
+import threading
+import urllib.error
+import urllib.request
+
+import pytest
+
+from vrpms_amd import service
+
+FX = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_fixtures.json")))
+WIRE = FX["wire"]
+ENDPOINTS = sorted(WIRE)
+
+FULL = {
+    "vrp": {"solutionName": "n", "solutionDescription": "d", "locationsKey": 1,
+            "durationsKey": 2, "capacities": [5, 5], "startTimes": [0, 30],
+            "ignoredCustomers": [], "completedCustomers": [], "multiThreaded": False,
+            "randomPermutationCount": 10, "iterationCount": 5},
+    "tsp": {"solutionName": "n", "solutionDescription": "d", "locationsKey": 1,
+            "durationsKey": 2, "customers": [1, 2, 3], "startNode": 0, "startTime": 0},
+}
+MATRIX = [[0, 5, 6, 7], [5, 0, 8, 9], [6, 8, 0, 4], [7, 9, 4, 0]]
+
+
+def store():
+    return service.MemoryStore({1: [{"id": i} for i in range(4)]}, {2: MATRIX},
+                               {"jwt": "tester@example.com"})
+
+
+def zero_solve(problem, algorithm, params, knobs, locations, durations):
+    """The reference's TODO-slot result."""
+    if problem == "tsp":
+        return {"duration": 0, "vehicle": []}
+    return {"durationMax": 0, "durationSum": 0, "vehicles": []}
+
+
+def call(handler_cls, method, body=None, raw=None):
+    """Drive one request through a handler class without a socket (the same
+    harness tests/golden/gen_reference_fixtures.py used on the reference)."""
+    h = handler_cls.__new__(handler_cls)
+    data = raw if raw is not None else (json.dumps(body).encode() if body is not None else b"")
+    h.rfile = io.BytesIO(data)
+    h.wfile = io.BytesIO()
+    h.headers = {"Content-Length": str(len(data))}
+    h.request_version = "HTTP/1.0"
+    h.requestline = f"{method} / HTTP/1.0"
+    h.command = method
+    h.client_address = ("127.0.0.1", 0)
+    getattr(h, "do_" + method)()
+    text = h.wfile.getvalue().decode()
+    head, _, payload = text.partition("\r\n\r\n")
+    lines = head.split("\r\n")
+    headers = [ln for ln in lines[1:] if not ln.startswith(("Date:", "Server:"))]
+    return {"status_line": lines[0], "headers": headers, "body": payload}
+
+
+def handler(ep, app=None):
+    problem, algorithm = ep.split("/")
+    return service.endpoint_handler(app or service.App(store(), solve=zero_solve),
+                                    problem, algorithm)
+
+
+@pytest.mark.parametrize("ep", ENDPOINTS)
+def test_get_banner_and_preflight(ep):
+    h = handler(ep)
+    assert call(h, "GET") == WIRE[ep]["GET"]
+    if "OPTIONS" in WIRE[ep]:
+        assert call(h, "OPTIONS") == WIRE[ep]["OPTIONS"]
+    else:
+        assert not hasattr(h, "do_OPTIONS")
+
+
+@pytest.mark.parametrize("ep", ENDPOINTS)
+def test_post_errors_and_zero_results(ep):
+    h = handler(ep)
+    body = FULL[ep.split("/")[0]]
+    assert call(h, "POST", {}) == WIRE[ep]["POST_empty"]
+    assert call(h, "POST", {**body, "durationsKey": 99}) == WIRE[ep]["POST_missing_db"]
+    assert call(h, "POST", body) == WIRE[ep]["POST_full"]
+
+
+@pytest.mark.parametrize("ep", ENDPOINTS)
+def test_post_auth_saves_the_reference_payload(ep):
+    st = store()
+    h = handler(ep, service.App(st, solve=zero_solve))
+    problem = ep.split("/")[0]
+    body = {**FULL[problem], "auth": "jwt"}
+    if problem == "vrp":
+        body["ignoredCustomers"] = [2]
+    assert call(h, "POST", body) == WIRE[ep]["POST_auth"]
+    assert [{"table": "solutions", "data": row} for row in st.solutions] == \
+        WIRE[ep]["POST_auth_insert"]
+
+
+@pytest.mark.parametrize("problem", ["vrp", "tsp"])
+def test_save_with_unknown_token_is_not_permitted(problem):
+    st = store()
+    h = handler(f"{problem}/sa", service.App(st, solve=zero_solve))
+    r = call(h, "POST", {**FULL[problem], "auth": "expired"})
+    assert r["status_line"] == "HTTP/1.0 400 Bad Request"
+    err = json.loads(r["body"])["errors"]
+    assert err[0]["what"] == "Not permitted" and st.solutions == []
+
+
+def test_missing_locations_and_durations_both_reported():
+    r = call(handler("vrp/ga"), "POST", {**FULL["vrp"], "locationsKey": 7, "durationsKey": 8})
+    errs = json.loads(r["body"])["errors"]
+    assert [e["reason"].split(".")[0] for e in errs] == [
+        "No location set found with given id 7", "No duration matrix found with given id 8"]
+
+
+def test_invalid_json_and_non_object_bodies():
+    h = handler("tsp/ga")
+    for raw in (b"{not json", b"[1, 2]"):
+        r = call(h, "POST", raw=raw)
+        assert r["status_line"] == "HTTP/1.0 400 Bad Request"
+        assert json.loads(r["body"])["errors"][0]["what"] == "Invalid request"
+
+
+def test_solver_errors_become_400():
+    def boom(*a):
+        raise ValueError("3 locations but a 4-node duration matrix")
+    r = call(handler("vrp/bf", service.App(store(), solve=boom)), "POST", FULL["vrp"])
+    assert r["status_line"] == "HTTP/1.0 400 Bad Request"
+    assert json.loads(r["body"])["errors"] == [
+        {"what": "Solver error", "reason": "3 locations but a 4-node duration matrix"}]
+
+
+def test_gpu_solver_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by tests/test_service_gpu.py")
+    r = call(handler("tsp/sa", service.App(store())), "POST", FULL["tsp"])
+    assert r["status_line"] == "HTTP/1.0 400 Bad Request"
+    err = json.loads(r["body"])["errors"][0]
+    assert err["what"] == "Solver error" and "GPU" in err["reason"]
+
+
+def test_parse_matches_reference_parsers():
+    names = {("vrp", None): "parse_common_vrp_parameters", ("vrp", "ga"): "parse_vrp_ga_parameters",
+             ("vrp", "sa"): "parse_vrp_sa_parameters", ("vrp", "aco"): "parse_vrp_aco_parameters",
+             ("tsp", None): "parse_common_tsp_parameters", ("tsp", "ga"): "parse_tsp_ga_parameters",
+             ("tsp", "sa"): "parse_tsp_sa_parameters", ("tsp", "aco"): "parse_tsp_aco_parameters"}
+    for (problem, algo), name in names.items():
+        for label, case in FX["parse"][name].items():
+            body = {"empty": {}, "vrp_full": FULL["vrp"], "tsp_full": FULL["tsp"],
+                    "falsy": {k: 0 for k in FULL["vrp"]}}[label]
+            errors = []
+            common, knobs = service.parse(problem, algo or "bf", dict(body), errors)
+            got = common if algo is None else knobs
+            want_err = case["errors"] if algo is None else case["errors"]
+            assert got == case["params"], (name, label)
+            if algo is None:
+                assert errors[:len(want_err)] == want_err, (name, label)
+
+
+def test_memory_store_json_roundtrip(tmp_path):
+    p = tmp_path / "db.json"
+    p.write_text(json.dumps({"locations": {"1": [{"id": 0}]}, "durations": {"2": [[0]]},
+                             "users": {"t": "a@b"}}))
+    st = service.MemoryStore.from_json(str(p))
+    s = st.session("t")
+    errs = []
+    assert s.get_locations_by_id(1, errs) == [{"id": 0}]
+    assert s.get_durations_by_id("2", errs) == [[0]]
+    assert s.get_durations_by_id([1], errs) is None and len(errs) == 1
+
+
+def test_router_over_http():
+    srv = service.serve(service.App(store(), solve=zero_solve), "127.0.0.1", 0)
+    port = srv.server_address[1]
+    th = threading.Thread(target=srv.serve_forever, daemon=True)
+    th.start()
+    opener = urllib.request.build_opener(urllib.request.ProxyHandler({}))
+    base = f"http://127.0.0.1:{port}"
+    try:
+        assert opener.open(base + "/api").read() == b"Hello!"
+        assert opener.open(base + "/api/vrp/aco").read() == \
+            WIRE["vrp/aco"]["GET"]["body"].encode()
+        req = urllib.request.Request(base + "/api/tsp/ga", data=json.dumps(FULL["tsp"]).encode(),
+                                     headers={"Content-Type": "application/json"})
+        assert json.loads(opener.open(req).read()) == json.loads(WIRE["tsp/ga"]["POST_full"]["body"])
+        with pytest.raises(urllib.error.HTTPError) as e:
+            opener.open(base + "/api/nope")
+        assert e.value.code == 404
+    finally:
+        srv.shutdown()
+        srv.server_close()

@@ -1,0 +1,328 @@
+"""GPU-box HTTP host for the eight solver endpoints.
+
+The reference serves each algorithm as a Vercel function
+(api/{tsp,vrp}/{bf,ga,sa,aco}/index.py): parse the body, fetch the location
+set and duration matrix from Supabase, run the algorithm (the
+`# TODO: Run algorithm` slot), optionally save the solution, respond.  This
+module keeps that request/response contract byte for byte -- banners,
+preflight headers, error lists, status lines, the save payload -- and fills
+the slot with the GPU solver (vrpms_amd.solver).  One process owns one GPU
+context; requests are served by a threading HTTP server and reach the GPU
+one at a time (the solver's context is per process).
+
+Storage is pluggable: anything with the three calls of the reference's
+Database classes (api/database.py) works.  `MemoryStore` (JSON-backed, the
+default and the one the tests use) returns the reference's exact error
+messages; a Supabase adapter is sketched in INTEGRATION.md §6.
+
+  python -m vrpms_amd.service --port 8000 --data instances.json
+
+Deliberate differences: a body that is not JSON gets a 400 with
+{'what': 'Invalid request'} (the reference's handler raises and drops the
+connection), and a solver exception becomes a 400 {'what': 'Solver error'}.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import threading
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+TITLES = {"bf": "Brute Force", "ga": "Genetic Algorithm", "sa": "Simulated Annealing",
+          "aco": "Ant Colony Optimization"}
+
+# (body key, params key) in the order the reference checks them
+# (api/parameters.py:4-15 and 34-44); 'auth' is the only optional one
+_COMMON = {
+    "vrp": [("solutionName", "name"), ("auth", "auth"), ("solutionDescription", "description"),
+            ("locationsKey", "locations_key"), ("durationsKey", "durations_key"),
+            ("capacities", "capacities"), ("startTimes", "start_times"),
+            ("ignoredCustomers", "ignored_customers"),
+            ("completedCustomers", "completed_customers")],
+    "tsp": [("solutionName", "name"), ("auth", "auth"), ("solutionDescription", "description"),
+            ("locationsKey", "locations_key"), ("durationsKey", "durations_key"),
+            ("customers", "customers"), ("startNode", "start_node"), ("startTime", "start_time")],
+}
+# algorithm knobs (api/parameters.py:18-23; every other algorithm takes none)
+_KNOBS = {("vrp", "ga"): [("multiThreaded", "multi_threaded"),
+                          ("randomPermutationCount", "random_permutationCount"),
+                          ("iterationCount", "iteration_count")]}
+
+
+def get_parameter(name, content, errors, optional=False):
+    """api/helpers.py:5-8."""
+    if name not in content and not optional:
+        errors += [{"what": "Missing parameter", "reason": f"'{name}' was not provided"}]
+    return content.get(name)
+
+
+def parse(problem: str, algorithm: str, content: dict, errors: list):
+    """(common params, algorithm params) exactly as parse_common_*_parameters
+    and parse_*_<algo>_parameters build them."""
+    common = {key: get_parameter(name, content, errors, optional=(name == "auth"))
+              for name, key in _COMMON[problem]}
+    knobs = {key: get_parameter(name, content, errors)
+             for name, key in _KNOBS.get((problem, algorithm), [])}
+    return common, knobs
+
+
+def remove_unused_locations(locations, ignored_customers, completed_customers):
+    """api/helpers.py:11-13."""
+    disregard = ignored_customers + completed_customers
+    return [loc for loc in locations if loc["id"] not in disregard]
+
+
+# ---------------------------------------------------------------------------
+# storage
+# ---------------------------------------------------------------------------
+_NOT_FOUND = ("Make sure you are accessing public data or data owned by you. "
+              "Check if your authentication token has expired.")
+_NOT_PERMITTED = {
+    "vrp": ("An authentication token is required to save solutions to database. "
+            "Please provide 'auth' with a valid JWT token in the request body. "
+            "If you have already provided a token, it has very likely expired."),
+    "tsp": ("An authentication token is required to save solutions to database."
+            " Please provide 'auth' with a valid JWT token in the request body"),
+}
+
+
+class MemoryStore:
+    """In-process stand-in for the Supabase tables the handlers use:
+    `locations` {id: [location, ...]}, `durations` {id: matrix},
+    `users` {token: email}; saved rows are appended to `solutions`."""
+
+    def __init__(self, locations=None, durations=None, users=None):
+        self.locations = dict(locations or {})
+        self.durations = dict(durations or {})
+        self.users = dict(users or {})
+        self.solutions = []
+        self._lock = threading.Lock()
+
+    @classmethod
+    def from_json(cls, path):
+        """{"locations": {"1": [...]}, "durations": {"2": [[...]]}, "users": {...}};
+        ids are matched as strings or ints."""
+        with open(path) as f:
+            raw = json.load(f)
+        return cls(raw.get("locations"), raw.get("durations"), raw.get("users"))
+
+    def session(self, auth):
+        return _Session(self, auth)
+
+    def _get(self, table, key):
+        for k in (key, str(key)):
+            try:
+                if k in table:
+                    return table[k]
+            except TypeError:       # unhashable id from the request body
+                return None
+        return None
+
+
+class _Session:
+    """The per-request Database object of api/database.py."""
+
+    def __init__(self, store: MemoryStore, auth):
+        self.store = store
+        self.email = store.users.get(auth) if isinstance(auth, str) else None
+
+    def get_locations_by_id(self, key, errors):
+        rows = self.store._get(self.store.locations, key)
+        if rows is None:
+            errors += [{"what": "Database read error",
+                        "reason": f"No location set found with given id {key}. " + _NOT_FOUND}]
+        return rows
+
+    def get_durations_by_id(self, key, errors):
+        m = self.store._get(self.store.durations, key)
+        if m is None:
+            errors += [{"what": "Database read error",
+                        "reason": f"No duration matrix found with given id {key}. " + _NOT_FOUND}]
+        return m
+
+    def save_solution(self, problem, data: dict, errors):
+        """DatabaseVRP/DatabaseTSP.save_solution: owner from the token."""
+        if not self.email:
+            errors += [{"what": "Not permitted", "reason": _NOT_PERMITTED[problem]}]
+            return
+        row = {"name": data["name"], "description": data["description"], "owner": self.email}
+        row.update({k: v for k, v in data.items() if k not in ("name", "description")})
+        with self.store._lock:
+            self.store.solutions.append(row)
+
+
+# ---------------------------------------------------------------------------
+# the endpoint logic
+# ---------------------------------------------------------------------------
+class App:
+    """Parse -> fetch -> solve -> save -> respond for one endpoint call.
+    `solve` is injectable (tests); by default it is the GPU solver."""
+
+    def __init__(self, store, device: int = 0, seed: int = 0, max_seconds: float | None = None,
+                 solve=None):
+        self.store = store
+        self.device = device
+        self.seed = seed
+        self.max_seconds = max_seconds
+        self.gpu_lock = threading.Lock()
+        self._solve = solve or self._gpu_solve
+
+    def _gpu_solve(self, problem, algorithm, params, knobs, locations, durations):
+        from . import solver
+        if problem == "tsp":
+            return solver.solve_tsp(algorithm, durations, params["customers"],
+                                    params["start_node"], params["start_time"] or 0,
+                                    seed=self.seed, time_limit=self.max_seconds,
+                                    device=self.device)
+        extra = {}
+        if knobs.get("random_permutationCount"):
+            extra["random_permutation_count"] = int(knobs["random_permutationCount"])
+        if knobs.get("iteration_count"):
+            extra["iteration_count"] = int(knobs["iteration_count"])
+        return solver.solve_vrp(algorithm, durations, locations, params["capacities"],
+                                params["start_times"], params["ignored_customers"],
+                                params["completed_customers"], seed=self.seed,
+                                time_limit=self.max_seconds, device=self.device, **extra)
+
+    def post(self, problem: str, algorithm: str, raw: bytes):
+        """-> (status, response dict) for a POST body."""
+        text = raw.decode("utf-8") if raw else ""
+        try:
+            content = json.loads(text) if text else dict()
+        except ValueError as e:
+            return 400, {"success": False,
+                         "errors": [{"what": "Invalid request", "reason": str(e)}]}
+        if not isinstance(content, dict):
+            return 400, {"success": False, "errors": [
+                {"what": "Invalid request", "reason": "the body must be a JSON object"}]}
+        errors = []
+        params, knobs = parse(problem, algorithm, content, errors)
+        if errors:
+            return 400, {"success": False, "errors": errors}
+        db = self.store.session(params["auth"])
+        locations = db.get_locations_by_id(params["locations_key"], errors)
+        durations = db.get_durations_by_id(params["durations_key"], errors)
+        if errors:
+            return 400, {"success": False, "errors": errors}
+        try:
+            with self.gpu_lock:
+                result = self._solve(problem, algorithm, params, knobs, locations, durations)
+        except Exception as e:   # bad instance shape, GPU unavailable, ...
+            return 400, {"success": False,
+                         "errors": [{"what": "Solver error", "reason": str(e)}]}
+        if params["auth"]:
+            if problem == "vrp":
+                data = {"name": params["name"], "description": params["description"],
+                        "durationMax": result["durationMax"], "durationSum": result["durationSum"],
+                        "locations": remove_unused_locations(locations, params["ignored_customers"],
+                                                             params["completed_customers"]),
+                        "vehicles": result["vehicles"]}
+            else:
+                data = {"name": params["name"], "description": params["description"],
+                        "duration": result["duration"], "locations": locations,
+                        "vehicle": result["vehicle"]}
+            db.save_solution(problem, data, errors)
+        if errors:
+            return 400, {"success": False, "errors": errors}
+        return 200, {"success": True, "message": result}
+
+
+def endpoint_handler(app: App, problem: str, algorithm: str):
+    """A BaseHTTPRequestHandler class for one endpoint, with the reference's
+    GET banner, POST contract and (VRP GA only) preflight response."""
+    banner = f"Hi, this is the {problem.upper()} {TITLES[algorithm]} endpoint"
+
+    class Handler(BaseHTTPRequestHandler):
+        def log_message(self, *a):
+            pass
+
+        def do_GET(self):
+            self.send_response(200)
+            self.send_header("Content-type", "text/plain")
+            self.end_headers()
+            self.wfile.write(banner.encode("utf-8"))
+
+        def do_POST(self):
+            n = int(self.headers.get("Content-Length", 0))
+            status, body = app.post(problem, algorithm, self.rfile.read(n))
+            self.send_response(status)
+            self.send_header("Content-type", "application/json")
+            self.end_headers()
+            self.wfile.write(json.dumps(body).encode("utf-8"))
+
+    if (problem, algorithm) == ("vrp", "ga"):
+        def do_OPTIONS(self):   # api/vrp/ga/index.py: the header is sent twice there too
+            self.send_response(200, "ok")
+            self.send_header("Access-Control-Allow-Origin", "*")
+            self.send_header("Access-Control-Allow-Methods", "*")
+            self.send_header("Access-Control-Allow-Headers", "*")
+            self.send_header("Access-Control-Allow-Headers", "*")
+            self.end_headers()
+        Handler.do_OPTIONS = do_OPTIONS
+    return Handler
+
+
+def router(app: App):
+    """One server for every route: /api (api/index.py) and
+    /api/{tsp,vrp}/{bf,ga,sa,aco}."""
+    routes = {f"/api/{p}/{a}": endpoint_handler(app, p, a)
+              for p in ("tsp", "vrp") for a in TITLES}
+
+    class Router(BaseHTTPRequestHandler):
+        def log_message(self, *a):
+            pass
+
+        def _dispatch(self, method):
+            path = self.path.split("?", 1)[0].rstrip("/")
+            if path == "/api" and method == "GET":
+                self.send_response(200)
+                self.send_header("Content-type", "text/plain")
+                self.end_headers()
+                self.wfile.write(b"Hello!")
+                return
+            cls = routes.get(path)
+            fn = getattr(cls, "do_" + method, None) if cls else None
+            if fn is None:
+                self.send_error(404 if cls is None else 501)
+                return
+            fn(self)
+
+        def do_GET(self):
+            self._dispatch("GET")
+
+        def do_POST(self):
+            self._dispatch("POST")
+
+        def do_OPTIONS(self):
+            self._dispatch("OPTIONS")
+
+    return Router
+
+
+def serve(app: App, host: str = "127.0.0.1", port: int = 8000) -> ThreadingHTTPServer:
+    return ThreadingHTTPServer((host, port), router(app))
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=8000)
+    ap.add_argument("--data", help="MemoryStore JSON (locations / durations / users)")
+    ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--max-seconds", type=float, default=None,
+                    help="wall-time cap per solve (default: the algorithm's own budget)")
+    args = ap.parse_args(argv)
+    store = MemoryStore.from_json(args.data) if args.data else MemoryStore()
+    srv = serve(App(store, device=args.device, seed=args.seed, max_seconds=args.max_seconds),
+                args.host, args.port)
+    print(f"vrpms_amd service on http://{args.host}:{args.port}/api", flush=True)
+    try:
+        srv.serve_forever()
+    except KeyboardInterrupt:
+        pass
+    srv.server_close()
+
+
+if __name__ == "__main__":
+    main()
