@@ -117,9 +117,13 @@ int vrpms_eval_path(vrpms_ctx* ctx, int32_t perm_bytes, int64_t ld, const void* 
  *   vrpms_eval; 1 = the first-generation eval_cvrp_words / eval_cvrp_packed,
  *   A/B only). */
 #define VRPMS_OPT_WORDS_KERNEL 3
-/*   VRPMS_OPT_WORDS_ILP: candidates per lane in eval_cvrp_words2 (0 = auto
- *   = 2, 1 or 2 force). */
+/*   VRPMS_OPT_WORDS_ILP: candidates per lane in eval_cvrp_words2 (0 = auto:
+ *   1 when two copies of the packed matrix fit the LDS, else 2; 1 or 2
+ *   force). */
 #define VRPMS_OPT_WORDS_ILP 4
+/*   VRPMS_OPT_WORDS_LOOKAHEAD: words ahead whose gathers eval_cvrp_words2
+ *   keeps in flight (0 = auto, 1 or 2 force; A/B). */
+#define VRPMS_OPT_WORDS_LOOKAHEAD 5
 int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value);
 
 /* Decode ONE giant tour into the result dict of api/vrp/ga/index.py:49-53

@@ -113,6 +113,7 @@ def words_gen(ctx):
     yield ctx
     ctx.set_words_kernel(0)
     ctx.set_words_ilp(0)
+    ctx.set_words_lookahead(0)
 
 
 # eval_cvrp_rows2 (row-major tiles staged through LDS) against the first
@@ -132,10 +133,11 @@ def test_rows2_matches_packed_and_oracle(words_gen, coracle, n, K, ld, C):
     np.testing.assert_array_equal(got[0], got[1])
 
 
-@pytest.mark.parametrize("ilp", [1, 2])
-def test_words2_ilp_variants(words_gen, coracle, ilp):
+@pytest.mark.parametrize("ilp,la", [(1, 1), (2, 1), (1, 2), (2, 2)])
+def test_words2_ilp_variants(words_gen, coracle, ilp, la):
     ctx = words_gen
     ctx.set_words_ilp(ilp)
+    ctx.set_words_lookahead(la)
     inst = synth.cvrp(100, 8, seed=11)
     check_words(ctx, coracle, inst, synth.random_perms(4097, inst.n, seed=ilp), inst.n)
 

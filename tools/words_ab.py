@@ -43,9 +43,12 @@ def main():
         words = ctx.to_words(perms, inst.n)
         out = {}
         keys = {}
-        for name, gen, ilp in (("words_gen1", 1, 0), ("words2_i1", 0, 1), ("words2_i2", 0, 2)):
+        for name, gen, ilp, la in (("words_gen1", 1, 0, 0), ("words2_i1", 0, 1, 1),
+                                   ("words2_i2", 0, 2, 1), ("words2_i1_la2", 0, 1, 2),
+                                   ("words2_i2_la2", 0, 2, 2)):
             ctx.set_words_kernel(gen)
             ctx.set_words_ilp(ilp)
+            ctx.set_words_lookahead(la)
             k = torch.empty(C, dtype=torch.int64, device=ctx.dev)
             t = timed(lambda: ctx.eval_words(words, inst.n, out=k))
             out[name] = {"ms": t * 1e3, "evals_per_s": C / t}
@@ -58,6 +61,7 @@ def main():
             keys[name] = k
         ctx.set_words_kernel(0)
         ctx.set_words_ilp(0)
+        ctx.set_words_lookahead(0)
         S = 1 << 16
         ref = coracle.eval_batch(inst.durations, perms[:S].cpu().numpy(), inst.demand,
                                  inst.capacities, inst.start_times)[0]

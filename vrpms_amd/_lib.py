@@ -28,6 +28,7 @@ OPT_SPLIT_MODE = 1
 OPT_STAGED_M = 2
 OPT_WORDS_KERNEL = 3
 OPT_WORDS_ILP = 4
+OPT_WORDS_LOOKAHEAD = 5
 OBJ_SUM = 0
 OBJ_MAX = 1
 

@@ -171,8 +171,12 @@ class Context:
         check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_WORDS_KERNEL, int(gen)))
 
     def set_words_ilp(self, ilp: int):
-        """Candidates per lane in eval_cvrp_words2: 0 = auto (2), 1 or 2 force."""
+        """Candidates per lane in eval_cvrp_words2: 0 = auto, 1 or 2 force."""
         check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_WORDS_ILP, int(ilp)))
+
+    def set_words_lookahead(self, la: int):
+        """Words of gathers eval_cvrp_words2 keeps in flight: 0 = auto, 1 or 2."""
+        check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_WORDS_LOOKAHEAD, int(la)))
 
     def set_staged_m(self, m: int):
         """Candidates per lane in eval_staged: 0 = auto, 1 or 2 force."""

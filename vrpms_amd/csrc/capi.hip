@@ -226,6 +226,12 @@ int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value) {
     ctx->opt_words_kernel = value;
     return VRPMS_OK;
   }
+  if (option == VRPMS_OPT_WORDS_LOOKAHEAD) {
+    if (value < 0 || value > 2)
+      return fail(VRPMS_EINVAL, "vrpms_set_option: words lookahead must be 0 (auto), 1 or 2");
+    ctx->opt_words_lookahead = value;
+    return VRPMS_OK;
+  }
   if (option == VRPMS_OPT_WORDS_ILP) {
     if (value < 0 || value > 2)
       return fail(VRPMS_EINVAL, "vrpms_set_option: words ILP must be 0 (auto), 1 or 2");
