@@ -103,12 +103,13 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096):
     from vrpms_amd import islands, runners
     n = inst.n
     dev = ctx.dev
-    probe = runners.SARunner(ctx, n, chains=chains, total_steps=1000, durations=inst.durations)
+    probe = runners.SARunner(ctx, n, chains=chains, total_steps=100000, durations=inst.durations)
+    probe.epoch(20)                      # first launch: code object load, LDS setup
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    probe.epoch(100)
+    probe.epoch(400)
     torch.cuda.synchronize(dev)
-    rate = 100 / (time.perf_counter() - t0)
+    rate = 400 / (time.perf_counter() - t0)
     del probe
     total = max(1000, int(rate * seconds * 0.95))
     per_epoch = max(50, total // 40)

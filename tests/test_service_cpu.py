@@ -197,3 +197,40 @@ def test_router_over_http():
     finally:
         srv.shutdown()
         srv.server_close()
+
+
+def test_tsp_batcher_coalesces_and_groups_by_node_count():
+    """Throughput mode: concurrent /api/tsp/sa requests share launches
+    (grouped by node count); each gets its own tour back.  The launch is
+    injected (the identity tour); the GPU one is in test_service_gpu.py."""
+    calls = []
+
+    def fake_launch(N, cis):
+        calls.append((N, len(cis)))
+        return [list(range(1, N)) for _ in cis]
+
+    st = service.MemoryStore({1: [{"id": i} for i in range(6)]},
+                             {2: [[abs(i - j) * 3 for j in range(6)] for i in range(6)]})
+    app = service.App(st, solve=zero_solve, batch_tsp=True, batch_window_s=0.05,
+                      batch_launch=fake_launch)
+    bodies = [{**FULL["tsp"], "customers": [1, 2, 3]}] * 6 + \
+             [{**FULL["tsp"], "customers": [1, 2, 3, 4, 5]}] * 4
+    out = [None] * len(bodies)
+
+    def go(i):
+        out[i] = app.post("tsp", "sa", json.dumps(bodies[i]).encode())
+
+    ths = [threading.Thread(target=go, args=(i,)) for i in range(len(bodies))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert sorted(calls) == [(4, 6), (6, 4)] and app.batcher.launches == 2
+    for (status, body), b in zip(out, bodies):
+        assert status == 200
+        k = len(b["customers"])
+        assert body["message"]["vehicle"] == [0] + list(range(1, k + 1)) + [0]
+        assert body["message"]["duration"] == 3 * k + 3 * k     # out and back along a line
+    # other algorithms never ride the batcher
+    status, body = app.post("tsp", "ga", json.dumps(bodies[0]).encode())
+    assert status == 200 and app.batcher.launches == 2

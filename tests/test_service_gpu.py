@@ -48,3 +48,26 @@ def test_vrp_endpoints_solve(algo):
     (row,) = st.solutions
     assert row["locations"] == [{"id": 0}, {"id": 1}, {"id": 3}]
     assert row["vehicles"] == msg["vehicles"] and row["durationSum"] == 21
+
+
+def test_tsp_batcher_on_gpu():
+    """Concurrent /api/tsp/sa requests ride shared tsp_batch_sa launches and
+    each gets an optimal tour of the 4-node instance."""
+    import threading
+    app = service.App(store(), batch_tsp=True, batch_window_s=0.05, batch_steps=200)
+    body = json.dumps(FULL["tsp"]).encode()
+    out = [None] * 24
+
+    def go(i):
+        out[i] = app.post("tsp", "sa", body)
+
+    ths = [threading.Thread(target=go, args=(i,)) for i in range(len(out))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert 1 <= app.batcher.launches < len(out)
+    for status, resp in out:
+        assert status == 200
+        msg = resp["message"]
+        assert msg["duration"] == 24 and sorted(msg["vehicle"][1:-1]) == [1, 2, 3]

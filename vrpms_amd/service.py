@@ -26,6 +26,7 @@ from __future__ import annotations
 import argparse
 import json
 import threading
+import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
 TITLES = {"bf": "Brute Force", "ga": "Genetic Algorithm", "sa": "Simulated Annealing",
@@ -152,6 +153,88 @@ class _Session:
 
 
 # ---------------------------------------------------------------------------
+# throughput mode: concurrent small TSP requests share one launch
+# ---------------------------------------------------------------------------
+class TspBatcher:
+    """Coalesces concurrent /api/tsp/sa requests on static matrices into one
+    `tsp_batch_sa` launch per node count (one workgroup per request, config
+    5 of BASELINE.json).  A request waits at most `window_s` for company.
+    Requests in one launch share its seed and temperature schedule (scaled
+    to the batch's mean edge), so a batched answer depends on the batch it
+    rode in; the unbatched path is deterministic per request."""
+
+    MIN_N, MAX_N = 4, 190        # compact nodes; N*N int32 must fit the LDS
+
+    def __init__(self, app, window_s: float = 0.005, steps: int = 2000, max_batch: int = 16384,
+                 launch=None):
+        self.app = app
+        self.window_s = window_s
+        self.steps = steps
+        self.max_batch = max_batch
+        self.launches = 0
+        self._launch = launch or self._gpu_launch
+        self._q = []
+        self._cv = threading.Condition()
+        threading.Thread(target=self._loop, daemon=True, name="tsp-batcher").start()
+
+    @classmethod
+    def accepts(cls, ci) -> bool:
+        return ci.durations.shape[0] == 1 and cls.MIN_N <= ci.N <= cls.MAX_N
+
+    def solve(self, ci) -> dict:
+        """Blocks until the request's launch finished -> the TSP slot dict."""
+        job = {"ci": ci, "done": threading.Event()}
+        with self._cv:
+            self._q.append(job)
+            self._cv.notify()
+        job["done"].wait()
+        if "error" in job:
+            raise job["error"]
+        D = ci.durations[0]
+        path = [0] + list(job["tour"]) + [0]
+        duration = int(sum(int(D[a][b]) for a, b in zip(path, path[1:])))
+        return {"duration": duration, "vehicle": [ci.nodes[c] for c in path]}
+
+    def _loop(self):
+        while True:
+            with self._cv:
+                while not self._q:
+                    self._cv.wait()
+            time.sleep(self.window_s)          # let concurrent requests join
+            with self._cv:
+                batch, self._q = self._q[:self.max_batch], self._q[self.max_batch:]
+            groups = {}
+            for job in batch:
+                groups.setdefault(job["ci"].N, []).append(job)
+            for N, jobs in groups.items():
+                try:
+                    tours = self._launch(N, [j["ci"] for j in jobs])
+                    self.launches += 1
+                    for j, t in zip(jobs, tours):
+                        j["tour"] = t
+                except Exception as e:         # every waiter of the group sees it
+                    for j in jobs:
+                        j["error"] = e
+                for j in jobs:
+                    j["done"].set()
+
+    def _gpu_launch(self, N, cis):
+        import numpy as np
+        import torch
+        from . import runners, solver
+        ctx = solver.context(self.app.device)
+        mats = torch.tensor(np.stack([ci.durations[0] for ci in cis]), dtype=torch.int32,
+                            device=ctx.dev)
+        edge = float(np.mean([runners.typical_edge(ci.durations[0]) for ci in cis]))
+        inv_t0 = 1.0 / (0.5 * edge)
+        inv_alpha = (0.5 / 0.002) ** (1.0 / max(1, self.steps))
+        with self.app.gpu_lock:
+            tours, _ = ctx.tsp_batch_sa(mats, self.steps, inv_t0, inv_alpha, self.app.seed)
+            torch.cuda.synchronize(ctx.dev)
+        return [[int(x) for x in row] for row in tours.cpu().tolist()]
+
+
+# ---------------------------------------------------------------------------
 # the endpoint logic
 # ---------------------------------------------------------------------------
 class App:
@@ -159,13 +242,25 @@ class App:
     `solve` is injectable (tests); by default it is the GPU solver."""
 
     def __init__(self, store, device: int = 0, seed: int = 0, max_seconds: float | None = None,
-                 solve=None):
+                 solve=None, batch_tsp: bool = False, batch_window_s: float = 0.005,
+                 batch_steps: int = 2000, batch_launch=None):
         self.store = store
         self.device = device
         self.seed = seed
         self.max_seconds = max_seconds
         self.gpu_lock = threading.Lock()
         self._solve = solve or self._gpu_solve
+        self.batcher = TspBatcher(self, batch_window_s, batch_steps, launch=batch_launch) \
+            if batch_tsp else None
+
+    def _batched_tsp(self, params, durations):
+        """The compact instance when this request rides the batcher, else None."""
+        if self.batcher is None:
+            return None
+        from . import solver
+        ci = solver.compact_tsp(durations, params["customers"], params["start_node"],
+                                params["start_time"] or 0)
+        return ci if TspBatcher.accepts(ci) else None
 
     def _gpu_solve(self, problem, algorithm, params, knobs, locations, durations):
         from . import solver
@@ -205,8 +300,13 @@ class App:
         if errors:
             return 400, {"success": False, "errors": errors}
         try:
-            with self.gpu_lock:
-                result = self._solve(problem, algorithm, params, knobs, locations, durations)
+            ci = self._batched_tsp(params, durations) if (problem, algorithm) == ("tsp", "sa") \
+                else None
+            if ci is not None:
+                result = self.batcher.solve(ci)
+            else:
+                with self.gpu_lock:
+                    result = self._solve(problem, algorithm, params, knobs, locations, durations)
         except Exception as e:   # bad instance shape, GPU unavailable, ...
             return 400, {"success": False,
                          "errors": [{"what": "Solver error", "reason": str(e)}]}
@@ -312,10 +412,16 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--max-seconds", type=float, default=None,
                     help="wall-time cap per solve (default: the algorithm's own budget)")
+    ap.add_argument("--batch-tsp", action="store_true",
+                    help="coalesce concurrent /api/tsp/sa requests into one launch")
+    ap.add_argument("--batch-window-ms", type=float, default=5.0)
+    ap.add_argument("--batch-steps", type=int, default=2000)
     args = ap.parse_args(argv)
     store = MemoryStore.from_json(args.data) if args.data else MemoryStore()
-    srv = serve(App(store, device=args.device, seed=args.seed, max_seconds=args.max_seconds),
-                args.host, args.port)
+    app = App(store, device=args.device, seed=args.seed, max_seconds=args.max_seconds,
+              batch_tsp=args.batch_tsp, batch_window_s=args.batch_window_ms * 1e-3,
+              batch_steps=args.batch_steps)
+    srv = serve(app, args.host, args.port)
     print(f"vrpms_amd service on http://{args.host}:{args.port}/api", flush=True)
     try:
         srv.serve_forever()
