@@ -26,11 +26,13 @@ run() {  # name, seconds, cmd...
 
 for step in "$@"; do
   case $step in
-    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     benchq) run bench_quick 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
     probe) run sa_probe 300 python tools/sa_probe.py ;;
+    quality) run quality_sweep 1100 python -u tools/quality_sweep.py ;;
+    quality_short) run quality_sweep 400 python -u tools/quality_sweep.py --T 1 10 ;;
     prof)
       cd /tmp
       run rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv \
@@ -45,6 +47,16 @@ for step in "$@"; do
           --output-format csv -d "$OUT/pmc_b" -o run -- $B
       run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- $B
       run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- $B
+      cd "$ROOT" ;;
+    lprobe) run lds_valu_probe 120 ./tools/lds_valu_probe ;;
+    pmc_l2)
+      cd /tmp
+      S="python3 $ROOT/tools/staged_run.py 3"
+      run pmc_l2_hit 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc_l2_hit" -o run -- $S
+      run pmc_l2_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_l2_fetch" -o run -- $S
+      run pmc_l2_sq 300 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
+          --output-format csv -d "$OUT/pmc_l2_sq" -o run -- $S
+      run pmc_l2_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/pmc_l2_stats" -o run -- $S
       cd "$ROOT" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Best-cost gap at equal wall time, swept over T and instance seeds
+(T in {1, 10, 60} s, median over seeds 0..4).
+
+Each (seed, T) cell runs bench.quality(): the GPU SA leg (4096 chains, elite
+migration) and the C/OpenMP SA leg on the host cores, each for T seconds of
+wall time with the cooling schedule spread over that time.  Writes
+gpurun_out/quality_sweep.json and prints one line per cell as it finishes.
+
+usage: python tools/quality_sweep.py [--T 1 10 60] [--seeds 0 1 2 3 4]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--T", type=float, nargs="+", default=[1.0, 10.0, 60.0])
+    ap.add_argument("--seeds", type=int, nargs="+", default=[0, 1, 2, 3, 4])
+    ap.add_argument("--chains", type=int, default=4096)
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "quality_sweep.json"))
+    args = ap.parse_args()
+
+    import torch
+    import bench
+    from vrpms_amd import synth
+    from vrpms_amd.core import CVRP, Context
+
+    torch.cuda.set_device(0)
+    ctx = Context(0)
+    cells = []
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    t_start = time.time()
+    for seed in args.seeds:
+        inst = synth.cvrp(100, 8, seed=seed)
+        ctx.set_instance(CVRP, inst.durations, inst.demand, inst.capacities, inst.start_times)
+        for T in args.T:
+            q = bench.quality(ctx, inst, T, 1, 0, None, with_cpu=True, chains=args.chains,
+                              label=f"cvrp100_k8 seed {seed}")
+            q["seed"] = seed
+            cells.append(q)
+            print(json.dumps({"seed": seed, "T_s": T, "gpu": q["gpu"]["duration_sum"],
+                              "cpu": q["cpu"]["duration_sum"], "gap": q["gap"],
+                              "gpu_wall": round(q["gpu"]["wall_s"], 3),
+                              "cpu_wall": round(q["cpu"]["wall_s"], 3),
+                              "elapsed": round(time.time() - t_start, 1)}), flush=True)
+            summary = {}
+            for t in args.T:
+                gaps = [c["gap"] for c in cells if c["T_s"] == t and c["gap"] is not None]
+                if gaps:
+                    summary[str(t)] = {"median_gap": statistics.median(gaps), "n": len(gaps),
+                                       "min_gap": min(gaps), "max_gap": max(gaps),
+                                       "gpu_better": sum(g < 0 for g in gaps)}
+            with open(args.out, "w") as f:
+                json.dump({"metric": "best-cost gap at equal wall time, (gpu - cpu) / cpu "
+                                     "on durationSum, negative = GPU better",
+                           "workload": "CVRP-100, K=8 (synth.cvrp), SA on both sides",
+                           "cpu_cores": cells[0]["cpu"]["cores"],
+                           "summary": summary, "cells": cells}, f, indent=1)
+    print(json.dumps({"summary": summary}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
