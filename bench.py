@@ -50,6 +50,8 @@ def parse():
                     help="target CPU work for the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-other-configs", action="store_true")
+    ap.add_argument("--island-epochs", type=int, default=20,
+                    help="cfg 4 island-SA leg (all ranks, RCCL elite all-gather); 0 disables")
     ap.add_argument("--quality-seconds", type=float, default=5.0,
                     help="wall time per side for the best-cost gap (0 disables)")
     return ap.parse_args()
@@ -275,6 +277,64 @@ def other_configs(ctx, torch, dev, seed=0):
     return out
 
 
+def island_leg(ctx, torch, dev, world, rank, dist, epochs=20, steps=25, chains=1024, E=8,
+               every=5, seed=0):
+    """BASELINE.json cfg 4 as a search, not a scoring pass: X-style CVRP-1000
+    (u16 matrix L2-resident), `chains` SA chains per GPU, a fixed number of
+    epochs with an elite exchange every `every` epochs -- an RCCL all-gather
+    of every rank's E best (tour + key) over xGMI when N > 1, local
+    re-injection at N = 1.  Every rank runs the same control flow
+    (islands.run_fixed), and a pre-flight all-reduce makes all ranks skip
+    together if any rank failed to set up.  Reports whole-job full-tour
+    evals/s inside the search (every sampled move is a full re-evaluation of
+    the moved tour: 64 per chain-step), the mean exchange time and the
+    global best."""
+    from vrpms_amd import islands, runners, synth
+    from vrpms_amd.core import CVRP
+    ok, err, r = 1, None, None
+    try:
+        x = synth.x_style(1000, seed=seed)
+        ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
+        r = runners.SARunner(ctx, x.n, chains=chains, seed=500 + rank,
+                             total_steps=epochs * steps, steps_per_epoch=steps,
+                             durations=x.durations)
+        r.epoch(2)                          # code object load, instance staging
+        torch.cuda.synchronize(dev)
+    except Exception:
+        ok, err = 0, traceback.format_exc(limit=3)
+    if world > 1:
+        f = torch.tensor([ok], dtype=torch.int32, device=dev)
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        ok = int(f.item())
+    if not ok:
+        return {"error": err or "another rank failed to set up"}
+    # untimed warm epoch + exchange: sort/gather kernels load, communicators form
+    islands.run_fixed(r, 1, 1, E)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    n_ex, t_ex = islands.run_fixed(r, epochs, every, E,
+                                   sync=lambda: torch.cuda.synchronize(dev))
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    key, tour = r.best()
+    if world > 1:
+        t = torch.tensor([wall, t_ex], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall, t_ex = float(t[0]), float(t[1])
+        key, _ = islands.global_best(key, tour.cpu().tolist(), x.n, device=dev)
+    evals = world * chains * epochs * steps * 64
+    return {"workload": "cfg4 X-style CVRP-1000, island SA", "vehicles": x.K,
+            "chains_per_gpu": chains, "epochs": epochs, "steps_per_epoch": steps,
+            "moves_per_step": 64, "exchange_every": every, "elites": E,
+            "exchange": "RCCL all_gather over xGMI" if world > 1 else "local re-injection",
+            "wall_s": wall, "evals_per_s": evals / wall,
+            "gathers_per_eval": x.n + x.K,
+            "exchanges": n_ex, "exchange_ms_mean": t_ex / max(n_ex, 1) * 1e3,
+            "best": {"unvisited": key >> 56, "duration_sum": (key >> 28) & (2**28 - 1)}}
+
+
 def pmc_traffic(kernel, grid):
     """HBM bytes per launch from the committed PMC pass of this same command
     (profiles/pmc_traffic.json, written by tools/summarize_profiles.py from
@@ -360,6 +420,11 @@ def main():
         except Exception:
             qual = {"error": traceback.format_exc(limit=3)}
 
+    isl = None
+    if args.island_epochs > 0:
+        # after every other device use of the matrix instance: it loads its own
+        isl = island_leg(ctx, torch, dev, world, rank, dist, epochs=args.island_epochs)
+
     if rank == 0:
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         nbytes = 4 * ((n + 3) // 4)
@@ -407,6 +472,8 @@ def main():
         out["rows_vs_words_identical"] = same
         if qual is not None:
             out["quality"] = qual
+        if isl is not None:
+            out["islands"] = isl
         if world == 1 and not args.no_cpu_baseline:
             cb, ref, S = cpu_baseline(inst, perms, args.cpu_seconds)
             got = keys[:S].cpu().numpy().view(np.uint64)

@@ -97,3 +97,57 @@ def test_select_global_orders_as_uint64():
     t, k = islands.select_global(tours, keys, 3)
     assert k.tolist() == [3, 3, 5]
     assert t[:, 0].tolist() == [4, 6, 0]
+
+
+class CountingRunner(FakeRunner):
+    """Epochs lower one member's key, so migrations carry changing elites."""
+
+    def __init__(self, rank):
+        super().__init__(rank)
+        self.epochs = 0
+        self.log = []
+
+    def epoch(self):
+        self.epochs += 1
+        self.keys[self.epochs % self.keys.shape[0]] -= 1
+
+    def inject(self, tours, keys):
+        super().inject(tours, keys)
+        self.log.append(keys.tolist())
+
+
+def _fixed_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        r = CountingRunner(rank)
+        n_ex, t_ex = islands.run_fixed(r, epochs=12, exchange_every=4, E=2)
+        q.put((rank, {"n_ex": n_ex, "epochs": r.epochs, "log": r.log, "t_ex": t_ex}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_run_fixed_world2_same_collectives_and_merges():
+    """The bench's island leg (cfg 4) at N > 1: a fixed epoch count, so every
+    rank enters the same number of all-gathers and injects identical elites."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fixed_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert out[0]["n_ex"] == out[1]["n_ex"] == 3
+    assert out[0]["epochs"] == out[1]["epochs"] == 12
+    assert out[0]["log"] == out[1]["log"] and len(out[0]["log"]) == 3
+    assert all(k == sorted(k) for k in out[0]["log"])
+
+
+def test_run_fixed_single_rank_injects_locally():
+    r = CountingRunner(0)
+    n_ex, _ = islands.run_fixed(r, epochs=10, exchange_every=5, E=2)
+    assert n_ex == 2 and len(r.log) == 2 and r.epochs == 10

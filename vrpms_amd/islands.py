@@ -66,6 +66,35 @@ def run_islands(runner, epochs: int, exchange_every: int = 5, E: int = 8, group=
     return runner.best()
 
 
+def run_fixed(runner, epochs: int, exchange_every: int = 5, E: int = 8, group=None, sync=None):
+    """`epochs` island epochs with a migration every `exchange_every` epochs,
+    on a FIXED count: every rank runs the identical control flow (no
+    wall-clock exit), so every rank enters every collective.  With one rank
+    the migration is local (the E best re-injected into the worst chains).
+    `sync` (e.g. torch.cuda.synchronize) brackets each exchange so its time
+    is measured apart.  Returns (exchanges, exchange_seconds)."""
+    import time
+
+    import torch.distributed as dist
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    n_ex, t_ex = 0, 0.0
+    for e in range(1, epochs + 1):
+        runner.epoch()
+        if e % exchange_every == 0:
+            if sync:
+                sync()
+            t0 = time.perf_counter()
+            if multi:
+                exchange(runner, E, group)
+            else:
+                runner.inject(*runner.elites(E))
+            if sync:
+                sync()
+            t_ex += time.perf_counter() - t0
+            n_ex += 1
+    return n_ex, t_ex
+
+
 def global_best(key: int, tour, n: int, group=None, device=None):
     """Reduce the per-rank best (key, tour) to the global best on every rank."""
     import torch.distributed as dist
