@@ -449,8 +449,10 @@ def main():
                        "parallelism": f"islands{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         # launch_words2's auto grid: two tours per lane, one
+                         # 1024-lane workgroup per CU
                          "traffic": pmc_traffic("eval_cvrp_words2",
-                                                min((C + 1023) // 1024, 2 * cus) * 1024),
+                                                min((C + 2047) // 2048, cus) * 1024),
                          "traffic_unit": "bytes/launch (PMC, profiles/pmc_traffic.json)",
                          "kernel": "eval_cvrp_words2", "kernel_ms": kernel_ms,
                          "bytes_per_launch": bytes_per_launch,

@@ -161,7 +161,8 @@ def test_words_layout_cvrp100(ctx, coracle, C):
     check_words(ctx, coracle, inst, synth.random_perms(C, inst.n, seed=C), inst.n)
 
 
-@pytest.mark.parametrize("n,K,slack", [(29, 1, 0.5), (37, 4, 0.9), (5, 2, 1.0), (64, 8, 0.8)])
+@pytest.mark.parametrize("n,K,slack", [(29, 1, 0.5), (37, 4, 0.9), (5, 2, 1.0), (64, 8, 0.8),
+                                       (100, 8, 1.03), (100, 8, 1.05), (101, 8, 1.0)])
 def test_words_layout_ragged_and_tight(ctx, coracle, n, K, slack, split_mode):
     inst = synth.cvrp(n, K, seed=n, slack=slack)
     P = synth.random_perms(20000, inst.n, seed=1)
@@ -284,3 +285,27 @@ def test_errors_are_raised(ctx):
         ctx.set_instance(CVRP, D, [0, 1, 1, 1, 1], [3], [0])
     with pytest.raises(VrpmsError, match="A9"):
         ctx.set_instance(CVRP, np.full((5, 5), 2**29), [0, 1, 1, 1, 1], [3], [0])
+
+
+# The headline kernels walk the split without the fleet-exhaustion test and
+# re-walk exactly the lanes whose vehicle counter met the fleet limit
+# (eval_words.hip split_step_fast / redo_exact): waves where some lanes
+# exhaust and others do not, on every ILP / look-ahead variant and on the
+# row-major kernel, against the oracle.
+@pytest.mark.parametrize("ilp,la", [(1, 1), (2, 1), (1, 2), (2, 2)])
+@pytest.mark.parametrize("slack", [1.03, 0.9])
+def test_words2_mixed_exhaustion(words_gen, coracle, ilp, la, slack):
+    ctx = words_gen
+    ctx.set_words_ilp(ilp)
+    ctx.set_words_lookahead(la)
+    inst = synth.cvrp(100, 8, seed=12, slack=slack)
+    check_words(ctx, coracle, inst, synth.random_perms(8191, inst.n, seed=ilp + 2 * la), inst.n,
+                objective=ilp - 1)
+
+
+@pytest.mark.parametrize("n,ld,slack", [(100, 100, 1.03), (97, 100, 0.95), (30, 32, 0.7)])
+def test_rows2_mixed_exhaustion(words_gen, coracle, n, ld, slack):
+    ctx = words_gen
+    inst = synth.cvrp(n, 8 if n > 50 else 3, seed=n + 1, slack=slack)
+    P = synth.random_perms(6001, inst.n, seed=3, ld=ld)
+    check_batch(ctx, coracle, inst, P, n=inst.n, expect_path=0)

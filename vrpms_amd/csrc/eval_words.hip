@@ -61,6 +61,25 @@ VRPMS_DEV void split_step(SplitAcc& s, uint64_t e, uint32_t vsmask, uint32_t kin
   s.acc = fits ? t : (exhausted ? deadacc : hi);
 }
 
+// The same step without the fleet-exhaustion test: a customer that does not
+// fit always opens a new route, and dsum's vehicle counter keeps counting.
+// Identical to split_step until the K-th route closes, which sets dsum's
+// sign bit (the counter starts at 2^B - K) -- and that bit stays set, since
+// the counter only grows and 2^B > n keeps it below 2^32.  So a chain whose
+// dsum is non-negative at the end never met the exhaustion branch and its
+// result is exact; the rare chain that did is re-walked with split_step
+// (redo_exact).  Random CVRP-100 giant tours never exhaust the bench's
+// fleet (0 of 200k), and this drops a compare + select per customer.
+VRPMS_DEV void split_step_fast(SplitAcc& s, uint64_t e, uint32_t vsmask, uint32_t kinc) {
+  const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
+  const uint32_t t = s.acc + lo;
+  const bool fits = (int32_t)t < 0;
+  const uint32_t rdm = fits ? 0u : ((s.acc & vsmask) | kinc);
+  s.dsum += rdm;
+  s.dmax = max(s.dmax, rdm);
+  s.acc = fits ? t : hi;
+}
+
 // Copy the packed matrix E into LDS (16-byte vectors + an 8-byte tail).
 VRPMS_DEV void stage_table(const uint64_t* pack, int N, unsigned char* smem) {
   const uint32_t ebytes = (uint32_t)N * N * 8;
@@ -116,7 +135,26 @@ struct WordChains {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int i = 0; i < ILP; ++i) split_step(sa[i], g[i][q], vsmask, kinc, deadacc);
+      for (int i = 0; i < ILP; ++i) split_step_fast(sa[i], g[i][q], vsmask, kinc);
+  }
+  // The exact split of one tour, word by word (word(w) returns tour word w):
+  // the slow path for a chain whose fast walk met the fleet limit.
+  template <class WordAt>
+  VRPMS_DEV SplitAcc redo_exact(const FastSplit& f, int n, WordAt word) const {
+    SplitAcc s;
+    s.init(f);
+    uint32_t prev = 0;  // byte 3 = the depot before the first customer
+    const int nw = (n + 3) >> 2;
+    for (int w = 0; w < nw; ++w) {
+      const uint32_t x = word(w);
+      const int rem = min(4, n - 4 * w);
+      if (rem > 0) split_step(s, gat(__builtin_amdgcn_perm(x, prev, kSel30)), vsmask, kinc, deadacc);
+      if (rem > 1) split_step(s, gat(__builtin_amdgcn_perm(x, x, kSel01)), vsmask, kinc, deadacc);
+      if (rem > 2) split_step(s, gat(__builtin_amdgcn_perm(x, x, kSel12)), vsmask, kinc, deadacc);
+      if (rem > 3) split_step(s, gat(__builtin_amdgcn_perm(x, x, kSel23)), vsmask, kinc, deadacc);
+      prev = x;
+    }
+    return s;
   }
   // next word's address math (perm + dot2) interleaved into this word's
   // split chain, each ds_read well after its dot2
@@ -257,9 +295,12 @@ __global__ __launch_bounds__(1024) void eval_cvrp_words2(WordsArgs a) {
       }
     }
 #pragma unroll
-    for (int i = 0; i < ILP; ++i)
-      if (live[i])
-        store_cost(a.f, ch.sa[i], n, c0 + threadIdx.x + 1024 * i, a.keys, a.sums, a.maxs, a.unv);
+    for (int i = 0; i < ILP; ++i) {
+      const int64_t c = c0 + threadIdx.x + 1024 * i;
+      if (live[i] && (int32_t)ch.sa[i].dsum < 0)  // met the fleet limit: exact re-walk
+        ch.sa[i] = ch.redo_exact(a.f, n, [&](int w) { return a.words[(int64_t)w * C + c]; });
+      if (live[i]) store_cost(a.f, ch.sa[i], n, c, a.keys, a.sums, a.maxs, a.unv);
+    }
   }
 }
 
@@ -381,6 +422,10 @@ __global__ __launch_bounds__(1024) void eval_cvrp_rows2(RowsArgs a) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int64_t c = t0 + wave * WR + l + 64 * i;
+      if (c < C && (int32_t)ch.sa[i].dsum < 0)  // met the fleet limit: exact re-walk
+        ch.sa[i] = ch.redo_exact(a.f, n, [&](int w) {
+          return *reinterpret_cast<const uint32_t*>(a.perms + c * (int64_t)a.ld + 4 * w);
+        });
       if (c < C) store_cost(a.f, ch.sa[i], n, c, a.keys, a.sums, a.maxs, a.unv);
     }
   }
@@ -389,13 +434,15 @@ __global__ __launch_bounds__(1024) void eval_cvrp_rows2(RowsArgs a) {
 int launch_words2(const vrpms_ctx* ctx, const WordsArgs& w, int R, hipStream_t s) {
   const Instance& in = ctx->inst;
   const size_t lds = ((size_t)in.N * in.N * 8 + 15) & ~(size_t)15;
-  // Auto: when two copies of the matrix fit the LDS (N <= 101), one chain
-  // per lane with two words of gathers in flight (<= 64 VGPRs: two 1024-lane
-  // workgroups per CU); otherwise two chains per lane, one word ahead (one
-  // workgroup per CU).  Measured on CVRP-100: 32.5 vs 31.6 G evals/s.
+  // Auto: two chains per lane (one 1024-lane workgroup per CU), two words of
+  // gathers in flight when the matrix is small enough for two workgroups'
+  // copies (N <= 101), else one.  Measured on CVRP-100 with the fast split
+  // (tools/words_ab.py): ILP2/LA2 36.7, ILP2/LA1 36.2-36.7, ILP1/LA2 35.1,
+  // ILP1/LA1 34.0-35.5 G evals/s.  (Before the fast split, at ~2.5 more
+  // VALU per customer, ILP1/LA2 with two workgroups per CU led: 32.5 vs 31.6.)
   const bool two_wg = 2 * lds <= ctx->max_lds;
-  const int ilp = ctx->opt_words_ilp ? ctx->opt_words_ilp : (two_wg ? 1 : 2);
-  const int la = ctx->opt_words_lookahead ? ctx->opt_words_lookahead : (ilp == 1 ? 2 : 1);
+  const int ilp = ctx->opt_words_ilp ? ctx->opt_words_ilp : 2;
+  const int la = ctx->opt_words_lookahead ? ctx->opt_words_lookahead : (two_wg ? 2 : 1);
   // ILP2 needs > 64 VGPRs: one 1024-lane workgroup per CU; ILP1 fits two
   const int per_cu = ilp == 2 ? 1 : (two_wg ? 2 : 1);
   const int64_t blocks = (w.C + 1024 * ilp - 1) / (1024 * ilp);
