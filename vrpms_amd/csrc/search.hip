@@ -276,10 +276,10 @@ VRPMS_DEV uint64_t eval_mapped(const FastSplit& f, const unsigned char* E, uint3
     const int q = 4 * b + 8;
     const uint32_t c0 = rd(q), c1 = rd(q + 1), c2 = rd(q + 2), c3 = rd(q + 3);
     const uint64_t f0 = gat(last, b0), f1 = gat(b0, b1), f2 = gat(b1, b2), f3 = gat(b2, b3);
-    sa.step(e0, smask, kinc, deadacc);
-    sa.step(e1, smask, kinc, deadacc);
-    sa.step(e2, smask, kinc, deadacc);
-    sa.step(e3, smask, kinc, deadacc);
+    sa.step_fast(e0, smask, kinc);
+    sa.step_fast(e1, smask, kinc);
+    sa.step_fast(e2, smask, kinc);
+    sa.step_fast(e3, smask, kinc);
     last = b3;
     b0 = c0;
     b1 = c1;
@@ -291,9 +291,18 @@ VRPMS_DEV uint64_t eval_mapped(const FastSplit& f, const unsigned char* E, uint3
     e3 = f3;
   }
   const int rem = n & 3;  // e0..e(rem-1): the ragged last block
-  if (rem > 0) sa.step(e0, smask, kinc, deadacc);
-  if (rem > 1) sa.step(e1, smask, kinc, deadacc);
-  if (rem > 2) sa.step(e2, smask, kinc, deadacc);
+  if (rem > 0) sa.step_fast(e0, smask, kinc);
+  if (rem > 1) sa.step_fast(e1, smask, kinc);
+  if (rem > 2) sa.step_fast(e2, smask, kinc);
+  if (sa.hit_fleet_limit()) {  // rare: exact re-walk with the exhaustion test
+    sa.init(f);
+    uint32_t prev = 0;
+    for (int q = 0; q < n; ++q) {
+      const uint32_t c = rd(q);
+      sa.step(gat(prev, c), smask, kinc, deadacc);
+      prev = c;
+    }
+  }
   return sa.finish(f, n).key;
 }
 

@@ -62,6 +62,24 @@ struct SplitAcc {
     acc = bsel(fm, t, bsel(am, deadacc, hi));
   }
 
+  // step() without the fleet-exhaustion test (a customer that does not fit
+  // always opens a new route).  Exact until the K-th route closes, which
+  // sets dsum's sign bit for good (the counter only grows, 2^B > n): a walk
+  // that ends with dsum >= 0 equals the step() walk; one that does not is
+  // re-walked with step() by the caller.
+  VRPMS_DEV void step_fast(uint64_t e, uint32_t smask, uint32_t kinc) {
+    auto bsel = [](uint32_t m, uint32_t x, uint32_t y) { return (x & m) | (y & ~m); };
+    auto sgn = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_sbfe((int)x, 31u, 1u); };
+    const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
+    const uint32_t t = acc + lo;
+    const uint32_t fm = sgn(t);
+    const uint32_t rdm = bsel(fm, 0u, (acc & smask) | kinc);
+    dsum += rdm;
+    dmax = max(dmax, rdm);
+    acc = bsel(fm, t, hi);
+  }
+  VRPMS_DEV bool hit_fleet_limit() const { return (int32_t)dsum < 0; }
+
   VRPMS_DEV TourCost finish(const FastSplit& f, int n) const {
     const uint32_t kinc = 1u << f.ks;
     const bool dead = (int32_t)dsum < 0;
