@@ -118,8 +118,7 @@ int vrpms_eval_path(vrpms_ctx* ctx, int32_t perm_bytes, int64_t ld, const void* 
  *   A/B only). */
 #define VRPMS_OPT_WORDS_KERNEL 3
 /*   VRPMS_OPT_WORDS_ILP: candidates per lane in eval_cvrp_words2 (0 = auto:
- *   1 when two copies of the packed matrix fit the LDS, else 2; 1 or 2
- *   force). */
+ *   2; 1, 2 or 3 force, A/B). */
 #define VRPMS_OPT_WORDS_ILP 4
 /*   VRPMS_OPT_WORDS_LOOKAHEAD: words ahead whose gathers eval_cvrp_words2
  *   keeps in flight (0 = auto, 1 or 2 force; A/B). */

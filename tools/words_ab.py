@@ -45,7 +45,7 @@ def main():
         keys = {}
         for name, gen, ilp, la in (("words_gen1", 1, 0, 0), ("words2_i1", 0, 1, 1),
                                    ("words2_i2", 0, 2, 1), ("words2_i1_la2", 0, 1, 2),
-                                   ("words2_i2_la2", 0, 2, 2)):
+                                   ("words2_i2_la2", 0, 2, 2), ("words2_i3", 0, 3, 1)):
             ctx.set_words_kernel(gen)
             ctx.set_words_ilp(ilp)
             ctx.set_words_lookahead(la)

@@ -233,8 +233,8 @@ int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value) {
     return VRPMS_OK;
   }
   if (option == VRPMS_OPT_WORDS_ILP) {
-    if (value < 0 || value > 2)
-      return fail(VRPMS_EINVAL, "vrpms_set_option: words ILP must be 0 (auto), 1 or 2");
+    if (value < 0 || value > 3)
+      return fail(VRPMS_EINVAL, "vrpms_set_option: words ILP must be 0 (auto), 1, 2 or 3");
     ctx->opt_words_ilp = value;
     return VRPMS_OK;
   }

@@ -443,8 +443,8 @@ int launch_words2(const vrpms_ctx* ctx, const WordsArgs& w, int R, hipStream_t s
   const bool two_wg = 2 * lds <= ctx->max_lds;
   const int ilp = ctx->opt_words_ilp ? ctx->opt_words_ilp : 2;
   const int la = ctx->opt_words_lookahead ? ctx->opt_words_lookahead : (two_wg ? 2 : 1);
-  // ILP2 needs > 64 VGPRs: one 1024-lane workgroup per CU; ILP1 fits two
-  const int per_cu = ilp == 2 ? 1 : (two_wg ? 2 : 1);
+  // ILP >= 2 needs > 64 VGPRs: one 1024-lane workgroup per CU; ILP1 fits two
+  const int per_cu = ilp >= 2 ? 1 : (two_wg ? 2 : 1);
   const int64_t blocks = (w.C + 1024 * ilp - 1) / (1024 * ilp);
   const int grid = (int)std::min<int64_t>(blocks, (int64_t)ctx->num_cus * per_cu);
   auto go = [&](auto kern) {
@@ -465,7 +465,9 @@ int launch_words2(const vrpms_ctx* ctx, const WordsArgs& w, int R, hipStream_t s
   using one = std::integral_constant<int, 1>;
   using two = std::integral_constant<int, 2>;
   const bool la2 = la == 2;
-  if (ilp == 2) la2 ? pick(two{}, two{}) : pick(two{}, one{});
+  using three = std::integral_constant<int, 3>;
+  if (ilp == 3) pick(three{}, one{});  // (ILP3 with two words ahead spills)
+  else if (ilp == 2) la2 ? pick(two{}, two{}) : pick(two{}, one{});
   else la2 ? pick(one{}, two{}) : pick(one{}, one{});
   VRPMS_HIP(hipGetLastError());
   return VRPMS_OK;
