@@ -127,10 +127,11 @@ def test_rows2_matches_packed_and_oracle(words_gen, coracle, n, K, ld, C):
     inst = synth.cvrp(n, K, seed=n)
     P = synth.random_perms(C, inst.n, seed=K, ld=ld)
     got = {}
-    for gen in (0, 1):
+    for gen in (0, 1, 2):    # rows2, eval_cvrp_packed, words2 reading the rows in place
         ctx.set_words_kernel(gen)
         got[gen] = check_batch(ctx, coracle, inst, P, n=inst.n, objective=n % 2, expect_path=0)
     np.testing.assert_array_equal(got[0], got[1])
+    np.testing.assert_array_equal(got[0], got[2])
 
 
 @pytest.mark.parametrize("ilp,la", [(1, 1), (2, 1), (1, 2), (2, 2)])
@@ -308,4 +309,6 @@ def test_rows2_mixed_exhaustion(words_gen, coracle, n, ld, slack):
     ctx = words_gen
     inst = synth.cvrp(n, 8 if n > 50 else 3, seed=n + 1, slack=slack)
     P = synth.random_perms(6001, inst.n, seed=3, ld=ld)
-    check_batch(ctx, coracle, inst, P, n=inst.n, expect_path=0)
+    for gen in (0, 2):
+        ctx.set_words_kernel(gen)
+        check_batch(ctx, coracle, inst, P, n=inst.n, expect_path=0)

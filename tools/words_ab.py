@@ -53,7 +53,7 @@ def main():
             t = timed(lambda: ctx.eval_words(words, inst.n, out=k))
             out[name] = {"ms": t * 1e3, "evals_per_s": C / t}
             keys[name] = k
-        for name, gen in (("rows_packed_gen1", 1), ("rows2", 0)):
+        for name, gen in (("rows_packed_gen1", 1), ("rows2", 0), ("rows_direct", 2)):
             ctx.set_words_kernel(gen)
             k = torch.empty(C, dtype=torch.int64, device=ctx.dev)
             t = timed(lambda: ctx.eval(perms, n=inst.n, out=k))

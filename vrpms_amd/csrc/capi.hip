@@ -221,8 +221,8 @@ int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value) {
     return VRPMS_OK;
   }
   if (option == VRPMS_OPT_WORDS_KERNEL) {
-    if (value < 0 || value > 1)
-      return fail(VRPMS_EINVAL, "vrpms_set_option: words kernel must be 0 (auto) or 1");
+    if (value < 0 || value > 2)
+      return fail(VRPMS_EINVAL, "vrpms_set_option: words kernel must be 0 (auto), 1 or 2");
     ctx->opt_words_kernel = value;
     return VRPMS_OK;
   }

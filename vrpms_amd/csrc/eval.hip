@@ -741,6 +741,12 @@ extern "C" int vrpms_eval(vrpms_ctx* ctx, const void* d_perms, int32_t perm_byte
   const int path = vrpms_eval_path(ctx, perm_bytes, ld, d_perms);
   if (path == 0) {
     FastSplit f;
+    if (ctx->opt_words_kernel == 2 && fast_split_params(ctx, n, &f)) {
+      // rows read in place by eval_cvrp_words2 (one dword per word per lane)
+      WordsArgs w{f, static_cast<const uint32_t*>(d_perms), C, n, d_keys, d_sum, d_max, d_unv,
+                  1, (uint32_t)(ld / 4)};
+      return launch_words2(ctx, w, words2_ring(n), s);
+    }
     if (ctx->opt_words_kernel != 1 && fast_split_params(ctx, n, &f) &&
         rows2_chunk_words(ctx, f) > 0) {
       RowsArgs r{f, static_cast<const unsigned char*>(d_perms), C, n, (int)ld,
@@ -805,18 +811,13 @@ extern "C" int vrpms_eval_words(vrpms_ctx* ctx, const uint32_t* d_words, int64_t
   hipStream_t s = (hipStream_t)stream;
   FastSplit f;
   if (fast_split_params(ctx, n, &f)) {
-    WordsArgs w{f, d_words, C, n, d_keys, d_sum, d_max, d_unv};
+    WordsArgs w{f, d_words, C, n, d_keys, d_sum, d_max, d_unv, C, 1u};
     const size_t lds = ((size_t)in.N * in.N * 8 + 15) & ~(size_t)15;
     const int per_cu = std::max<int>(1, std::min<int>(2, (int)(ctx->max_lds / lds)));
     const int64_t blocks = (C + 1023) / 1024;
     const int grid = (int)std::min<int64_t>(blocks, (int64_t)ctx->num_cus * per_cu);
     // ring depth: the R in [4, 8] that wastes the fewest slots on ceil(n/4) words
-    const int nw = (n + 3) / 4;
-    int R = 8, waste = 1 << 30;
-    for (int r = 8; r >= 4; --r) {
-      const int wst = (nw + r - 1) / r * r - nw;
-      if (wst < waste) { waste = wst; R = r; }
-    }
+    const int R = words2_ring(n);
     if (ctx->opt_words_kernel != 1) return launch_words2(ctx, w, R, s);
     auto go = [&](auto kern) {
       allow_lds(kern, lds);

@@ -214,13 +214,17 @@ __global__ __launch_bounds__(1024) void eval_cvrp_words2(WordsArgs a) {
       lane[i] = live[i] ? threadIdx.x + 1024u * i : threadIdx.x;
     }
     if (!live[0]) continue;
-    const uint32_t* row = a.words + c0;
+    const uint32_t* row = a.words + c0 * a.cstride;
+    const int64_t wstride = a.wstride;
+    uint32_t loff[ILP];
+#pragma unroll
+    for (int i = 0; i < ILP; ++i) loff[i] = lane[i] * a.cstride;
     uint32_t ring[ILP][R];
 #pragma unroll
     for (int u = 0; u < R; ++u) {
 #pragma unroll
-      for (int i = 0; i < ILP; ++i) ring[i][u] = u < nw ? row[lane[i]] : 0u;
-      row += C;
+      for (int i = 0; i < ILP; ++i) ring[i][u] = u < nw ? row[loff[i]] : 0u;
+      row += wstride;
     }
     ch.reset(a.f);
     // software pipeline: the gathers of word w + LA are issued before the
@@ -242,9 +246,9 @@ __global__ __launch_bounds__(1024) void eval_cvrp_words2(WordsArgs a) {
 #pragma unroll
       for (int i = 0; i < ILP; ++i) {
         wd[i] = ring[i][u];
-        if (refill) ring[i][u] = row[lane[i]];  // word w + R
+        if (refill) ring[i][u] = row[loff[i]];  // word w + R
       }
-      if (refill) row += C;
+      if (refill) row += wstride;
       uint64_t f[ILP][4];
       if (has_next) {
 #pragma unroll
@@ -281,10 +285,10 @@ __global__ __launch_bounds__(1024) void eval_cvrp_words2(WordsArgs a) {
     // ragged tail (n not a multiple of 4R): word by word, the last one partial
     for (int w = nblk * R; w < nw; ++w) {
       const int rem = min(4, n - 4 * w);  // uniform
-      const uint32_t* rw = a.words + c0 + (int64_t)w * C;
+      const uint32_t* rw = a.words + c0 * a.cstride + (int64_t)w * wstride;
       uint32_t x[ILP];
 #pragma unroll
-      for (int i = 0; i < ILP; ++i) x[i] = rw[lane[i]];
+      for (int i = 0; i < ILP; ++i) x[i] = rw[loff[i]];
       if (rem == 4) {
         ch.issue(e, x, ch.wprev);
         ch.steps(e);
@@ -298,7 +302,9 @@ __global__ __launch_bounds__(1024) void eval_cvrp_words2(WordsArgs a) {
     for (int i = 0; i < ILP; ++i) {
       const int64_t c = c0 + threadIdx.x + 1024 * i;
       if (live[i] && (int32_t)ch.sa[i].dsum < 0)  // met the fleet limit: exact re-walk
-        ch.sa[i] = ch.redo_exact(a.f, n, [&](int w) { return a.words[(int64_t)w * C + c]; });
+        ch.sa[i] = ch.redo_exact(a.f, n, [&](int w) {
+          return a.words[(int64_t)w * wstride + c * (int64_t)a.cstride];
+        });
       if (live[i]) store_cost(a.f, ch.sa[i], n, c, a.keys, a.sums, a.maxs, a.unv);
     }
   }
@@ -471,6 +477,16 @@ int launch_words2(const vrpms_ctx* ctx, const WordsArgs& w, int R, hipStream_t s
   else la2 ? pick(one{}, two{}) : pick(one{}, one{});
   VRPMS_HIP(hipGetLastError());
   return VRPMS_OK;
+}
+
+int words2_ring(int n) {
+  const int nw = (n + 3) / 4;
+  int R = 8, waste = 1 << 30;
+  for (int r = 8; r >= 4; --r) {
+    const int wst = (nw + r - 1) / r * r - nw;
+    if (wst < waste) { waste = wst; R = r; }
+  }
+  return R;
 }
 
 int rows2_chunk_words(const vrpms_ctx* ctx, const FastSplit& f) {
