@@ -49,6 +49,13 @@ for step in "$@"; do
       run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- $B
       cd "$ROOT" ;;
     lprobe) run lds_valu_probe 120 ./tools/lds_valu_probe ;;
+    pmc_search)
+      cd /tmp
+      S="python3 $ROOT/tools/search_run.py 3"
+      run pmc_s_sq 300 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
+          --output-format csv -d "$OUT/pmc_s_sq" -o run -- $S
+      run pmc_s_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/pmc_s_stats" -o run -- $S
+      cd "$ROOT" ;;
     pmc_l2)
       cd /tmp
       S="python3 $ROOT/tools/staged_run.py 3"
