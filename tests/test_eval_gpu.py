@@ -214,6 +214,15 @@ def test_tdvrp_small_lds_tier(ctx, coracle):
     check_batch(ctx, coracle, inst, P, expect_path=2)
 
 
+def test_max_uint8_instance(ctx, coracle):
+    """N = 256, the largest instance uint8 tours can name (255 customers):
+    row-major and word-interleaved layouts, ragged batch."""
+    inst = synth.cvrp(255, 20, seed=9)
+    P = synth.random_perms(3001, inst.n, seed=2)
+    check_batch(ctx, coracle, inst, P, expect_path=2)
+    check_words(ctx, coracle, inst, P, inst.n)
+
+
 def test_x1000_l2_tier(ctx, coracle):
     inst = synth.x_style(1000, seed=0)
     P = synth.random_perms(2048, inst.n, seed=1, dtype=np.uint16)
