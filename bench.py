@@ -87,10 +87,23 @@ def cpu_baseline(inst, perms_dev, seconds):
                                  inst.start_times, 1, 0, threads=threads)
         dt += time.perf_counter() - t0
         passes += 1
+    # the pure-Python restatement in the reference's own stdlib style (SURVEY
+    # §8d comparator (i)), one core, a small slice of the same tours
+    from oracle import spec
+    py_n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < min(2.0, seconds) and py_n < S:
+        spec.eval_cvrp(inst.durations, sample[py_n], inst.demand, inst.capacities,
+                       inst.start_times)
+        py_n += 1
+    py_dt = time.perf_counter() - t0
     return {"value": S * passes / dt, "unit": "evals/s", "cores": threads, "kind": "port",
             "sample": f"{passes} pass(es) over the first {S} of the same CVRP-100 tours, C "
                       f"restatement oracle/oracle_c.c (OpenMP, {threads} threads), "
-                      f"{dt:.2f} s"}, ref, S
+                      f"{dt:.2f} s",
+            "python_port": {"value": py_n / py_dt, "unit": "evals/s", "cores": 1,
+                            "sample": f"first {py_n} of the same tours through oracle/spec.py "
+                                      f"eval_cvrp (pure Python, the reference's language), "
+                                      f"{py_dt:.2f} s"}}, ref, S
 
 
 class _TimedCooling:
