@@ -35,6 +35,11 @@
 
 namespace vrpms {
 
+// VALU per ds_read slot in the interleaved schedule (A/B builds override)
+#ifndef VRPMS_IL_VALU
+#define VRPMS_IL_VALU 10
+#endif
+
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) const uint64_t lds_u64;
 typedef __attribute__((address_space(3))) unsigned char lds_uc;
@@ -159,11 +164,13 @@ struct WordChains {
   // next word's address math (perm + dot2) interleaved into this word's
   // split chain, each ds_read well after its dot2
   VRPMS_DEV static void interleave() {
+#if VRPMS_IL_VALU > 0
 #pragma unroll
     for (int q = 0; q < 4 * ILP; ++q) {
-      __builtin_amdgcn_sched_group_barrier(0x2, 10, 0);
+      __builtin_amdgcn_sched_group_barrier(0x2, VRPMS_IL_VALU, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
+#endif
   }
   // a partial last word of rem (1..3) customers
   VRPMS_DEV void partial(const uint32_t (&x)[ILP], int rem) {
