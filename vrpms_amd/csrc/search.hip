@@ -864,7 +864,7 @@ __global__ __launch_bounds__(256) void tsp_batch_sa_kernel(TspBatchArgs a) {
       A[j] = t;
     }
   wave_sync();
-  auto dist = [&](uint32_t x, uint32_t y) { return D[x * (uint32_t)N + y]; };
+  auto dist = [&](uint32_t x, uint32_t y) { return D[__umul24(x, (uint32_t)N) + y]; };
   auto full = [&](const uint16_t* T) {
     int s = 0;
     uint32_t prev = 0;

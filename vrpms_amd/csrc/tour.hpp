@@ -26,7 +26,8 @@ struct MatView {
   uint32_t N, NN;
   int H;
   VRPMS_DEV int operator()(int t, uint32_t a, uint32_t b) const {
-    return (int)M[hour_of<HM>(t, H) * NN + a * N + b];
+    // a, N < 2^24: the full-rate 24-bit multiply gives the same 32-bit product
+    return (int)M[hour_of<HM>(t, H) * NN + __umul24(a, N) + b];
   }
 };
 
