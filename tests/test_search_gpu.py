@@ -135,17 +135,20 @@ def test_sa_cvrp100_matches_c_restatement(ctx, coracle):
     assert (best.cpu().numpy().view(np.uint16) == cbest).all()
 
 
-@pytest.mark.parametrize("symmetric", [True, False])
-def test_tsp_batch_matches_oracle(ctx, symmetric):
-    """Config-5 throughput kernel: O(1)-delta SA == full-evaluation replay."""
+@pytest.mark.parametrize("kind", ["symmetric", "asymmetric", "large"])
+def test_tsp_batch_matches_oracle(ctx, kind):
+    """Config-5 throughput kernel: O(1)-delta SA == full-evaluation replay.
+    "large": entries >= 2^26 / N take the 64-bit (key, lane) argmin instead
+    of the one-dword (duration << 6 | lane) one."""
     torch = torch_()
     rng = np.random.default_rng(4)
     mats = []
     for r in range(3):
-        if symmetric:
+        if kind == "symmetric":
             mats.append(synth.random_symmetric(9, rng))
         else:
-            m = rng.integers(3, 320, size=(9, 9))
+            hi = 320 if kind == "asymmetric" else 12_000_000
+            m = rng.integers(3 if hi == 320 else 8_000_000, hi, size=(9, 9))
             np.fill_diagonal(m, 0)
             mats.append(m)
     M = torch.tensor(np.array(mats), dtype=torch.int32, device=ctx.dev)

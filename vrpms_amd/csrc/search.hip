@@ -838,12 +838,17 @@ __global__ __launch_bounds__(256) void tsp_batch_sa_kernel(TspBatchArgs a) {
   const int32_t* src = a.mats + (int64_t)r * NN;
   for (uint32_t i = threadIdx.x; i < NN; i += blockDim.x) D[i] = src[i];
   __syncthreads();
-  int asym = 0;
+  int asym = 0, big = 0;
+  // tour durations < 2^26 when every entry is below 2^26 / N: the 64-lane
+  // argmin of (duration, lane) then fits one dword
+  const int32_t lim26 = (int32_t)((1u << 26) / (uint32_t)N);
   for (uint32_t i = threadIdx.x; i < NN; i += blockDim.x) {
     const uint32_t x = i / N, y = i % N;
     asym |= D[i] != D[y * N + x];
+    big |= D[i] < 0 || D[i] >= lim26;
   }
   const bool symmetric = __syncthreads_or(asym) == 0;
+  const bool small = __syncthreads_or(big) == 0;
   const uint32_t npad = ((uint32_t)n + 7u) & ~7u;
   const int wave = threadIdx.x >> 6, lane = lane_id();
   uint16_t* buf = reinterpret_cast<uint16_t*>(smem + ((NN * 4 + 15u) & ~15u)) + wave * 3 * npad;
@@ -883,10 +888,20 @@ __global__ __launch_bounds__(256) void tsp_batch_sa_kernel(TspBatchArgs a) {
     const Move m = decode_move(rr.x, rr.y, rr.z, n);
     auto tourA = [&](int q) { return (uint32_t)A[q]; };
     const int nd = dur + tsp_move_delta(dist, tourA, n, m, symmetric);
-    uint64_t k = pack_key(0, (uint32_t)nd, 0);
-    uint64_t who = (uint64_t)lane;
-    wave_argmin(k, who);
-    const int bl = (int)who;
+    uint64_t k;
+    int bl;
+    if (small) {  // (duration << 6 | lane): the same order as (key, lane)
+      uint32_t v = ((uint32_t)nd << 6) | (uint32_t)lane;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off, 64));
+      bl = (int)(v & 63u);
+      k = pack_key(0, v >> 6, 0);
+    } else {
+      k = pack_key(0, (uint32_t)nd, 0);
+      uint64_t who = (uint64_t)lane;
+      wave_argmin(k, who);
+      bl = (int)who;
+    }
     bool accept = k <= ck;
     if (!accept) {
       const uint64_t d = (k >> 28) - (ck >> 28);
