@@ -73,4 +73,33 @@ VRPMS_DEV void wave_argmin(uint64_t& key, uint64_t& idx) {
   }
 }
 
+// Wave64 min over uint32 with every lane active, returned wave-uniform (SGPR):
+// three DPP steps reduce each 16-lane row in VALU (xor 1, xor 2 inside quads,
+// then the half-row and row mirrors), and four v_readlane + s_min combine the
+// rows -- no LDS round trip, unlike a 6-step ds_bpermute butterfly.
+VRPMS_DEV uint32_t wave_min_u32_uniform(uint32_t v) {
+  auto step = [](uint32_t x, int ctrl) -> uint32_t {
+    uint32_t o = 0;
+    switch (ctrl) {  // the DPP control must be an immediate
+      case 0: o = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false); break;   // quad [1,0,3,2]
+      case 1: o = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false); break;   // quad [2,3,0,1]
+      case 2: o = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false); break;  // row_half_mirror
+      default: o = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false); break; // row_mirror
+    }
+    return min(x, o);
+  };
+  v = step(v, 0);
+  v = step(v, 1);
+  v = step(v, 2);
+  v = step(v, 3);
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+  const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+  const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 32);
+  const uint32_t r3 = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+  return min(min(r0, r1), min(r2, r3));
+}
+
+// x of lane `src` (a wave-uniform index) broadcast through v_readlane.
+VRPMS_DEV int wave_bcast(int x, int src) { return __builtin_amdgcn_readlane(x, src); }
+
 }  // namespace vrpms

@@ -891,9 +891,7 @@ __global__ __launch_bounds__(256) void tsp_batch_sa_kernel(TspBatchArgs a) {
     uint64_t k;
     int bl;
     if (small) {  // (duration << 6 | lane): the same order as (key, lane)
-      uint32_t v = ((uint32_t)nd << 6) | (uint32_t)lane;
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off, 64));
+      const uint32_t v = wave_min_u32_uniform(((uint32_t)nd << 6) | (uint32_t)lane);
       bl = (int)(v & 63u);
       k = pack_key(0, v >> 6, 0);
     } else {
@@ -906,14 +904,14 @@ __global__ __launch_bounds__(256) void tsp_batch_sa_kernel(TspBatchArgs a) {
     if (!accept) {
       const uint64_t d = (k >> 28) - (ck >> 28);
       const uint32_t dp = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
-      accept = (__shfl(rr.w, bl, 64) >> 8) < accept_threshold(dp, invT);
+      accept = ((uint32_t)wave_bcast((int)rr.w, bl) >> 8) < accept_threshold(dp, invT);
     }
-    if (accept) {
+    if (accept) {  // bl is wave-uniform: the winner's move by v_readlane
       Move mb;
-      mb.typ = (uint32_t)__shfl((int)m.typ, bl, 64);
-      mb.i = __shfl(m.i, bl, 64);
-      mb.j = __shfl(m.j, bl, 64);
-      dur = __shfl(nd, bl, 64);
+      mb.typ = (uint32_t)wave_bcast((int)m.typ, bl);
+      mb.i = wave_bcast(m.i, bl);
+      mb.j = wave_bcast(m.j, bl);
+      dur = wave_bcast(nd, bl);
       for (int q = lane; q < n; q += 64) B[q] = A[moved_index(q, mb)];
       wave_sync();
       uint16_t* t = A;
