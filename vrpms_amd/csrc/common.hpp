@@ -99,6 +99,35 @@ VRPMS_DEV uint32_t wave_min_u32_uniform(uint32_t v) {
   return min(min(r0, r1), min(r2, r3));
 }
 
+// Lexicographic (key, lane) argmin with every lane active, both wave-uniform:
+// the same DPP row reduction on the 64-bit key (two dword moves per step),
+// the row minima combined in SGPRs, then the lowest lane holding the minimum
+// from a ballot.  Same result as wave_argmin(key, lane) without ds_bpermute.
+VRPMS_DEV uint64_t wave_argmin_lane(uint64_t key, int& who) {
+  uint64_t v = key;
+  auto take = [&](uint32_t olo, uint32_t ohi) {
+    const uint64_t o = ((uint64_t)ohi << 32) | olo;
+    v = o < v ? o : v;
+  };
+#define VRPMS_DPP_MIN64(ctrl)                                                        \
+  take((uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)v, ctrl, 0xF, 0xF, false), \
+       (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), ctrl, 0xF, 0xF, false))
+  VRPMS_DPP_MIN64(0xB1);   // quad [1,0,3,2]
+  VRPMS_DPP_MIN64(0x4E);   // quad [2,3,0,1]
+  VRPMS_DPP_MIN64(0x141);  // row_half_mirror
+  VRPMS_DPP_MIN64(0x140);  // row_mirror
+#undef VRPMS_DPP_MIN64
+  uint64_t m = ~0ull;
+#pragma unroll
+  for (int row = 0; row < 4; ++row) {
+    const uint64_t r = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 16 * row) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 16 * row);
+    m = r < m ? r : m;
+  }
+  who = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(key == m));
+  return m;
+}
+
 // x of lane `src` (a wave-uniform index) broadcast through v_readlane.
 VRPMS_DEV int wave_bcast(int x, int src) { return __builtin_amdgcn_readlane(x, src); }
 

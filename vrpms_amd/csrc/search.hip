@@ -181,22 +181,21 @@ __global__ __launch_bounds__(256) void sa_kernel(SaArgs a) {
       auto moved = [&](int q) { return (uint32_t)A[moved_index(q, m)]; };
       k = eval_tour<CVRP>(I.D, I.sp, moved, n).key;
     }
-    uint64_t who = (uint64_t)lane;
-    wave_argmin(k, who);
-    const int bl = (int)who;
+    int bl;
+    k = wave_argmin_lane(k, bl);  // wave-uniform (key, lane) minimum
     bool accept = k <= ck;
     if (!accept) {
       const uint64_t d = (k >> 28) - (ck >> 28);
       const uint32_t dp = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
-      const uint32_t u = __shfl(r.w, bl, 64) >> 8;
+      const uint32_t u = (uint32_t)wave_bcast((int)r.w, bl) >> 8;
       accept = u < accept_threshold(dp, invT);
     }
     if (accept) {
       Move mb;
-      mb.typ = (uint32_t)__shfl((int)m.typ, bl, 64);
-      mb.i = __shfl(m.i, bl, 64);
-      mb.j = __shfl(m.j, bl, 64);
-      if constexpr (kDelta) dur = __shfl(nd, bl, 64);
+      mb.typ = (uint32_t)wave_bcast((int)m.typ, bl);
+      mb.i = wave_bcast(m.i, bl);
+      mb.j = wave_bcast(m.j, bl);
+      if constexpr (kDelta) dur = wave_bcast(nd, bl);
       for (int q = lane; q < n; q += 64) B[q] = A[moved_index(q, mb)];
       wave_sync();
       uint16_t* t = A;
@@ -347,20 +346,19 @@ __global__ __launch_bounds__(1024) void sa_packed_kernel(SaPackedArgs a) {
                            (uint32_t)lane, a.seed_lo, a.seed_hi);
     const Move m = decode_move(r.x, r.y, r.z, n);
     uint64_t k = eval_mapped(a.f, smem, N8, A, n, move_map(m));
-    uint64_t who = (uint64_t)lane;
-    wave_argmin(k, who);
-    const int bl = (int)who;
+    int bl;
+    k = wave_argmin_lane(k, bl);  // wave-uniform (key, lane) minimum
     bool accept = k <= ck;
     if (!accept) {
       const uint64_t d = (k >> 28) - (ck >> 28);
       const uint32_t dp = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
-      accept = (__shfl(r.w, bl, 64) >> 8) < accept_threshold(dp, invT);
+      accept = ((uint32_t)wave_bcast((int)r.w, bl) >> 8) < accept_threshold(dp, invT);
     }
     if (accept) {
       Move mb;
-      mb.typ = (uint32_t)__shfl((int)m.typ, bl, 64);
-      mb.i = __shfl(m.i, bl, 64);
-      mb.j = __shfl(m.j, bl, 64);
+      mb.typ = (uint32_t)wave_bcast((int)m.typ, bl);
+      mb.i = wave_bcast(m.i, bl);
+      mb.j = wave_bcast(m.j, bl);
       const MoveMap mm = move_map(mb);
       for (int q = lane; q < n; q += 64) B[q] = A[map_src(mm, q)];
       wave_sync();
@@ -895,10 +893,7 @@ __global__ __launch_bounds__(256) void tsp_batch_sa_kernel(TspBatchArgs a) {
       bl = (int)(v & 63u);
       k = pack_key(0, v >> 6, 0);
     } else {
-      k = pack_key(0, (uint32_t)nd, 0);
-      uint64_t who = (uint64_t)lane;
-      wave_argmin(k, who);
-      bl = (int)who;
+      k = wave_argmin_lane(pack_key(0, (uint32_t)nd, 0), bl);
     }
     bool accept = k <= ck;
     if (!accept) {
