@@ -885,7 +885,8 @@ __global__ __launch_bounds__(256) void tsp_batch_sa_kernel(TspBatchArgs a) {
     const u32x4 rr = philox((uint32_t)s, 0u, cid, (uint32_t)lane, a.seed_lo, a.seed_hi);
     const Move m = decode_move(rr.x, rr.y, rr.z, n);
     auto tourA = [&](int q) { return (uint32_t)A[q]; };
-    const int nd = dur + tsp_move_delta(dist, tourA, n, m, symmetric);
+    const int nd = dur + (symmetric ? tsp_move_delta_sym(dist, tourA, n, m)
+                                    : tsp_move_delta(dist, tourA, n, m, false));
     uint64_t k;
     int bl;
     if (small) {  // (duration << 6 | lane): the same order as (key, lane)

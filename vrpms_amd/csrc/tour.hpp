@@ -195,6 +195,42 @@ VRPMS_DEV int tsp_move_delta(const Dist& d, const Tour& T, int n, const Move& m,
   return d(a, pi) + d(pi, pj) + d(y, b) - d(a, pj) - d(y, pi) - d(pi, b);
 }
 
+// tsp_move_delta for a symmetric matrix without divergent branches: every
+// move type is "add four edges, remove four edges" over the six tour
+// positions i-1 .. j+1 (unused slots add and remove the same edge, which
+// cancels exactly), so a wave whose lanes drew different move types issues
+// 6 tour reads + 8 matrix gathers once instead of running every type's
+// branch under its own exec mask.  Same integer result as tsp_move_delta.
+template <typename Dist, typename Tour>
+VRPMS_DEV int tsp_move_delta_sym(const Dist& d, const Tour& T, int n, const Move& m) {
+  auto at = [&](int q) -> uint32_t { return (uint32_t)q < (uint32_t)n ? (uint32_t)T(q) : 0u; };
+  const int i = m.i, j = m.j;
+  const uint32_t im1 = at(i - 1), pi = at(i), ip1 = at(i + 1);
+  const uint32_t jm1 = at(j - 1), pj = at(j), jp1 = at(j + 1);
+  const bool swp = m.typ == kMoveSwap, opt = m.typ == kMove2Opt, rel = m.typ == kMoveRelocate;
+  const bool adj = swp && j == i + 1, lo = rel && i < j, hi = rel && i > j;
+  // plus edges (a_k, b_k), minus edges (c_k, e_k), k = 0..3
+  // swap     : +(im1,pj) +(pj,ip1) +(jm1,pi) +(pi,jp1)  -(im1,pi) -(pi,ip1) -(jm1,pj) -(pj,jp1)
+  // swap adj : +(im1,pj) +(pj,pi)  +(pi,jp1) pad        -(im1,pi) -(pi,pj)  -(pj,jp1) pad
+  // 2-opt    : +(im1,pj) +(pi,jp1) pad       pad        -(im1,pi) -(pj,jp1) pad       pad
+  // reloc i<j: +(im1,ip1) +(pj,pi) +(pi,jp1) pad        -(im1,pi) -(pi,ip1) -(pj,jp1) pad
+  // reloc i>j: +(jm1,pi) +(pi,pj)  +(im1,ip1) pad       -(jm1,pj) -(im1,pi) -(pi,ip1) pad
+  const uint32_t a0 = hi ? jm1 : im1, b0 = lo ? ip1 : (hi ? pi : pj);
+  const uint32_t c0 = hi ? jm1 : im1, e0 = hi ? pj : pi;
+  const uint32_t a1 = opt ? pi : (lo ? pj : (hi ? pi : pj));
+  const uint32_t b1 = opt ? jp1 : (lo ? pi : (hi ? pj : (adj ? pi : ip1)));
+  const uint32_t c1 = opt ? pj : (hi ? im1 : pi);
+  const uint32_t e1 = opt ? jp1 : (hi ? pi : (adj ? pj : ip1));
+  const uint32_t a2 = opt ? pi : (hi ? im1 : (swp && !adj ? jm1 : pi));
+  const uint32_t b2 = opt ? pi : (hi ? ip1 : (swp && !adj ? pi : jp1));
+  const uint32_t c2 = opt ? pi : (hi ? pi : (swp && !adj ? jm1 : pj));
+  const uint32_t e2 = opt ? pi : (hi ? ip1 : (swp && !adj ? pj : jp1));
+  const bool full = swp && !adj;
+  const uint32_t a3 = pi, b3 = full ? jp1 : pi;
+  const uint32_t c3 = full ? pj : pi, e3 = full ? jp1 : pi;
+  return d(a0, b0) + d(a1, b1) + d(a2, b2) + d(a3, b3) - d(c0, e0) - d(c1, e1) - d(c2, e2) - d(c3, e3);
+}
+
 // ---------------------------------------------------------------------------
 // Deterministic SA acceptance threshold: floor(2^24 * exp(-dp * invT)) using
 // only IEEE fp32 multiply/add/sub (built with -ffp-contract=off) and exact
