@@ -175,7 +175,8 @@ __global__ __launch_bounds__(256) void sa_kernel(SaArgs a) {
     if constexpr (kDelta) {
       auto dist = [&](uint32_t x, uint32_t y) { return I.D(0, x, y); };
       auto tourA = [&](int q) { return min((uint32_t)A[q], Nm1); };
-      nd = dur + tsp_move_delta(dist, tourA, n, m, a.si.symmetric != 0);
+      nd = dur + (a.si.symmetric ? tsp_move_delta_sym(dist, tourA, n, m)
+                                 : tsp_move_delta(dist, tourA, n, m, false));
       k = pack_key(0, (uint32_t)nd, 0);
     } else {
       auto moved = [&](int q) { return (uint32_t)A[moved_index(q, m)]; };
