@@ -34,6 +34,8 @@ def load():
         lib.oracle_sa_run.restype = ctypes.c_int
         lib.oracle_sa_run.argtypes = [i32, vp, i32, i32, vp, vp, vp, i32, i32, vp, vp, vp, vp, i32,
                                       i32, i32, f32, f32, u64, u64, i32]
+        lib.oracle_tsp_batch_sa.restype = ctypes.c_int
+        lib.oracle_tsp_batch_sa.argtypes = [vp, i32, i32, i32, f32, f32, u64, vp, vp, i32]
         _lib = lib
     return _lib
 
@@ -89,6 +91,20 @@ def sa_run(durations, cur, best, best_key, steps, inv_t0, inv_alpha, seed, step0
                       float(inv_t0), float(inv_alpha), int(seed) & (2**64 - 1), int(step0),
                       threads)
     return cur_key
+
+
+def tsp_batch_sa(mats, steps, inv_t0, inv_alpha, seed, threads: int = 0):
+    """C/OpenMP restatement of vrpms_tsp_batch_sa (N <= 257): mats int [R][N][N]
+    -> (tours uint16 [R][N-1], keys uint64 [R])."""
+    lib = load()
+    M = np.ascontiguousarray(np.asarray(mats, dtype=np.int32))
+    R, N = M.shape[0], M.shape[1]
+    assert 2 <= N <= 257
+    tours = np.zeros((R, max(N - 1, 1)), dtype=np.uint16)
+    keys = np.zeros(R, dtype=np.uint64)
+    lib.oracle_tsp_batch_sa(_p(M), R, N, int(steps), float(inv_t0), float(inv_alpha),
+                            int(seed) & (2**64 - 1), _p(tours), _p(keys), threads)
+    return tours, keys
 
 
 def max_threads() -> int:

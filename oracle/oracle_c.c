@@ -317,6 +317,81 @@ int oracle_sa_run(int problem, const int32_t* D, int H, int N, const int32_t* de
   return 0;
 }
 
+/* Throughput-mode restatement (oracle/search.py tsp_batch_sa, the C-ABI's
+ * vrpms_tsp_batch_sa): R static TSP requests, int32 [R][N][N]; per request 4
+ * chains from Philox Fisher-Yates starts (counters (~0, ~0, 4r + w, i)), SA
+ * steps with counters (s, 0, 4r + w, lane), every candidate priced by a full
+ * re-evaluation (the device prices by O(1) deltas, so equality checks them);
+ * the answer is the best (key, chain).  Out: tours [R][N-1], keys [R]. */
+int oracle_tsp_batch_sa(const int32_t* mats, int R, int N, int steps, float inv_t0,
+                        float inv_alpha, uint64_t seed, uint16_t* out_tours, uint64_t* out_keys,
+                        int threads) {
+  const int n = N - 1;
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  int32_t zero = 0;
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+  for (int r = 0; r < R; ++r) {
+    inst_t I = {0, 1, N, 1, 0, mats + (int64_t)r * N * N, NULL, NULL, &zero};
+    uint16_t A[256], B[256], Bst[256], best_t[256];
+    uint64_t best_k = ~0ull;
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t cid = (uint32_t)(4 * r + w);
+      for (int q = 0; q < n; ++q) A[q] = (uint16_t)(q + 1);
+      for (int i = n - 1; i >= 1; --i) {
+        u32x4 x = philox(0xffffffffu, 0xffffffffu, cid, (uint32_t)i, k0, k1);
+        int j = (int)(x.x % (uint32_t)(i + 1));
+        uint16_t t = A[i];
+        A[i] = A[j];
+        A[j] = t;
+      }
+      uint64_t ck = tour_key(&I, A, n, NULL), bk = ck;
+      memcpy(Bst, A, (size_t)n * 2);
+      float invT = inv_t0;
+      for (int s = 0; s < steps && n >= 2; ++s) {
+        uint64_t kbest = ~0ull;
+        move_t mbest = {0, 0, 0};
+        uint32_t wbest = 0;
+        for (int lane = 0; lane < 64; ++lane) {
+          u32x4 rr = philox((uint32_t)s, 0u, cid, (uint32_t)lane, k0, k1);
+          move_t m = decode_move(rr.x, rr.y, rr.z, n);
+          uint64_t kk = tour_key(&I, A, n, &m);
+          if (kk < kbest) {
+            kbest = kk;
+            mbest = m;
+            wbest = rr.w;
+          }
+        }
+        int acc = kbest <= ck;
+        if (!acc) {
+          uint64_t d = (kbest >> 28) - (ck >> 28);
+          uint32_t dp = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
+          acc = (wbest >> 8) < accept_threshold(dp, invT);
+        }
+        if (acc) {
+          for (int q = 0; q < n; ++q) B[q] = A[moved_index(q, &mbest)];
+          memcpy(A, B, (size_t)n * 2);
+          ck = kbest;
+          if (ck < bk) {
+            bk = ck;
+            memcpy(Bst, A, (size_t)n * 2);
+          }
+        }
+        invT = invT * inv_alpha;
+      }
+      if (bk < best_k) {
+        best_k = bk;
+        memcpy(best_t, Bst, (size_t)n * 2);
+      }
+    }
+    memcpy(out_tours + (int64_t)r * n, best_t, (size_t)n * 2);
+    out_keys[r] = best_k;
+  }
+  return 0;
+}
+
 int oracle_max_threads(void) {
 #ifdef _OPENMP
   return omp_get_max_threads();

@@ -29,6 +29,18 @@ def test_calculate_duration_shape_and_stub_range():
     assert 3 <= got["duration"] <= 320
 
 
+def test_calculate_duration_seeded_equals_reference():
+    """With no matrix loaded the drop-in keeps the reference stub
+    (src/solver.py:12, randint(3, 320) on the global `random`): under
+    random.seed(7) it must return the reference's captured values exactly
+    (tests/golden/gen_reference_fixtures.py:148-149)."""
+    import random
+    solver._LOOKUP = None
+    random.seed(7)
+    got = [solver.calculate_duration("A", "B") for _ in range(len(FX["calculate_duration"]))]
+    assert got == FX["calculate_duration"]
+
+
 def test_calculate_duration_backed_by_matrix():
     D = np.zeros((24, 3, 3), dtype=np.int64)
     for h in range(24):

@@ -146,6 +146,25 @@ def test_c_sa_matches_python_replay(coracle, kind):
     assert best.tolist() == ref[2] and [int(x) for x in bk] == ref[3]
 
 
+@pytest.mark.parametrize("kind", ["symmetric", "asymmetric"])
+def test_c_tsp_batch_matches_python_replay(coracle, kind):
+    """The C restatement of vrpms_tsp_batch_sa (used for the TSP-50 GPU
+    parity test, where the pure-Python replay is too slow) == search.py."""
+    from oracle import search
+    rng = np.random.default_rng(6)
+    mats = []
+    for _ in range(3):
+        if kind == "symmetric":
+            mats.append(synth.random_symmetric(8, rng))
+        else:
+            m = rng.integers(3, 320, size=(8, 8))
+            np.fill_diagonal(m, 0)
+            mats.append(m)
+    tours, keys = coracle.tsp_batch_sa(mats, 20, 1 / 60.0, 1 / 0.97, 31)
+    rt, rk = search.tsp_batch_sa(mats, 20, 1 / 60.0, 1 / 0.97, 31)
+    assert tours.tolist() == rt and [int(k) for k in keys] == rk
+
+
 def test_accept_threshold_tracks_exp():
     from oracle import search
     for dp in [1, 5, 37, 400, 2000]:

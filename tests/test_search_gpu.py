@@ -135,6 +135,98 @@ def test_sa_cvrp100_matches_c_restatement(ctx, coracle):
     assert (best.cpu().numpy().view(np.uint16) == cbest).all()
 
 
+L2_CASES = [
+    # BASELINE cfg 3: 24 x 201^2 u16 = 1.94 MB (L2 tier, hour-indexed clock)
+    ("tdvrp200_h24", lambda: synth.td_cvrp(200, 16, seed=0)),
+    # BASELINE cfg 4: X-style CVRP-1000, 1001^2 u16 = 2.0 MB (L2 tier)
+    ("x1000", lambda: synth.x_style(1000, seed=0)),
+]
+
+
+@pytest.mark.parametrize("name,maker", L2_CASES, ids=[c[0] for c in L2_CASES])
+def test_sa_l2_tier_matches_c_restatement(ctx, coracle, name, maker):
+    """sa_kernel with the matrix L2-resident (mat_lds = 0) at the sizes
+    configs 3 and 4 run: 16 chains x 30 steps, tours and keys bit-equal to
+    the C restatement driven by the same Philox streams."""
+    torch = torch_()
+    inst = maker()
+    load(ctx, inst)
+    chains, n = 16, inst.n
+    P = synth.random_perms(chains, n, seed=31, dtype=np.uint16).astype(np.int16)
+    cur = torch.from_numpy(P).to(ctx.dev)
+    best = cur.clone()
+    ck = torch.empty(chains, dtype=torch.int64, device=ctx.dev)
+    bk = torch.full((chains,), -1, dtype=torch.int64, device=ctx.dev)
+    ctx.sa_run(cur, ck, best, bk, steps=30, inv_t0=1 / 100.0, inv_alpha=1 / 0.99, seed=17,
+               step0=40)
+    ccur, cbest = P.view(np.uint16).copy(), P.view(np.uint16).copy()
+    cbk = np.full(chains, 2**64 - 1, dtype=np.uint64)
+    cck = coracle.sa_run(inst.durations, ccur, cbest, cbk, 30, 1 / 100.0, 1 / 0.99, 17, 40,
+                         inst.demand, inst.capacities, inst.start_times)
+    assert (cur.cpu().numpy().view(np.uint16) == ccur).all()
+    assert u64(ck) == [int(x) for x in cck]
+    assert u64(bk) == [int(x) for x in cbk]
+    assert (best.cpu().numpy().view(np.uint16) == cbest).all()
+
+
+def test_sa_l2_tier_small_td_matches_python_oracle(ctx):
+    """A small hour-indexed instance whose matrix (24 x 61^2 u16 = 179 KB)
+    still exceeds the 64 KB LDS budget: the L2 branch against the pure-Python
+    replay."""
+    torch = torch_()
+    inst = synth.td_cvrp(60, 5, seed=12)
+    load(ctx, inst)
+    chains, n = 3, inst.n
+    P = synth.random_perms(chains, n, seed=4).astype(np.int16)
+    cur = torch.from_numpy(P).to(ctx.dev)
+    best = cur.clone()
+    ck = torch.empty(chains, dtype=torch.int64, device=ctx.dev)
+    bk = torch.full((chains,), -1, dtype=torch.int64, device=ctx.dev)
+    ctx.sa_run(cur, ck, best, bk, steps=8, inv_t0=1 / 90.0, inv_alpha=1 / 0.98, seed=3, step0=0)
+    ref = search.sa_run(scorer(inst), P.tolist(), P.tolist(), [2**64 - 1] * chains, 3, 0, 8,
+                        1 / 90.0, 1 / 0.98)
+    assert cur.cpu().numpy().tolist() == ref[0]
+    assert u64(ck) == ref[1]
+    assert best.cpu().numpy().tolist() == ref[2]
+    assert u64(bk) == ref[3]
+
+
+def test_ga_cvrp100_matches_oracle(ctx):
+    """GA at the cfg-2 size (4 islands x 64, 5 generations): every
+    population and key equal to the Python replay."""
+    torch = torch_()
+    inst = synth.cvrp(100, 8, seed=0)
+    load(ctx, inst)
+    islands, pop, n = 4, 64, inst.n
+    P = synth.random_perms(islands * pop, n, seed=13).astype(np.int16)
+    dpop = torch.from_numpy(P.reshape(islands, pop, n).copy()).to(ctx.dev)
+    keys = ctx.eval(dpop.view(islands * pop, n)).view(islands, pop)
+    sc = scorer(inst)
+    rpop = [[list(r) for r in P.reshape(islands, pop, n)[i]] for i in range(islands)]
+    rkeys = [[sc(t) for t in rpop[i]] for i in range(islands)]
+    seed, pmut = 2024, 0.25
+    pm = min(int(round(pmut * 2**32)), 2**32 - 1)
+    for g in range(5):
+        rpop, rkeys = search.ga_generation(sc, rpop, rkeys, seed, 10 + g, pm)
+    ctx.ga_generation(dpop, keys, generations=5, pmut=pmut, seed=seed, gen0=10)
+    assert dpop.cpu().numpy().tolist() == rpop
+    assert u64(keys) == [k for ks in rkeys for k in ks]
+
+
+def test_tsp_batch_tsp50_matches_c_restatement(ctx, coracle):
+    """Config-5 kernel at its real size (N = 50) on 128 requests x 300 steps:
+    best tours and keys equal the C restatement (full re-evaluation)."""
+    torch = torch_()
+    rng = np.random.default_rng(50)
+    R = 128
+    mats = np.stack([synth.random_symmetric(50, rng) for _ in range(R)])
+    M = torch.tensor(mats, dtype=torch.int32, device=ctx.dev)
+    tours, keys = ctx.tsp_batch_sa(M, steps=300, inv_t0=1 / 80.0, inv_alpha=1 / 0.99, seed=8)
+    rt, rk = coracle.tsp_batch_sa(mats, 300, 1 / 80.0, 1 / 0.99, 8)
+    assert (tours.cpu().numpy().view(np.uint16) == rt).all()
+    assert u64(keys) == [int(k) for k in rk]
+
+
 @pytest.mark.parametrize("kind", ["symmetric", "asymmetric", "large"])
 def test_tsp_batch_matches_oracle(ctx, kind):
     """Config-5 throughput kernel: O(1)-delta SA == full-evaluation replay.

@@ -46,8 +46,8 @@ struct SearchInst {
   const int32_t* dem;
   const int32_t* cap;
   const int32_t* start;
-  int mat_lds;       // 1: stage the matrix into LDS
-  uint32_t mat_bytes;
+  int mat_lds;       // 1: stage the matrix into LDS (only when mat_bytes <= 64 KB)
+  uint64_t mat_bytes; // H*N*N*elem: 64-bit, an int32 matrix can exceed 4 GB
   int symmetric;     // hour slice 0 symmetric (O(1) 2-opt delta)
 };
 
@@ -63,20 +63,20 @@ static SearchInst search_inst(const vrpms_ctx* ctx) {
   s.dem = in.dem;
   s.cap = in.cap;
   s.start = in.start;
-  s.mat_bytes = (uint32_t)((size_t)in.H * in.N * in.N * (in.use16 ? 2 : 4));
-  s.mat_lds = s.mat_bytes <= 64 * 1024 ? 1 : 0;
+  s.mat_bytes = (uint64_t)in.H * (uint64_t)in.N * (uint64_t)in.N * (in.use16 ? 2u : 4u);
+  s.mat_lds = s.mat_bytes <= 64u * 1024u ? 1 : 0;
   s.symmetric = in.symmetric ? 1 : 0;
   return s;
 }
 
 // LDS carve for the instance part: [matrix][dem N][cap K][start K], 16-B aligned.
 VRPMS_DEV uint32_t inst_lds_bytes(const SearchInst& si) {
-  const uint32_t m = si.mat_lds ? ((si.mat_bytes + 15u) & ~15u) : 0u;
+  const uint32_t m = si.mat_lds ? (((uint32_t)si.mat_bytes + 15u) & ~15u) : 0u;
   return m + (((uint32_t)(si.N + 2 * si.K) * 4u + 15u) & ~15u);
 }
 
 static size_t inst_lds_bytes_host(const SearchInst& si) {
-  const size_t m = si.mat_lds ? ((si.mat_bytes + 15u) & ~(size_t)15u) : 0u;
+  const size_t m = si.mat_lds ? (((size_t)si.mat_bytes + 15u) & ~(size_t)15u) : 0u;
   return m + ((((size_t)si.N + 2 * si.K) * 4u + 15u) & ~(size_t)15u);
 }
 
@@ -92,14 +92,14 @@ VRPMS_DEV StagedInst<MatT, HM> stage_inst(const SearchInst& si, unsigned char* s
   const MatT* M = static_cast<const MatT*>(si.mat);
   uint32_t off = 0;
   if (si.mat_lds) {
+    const uint32_t mb = (uint32_t)si.mat_bytes;  // <= 64 KB when staged
     const uint32_t* s = static_cast<const uint32_t*>(si.mat);
     uint32_t* d = reinterpret_cast<uint32_t*>(smem);
-    for (uint32_t i = threadIdx.x; i < si.mat_bytes / 4; i += blockDim.x) d[i] = s[i];
-    if ((si.mat_bytes & 2u) && threadIdx.x == 0)
-      reinterpret_cast<uint16_t*>(smem)[si.mat_bytes / 2 - 1] =
-          static_cast<const uint16_t*>(si.mat)[si.mat_bytes / 2 - 1];
+    for (uint32_t i = threadIdx.x; i < mb / 4; i += blockDim.x) d[i] = s[i];
+    if ((mb & 2u) && threadIdx.x == 0)
+      reinterpret_cast<uint16_t*>(smem)[mb / 2 - 1] = static_cast<const uint16_t*>(si.mat)[mb / 2 - 1];
     M = reinterpret_cast<const MatT*>(smem);
-    off = (si.mat_bytes + 15u) & ~15u;
+    off = (mb + 15u) & ~15u;
   }
   int32_t* dem = reinterpret_cast<int32_t*>(smem + off);
   int32_t* cap = dem + si.N;

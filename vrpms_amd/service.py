@@ -179,7 +179,15 @@ class TspBatcher:
 
     @classmethod
     def accepts(cls, ci) -> bool:
-        return ci.durations.shape[0] == 1 and cls.MIN_N <= ci.N <= cls.MAX_N
+        """Static matrices of MIN_N..MAX_N nodes that also pass the A9 int32
+        guard vrpms_set_instance applies on the unbatched path
+        ((N + K + 1) * max_duration < 2^31, K = 1, start time 0 here because
+        a static tour's duration does not depend on it); anything else takes
+        the unbatched path, so both paths share one error contract."""
+        if ci.durations.shape[0] != 1 or not cls.MIN_N <= ci.N <= cls.MAX_N:
+            return False
+        mx = int(ci.durations.max()) if ci.durations.size else 0
+        return (ci.N + 2) * mx < 2**31
 
     def solve(self, ci) -> dict:
         """Blocks until the request's launch finished -> the TSP slot dict."""
@@ -222,13 +230,13 @@ class TspBatcher:
         import numpy as np
         import torch
         from . import runners, solver
-        ctx = solver.context(self.app.device)
-        mats = torch.tensor(np.stack([ci.durations[0] for ci in cis]), dtype=torch.int32,
-                            device=ctx.dev)
         edge = float(np.mean([runners.typical_edge(ci.durations[0]) for ci in cis]))
         inv_t0 = 1.0 / (0.5 * edge)
         inv_alpha = (0.5 / 0.002) ** (1.0 / max(1, self.steps))
         with self.app.gpu_lock:
+            ctx = solver.context(self.app.device)
+            mats = torch.tensor(np.stack([ci.durations[0] for ci in cis]), dtype=torch.int32,
+                                device=ctx.dev)
             tours, _ = ctx.tsp_batch_sa(mats, self.steps, inv_t0, inv_alpha, self.app.seed)
             torch.cuda.synchronize(ctx.dev)
         return [[int(x) for x in row] for row in tours.cpu().tolist()]

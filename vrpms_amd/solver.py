@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import datetime
 import random
+import threading
 import time
 from dataclasses import dataclass
 
@@ -123,13 +124,18 @@ def compact_vrp(durations, locations, capacities, start_times, ignored_customers
 # device context (one per process; the handlers call in sequentially)
 # ---------------------------------------------------------------------------
 _CTX: Context | None = None
+_CTX_LOCK = threading.Lock()
 
 
 def context(device: int = 0) -> Context:
+    """The process-wide context on `device` (created once; the check and the
+    creation are one critical section, so concurrent first calls from the
+    request threads and the batcher share a single vrpms_ctx)."""
     global _CTX
-    if _CTX is None or _CTX.device != device:
-        _CTX = Context(device)
-    return _CTX
+    with _CTX_LOCK:
+        if _CTX is None or _CTX.device != device:
+            _CTX = Context(device)
+        return _CTX
 
 
 def load(ctx: Context, ci: CompactInstance, objective: int = OBJ_SUM):
