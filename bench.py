@@ -191,7 +191,7 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
     gpu_wall = cool.elapsed()
     key, tour = r.best()
     if world > 1:
-        key, _ = islands.global_best(key, tour.cpu().tolist(), n, device=dev)
+        key, _ = islands.global_best(r)
     out = {"T_s": seconds, "algorithm": "sa", "instance": label, "cooling": "wall-time geometric",
            "gpu": {"chains_per_gpu": chains, "steps_per_chain": r.step, "epochs": e,
                    "wall_s": gpu_wall, "unvisited": key >> 56,
@@ -336,7 +336,7 @@ def island_leg(ctx, torch, dev, world, rank, dist, epochs=20, steps=25, chains=1
         t = torch.tensor([wall, t_ex], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall, t_ex = float(t[0]), float(t[1])
-        key, _ = islands.global_best(key, tour.cpu().tolist(), x.n, device=dev)
+        key, _ = islands.global_best(r)
     evals = world * chains * epochs * steps * 64
     return {"workload": "cfg4 X-style CVRP-1000, island SA", "vehicles": x.K,
             "chains_per_gpu": chains, "epochs": epochs, "steps_per_epoch": steps,

@@ -88,8 +88,10 @@ int vrpms_eval(vrpms_ctx* ctx, const void* d_perms, int32_t perm_bytes, int64_t 
  *   d_words   uint32 [ceil(n/4)][C]; word w of candidate c packs customers
  *             4w..4w+3 (uint8 each, low byte first).  N <= 256.
  * Lane c's loads of word w form one contiguous 256-B wave access, so tours
- * stream HBM -> registers with no LDS staging (the layout the on-device
- * search kernels emit).  Outputs as vrpms_eval. */
+ * stream HBM -> registers with no LDS staging.  This is the layout the GA
+ * breed and ACO construct kernels emit for CVRP with N <= 256, so their
+ * children / ants are scored by this kernel (eval_cvrp_words2).  Outputs
+ * as vrpms_eval. */
 int vrpms_eval_words(vrpms_ctx* ctx, const uint32_t* d_words, int64_t C, int32_t n,
                      uint64_t* d_keys, int32_t* d_sum, int32_t* d_max, int32_t* d_unv,
                      void* stream);
@@ -178,7 +180,9 @@ typedef struct {
 } vrpms_ga_params;
 
 /* d_pop [islands][pop][n] and d_keys [islands][pop] in/out (keys must
- * score d_pop on entry, e.g. by vrpms_eval). */
+ * score d_pop on entry, e.g. by vrpms_eval).  For CVRP with N <= 256 (the
+ * packed-LDS instances) the breed kernel emits the children in the
+ * word-interleaved layout and eval_cvrp_words2 scores them. */
 int vrpms_ga_generation(vrpms_ctx* ctx, const vrpms_ga_params* p, uint16_t* d_pop,
                         uint64_t* d_keys, int32_t n, void* stream);
 
@@ -200,10 +204,16 @@ int vrpms_aco_init(vrpms_ctx* ctx, int32_t colonies, uint32_t tau0, uint32_t* d_
                    uint32_t* d_eta, void* stream);
 
 /* One iteration: construct d_tours [colonies][ants][n] (n = N - 1), score
- * them into d_keys, d_iter_best [colonies][2] = (key, ant), update tau. */
+ * them into d_keys, d_iter_best [colonies][2] = (key, ant), update tau.
+ * d_best_tours [colonies][n] / d_best_keys [colonies] (nullable, both or
+ * neither): each colony's best-so-far, replaced by its iteration best when
+ * strictly better (set the keys to UINT64_MAX before the first call).
+ * For CVRP with N <= 256 the ants also emit the word-interleaved layout and
+ * are scored by the headline kernel (eval_cvrp_words2). */
 int vrpms_aco_iteration(vrpms_ctx* ctx, const vrpms_aco_params* p, uint32_t* d_tau,
                         const uint32_t* d_eta, uint16_t* d_tours, uint64_t* d_keys,
-                        uint64_t* d_iter_best, int32_t n, void* stream);
+                        uint64_t* d_iter_best, uint16_t* d_best_tours, uint64_t* d_best_keys,
+                        int32_t n, void* stream);
 
 /* Brute force (api/{tsp,vrp}/bf/index.py): lexicographic ranks
  * [rank_begin, rank_end) of the permutations of customers 1..n (n <= 15);
@@ -222,6 +232,76 @@ int vrpms_bf_run(vrpms_ctx* ctx, int32_t n, uint64_t rank_begin, uint64_t rank_e
 int vrpms_tsp_batch_sa(vrpms_ctx* ctx, const int32_t* d_mats, int32_t R, int32_t N,
                        const vrpms_sa_params* p, uint16_t* d_best_tours, uint64_t* d_best_keys,
                        void* stream);
+
+/* ------------------------------------------------------------------------
+ * Populations and the island model.  A pool is a set of
+ * tours with their A8 keys: SA chains, a GA population ([islands][pop],
+ * each island sorted by (key, index)), or the per-colony bests of ACO.
+ * Everything here runs on the device, so the search path issues no torch
+ * compute (torch only owns the buffers).
+ * ---------------------------------------------------------------------- */
+typedef struct {
+  uint16_t* tours;   /* [count][n] */
+  uint64_t* keys;    /* [count] */
+  int32_t count;     /* rows */
+  int32_t n;         /* customers per tour */
+  int32_t groups;    /* VRPMS_INJECT_SORTED: `groups` sorted groups of count / groups rows */
+} vrpms_pool;
+
+/* How migrants enter a pool (vrpms_pool_inject / vrpms_island_exchange). */
+#define VRPMS_INJECT_WORST 0  /* migrant e replaces the e-th worst row, by (key desc, index asc) */
+#define VRPMS_INJECT_SORTED 1 /* migrant e takes slot count/groups - 1 - e/groups of group
+                                 e % groups; every group is re-sorted by (key, index) */
+#define VRPMS_INJECT_BETTER 2 /* migrant e replaces row e (< count) when its key is smaller */
+
+/* Start tours (the front-end's initial SA chains / GA population, the
+ * bench's candidate batch): row r of `count` is the Philox Fisher-Yates
+ * permutation of 1..n -- for i = n-1 .. 1 swap t[i] and t[w % (i+1)], w word
+ * (i & 3) of philox4x32_10((i >> 2, 0xfffffffe, r, stream_id), seed) --
+ * written as uint8 (tour_bytes 1, n <= 255) or uint16 rows of `ld` elements. */
+int vrpms_random_tours(vrpms_ctx* ctx, int64_t count, int32_t n, int64_t ld, int32_t tour_bytes,
+                       uint64_t seed, uint32_t stream_id, void* d_tours, void* stream);
+
+/* The E best rows of a pool by (key, index), ascending: d_tours [E][n],
+ * d_keys [E] (0 < E <= min(count, 1024)). */
+int vrpms_pool_elites(vrpms_ctx* ctx, const vrpms_pool* pool, int32_t E, uint16_t* d_tours,
+                      uint64_t* d_keys, void* stream);
+
+/* Put E migrants (d_tours [E][n], d_keys [E]) into a pool by `mode`. */
+int vrpms_pool_inject(vrpms_ctx* ctx, const vrpms_pool* pool, int32_t mode,
+                      const uint16_t* d_tours, const uint64_t* d_keys, int32_t E, void* stream);
+
+/* Island message of E elites of n customers: [E keys u64][E x n tours u16],
+ * zero padded to a multiple of 16 bytes.  Returns its size in bytes. */
+int64_t vrpms_island_msg_bytes(int32_t E, int32_t n);
+
+/* The E elites of `pool` as one message (d_msg, vrpms_island_msg_bytes). */
+int vrpms_island_pack(vrpms_ctx* ctx, const vrpms_pool* pool, int32_t E, void* d_msg,
+                      void* stream);
+
+/* The E best of `world` gathered messages (d_msgs = world messages back to
+ * back, in rank order) by (key, rank, position in the message). */
+int vrpms_island_merge(vrpms_ctx* ctx, const void* d_msgs, int32_t world, int32_t E, int32_t n,
+                       uint16_t* d_tours, uint64_t* d_keys, void* stream);
+
+/* RCCL communicator of the island model: rank 0 calls vrpms_island_unique_id
+ * (128 opaque bytes), shares them with every rank (the front-end uses its
+ * torch.distributed group), and every rank calls vrpms_island_init.  One
+ * process per GPU; the communicator runs over xGMI on an MI355X node. */
+int vrpms_island_unique_id(void* out128);
+int vrpms_island_init(vrpms_ctx* ctx, const void* unique_id, int32_t rank, int32_t world);
+/* world of the context's communicator, 0 when none was initialised */
+int vrpms_island_world(vrpms_ctx* ctx);
+
+/* One migration: the E elites of `src` are packed, all-gathered over the
+ * context's RCCL communicator (a local copy when none: world 1), merged by
+ * (key, rank, position) and injected into `dst` by `mode` -- every rank ends
+ * with the same E migrants.  SA: src = bests, dst = current chains, WORST;
+ * GA: src = dst = population, SORTED; ACO: src = dst = colony bests, BETTER.
+ * (SURVEY.md §8b names this vrpms_island_exchange(ctx, n_elite, stream); the
+ * pools are passed per call instead of being registered in the context.) */
+int vrpms_island_exchange(vrpms_ctx* ctx, const vrpms_pool* src, const vrpms_pool* dst,
+                          int32_t mode, int32_t E, void* stream);
 
 /* Roofline probe (measurement only): `blocks` x 1024 lanes each issue
  * 4 * iters random ds_read_b64 gathers over a `slots`-entry u64 table staged

@@ -1,15 +1,27 @@
-"""world_size-2 gloo tests of the island exchange and the brute-force rank
-split (the N > 1 path), on CPU tensors with stand-in runners."""
+"""world_size-2 gloo tests of the island model (the N > 1 path) on CPU.
+
+The real runners of vrpms_amd.runners (SARunner, GARunner) are driven
+through vrpms_amd.islands with oracle.standin.StandInContext in place of the
+GPU context: the same exchange code path as on the MI355X node with the
+fallback communicator (library-format messages all-gathered by
+torch.distributed), every pool operation restated by oracle/pool.py.  The
+expected migrants are recomputed from every rank's pre-exchange state.
+"""
 import math
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from vrpms_amd import islands
+from oracle import pool as opool
+from oracle.standin import StandInContext
+from vrpms_amd import islands, runners, synth
+
+M64 = (1 << 64) - 1
 
 
 def _free_port():
@@ -20,29 +32,16 @@ def _free_port():
     return p
 
 
-class FakeRunner:
-    """Keys are sums of the tour (so different ranks hold different elites)."""
+def _u64(t):
+    return [int(x) & M64 for x in t.reshape(-1).tolist()]
 
-    def __init__(self, rank, n=6, members=5):
-        g = torch.Generator().manual_seed(100 + rank)
-        self.n = n
-        self.tours = torch.stack([torch.randperm(n, generator=g) + 1 for _ in range(members)]).to(torch.int16)
-        self.keys = (torch.arange(members, dtype=torch.int64) * 10 + rank * 3 + 1)
-        self.injected = None
 
-    def elites(self, E):
-        order = torch.argsort(self.keys, stable=True)[:E]
-        return self.tours[order].clone(), self.keys[order].clone()
+def _inst():
+    return synth.cvrp(12, 3, seed=5, slack=1.0)
 
-    def inject(self, tours, keys):
-        self.injected = (tours.clone(), keys.clone())
 
-    def epoch(self):
-        pass
-
-    def best(self):
-        i = int(torch.argmin(self.keys))
-        return int(self.keys[i]), self.tours[i]
+def _snap(tours, keys):
+    return tours.reshape(-1, tours.shape[-1]).tolist(), _u64(keys)
 
 
 def _worker(rank, world, port, q):
@@ -50,38 +49,79 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        r = FakeRunner(rank)
-        bk = islands.exchange(r, E=3)
-        res = {"keys": bk.tolist(), "inj": r.injected[1].tolist(),
-               "tours": r.injected[0].tolist()}
-        # brute-force split: bf over [lo, hi) of 5! with key = (rank * 7919) % 113
+        inst = _inst()
+        ctx = StandInContext(inst)
+        res = {}
+        # SA chains: elites from the bests, migrants restart the worst chains
+        r = runners.SARunner(ctx, inst.n, chains=6, seed=40 + rank, total_steps=60,
+                             steps_per_epoch=10, durations=inst.durations)
+        r.epoch()
+        res["sa_src"], res["sa_dst"] = _snap(*r.src()), _snap(*r.dst())
+        islands.exchange(r, E=3)
+        res["sa_after"] = _snap(*r.dst())
+        # GA islands: migrants take the worst slots, islands stay sorted
+        g = runners.GARunner(ctx, inst.n, islands=2, pop=6, seed=70 + rank, gens_per_epoch=2)
+        g.epoch()
+        res["ga_src"] = _snap(*g.src())
+        islands.exchange(g, E=3)
+        res["ga_after"] = _snap(*g.dst())
+        # the global best is identical on every rank
+        res["gb"] = islands.global_best(r)
+
+        # brute-force split: bf over [lo, hi) of 5! with key = (x * 7919) % 113
         def bf_fn(lo, hi):
             return min(((x * 7919) % 113, x) for x in range(lo, hi))
         res["bf"] = islands.bf_distributed(bf_fn, 5)
-        k, t = islands.global_best(int(r.keys.min()) + 1000 * rank, r.tours[0].tolist(), r.n)
-        res["gb"] = (k, t)
+        # a fixed epoch count: every rank enters the same collectives
+        r2 = runners.SARunner(ctx, inst.n, chains=4, seed=90 + rank, total_steps=40,
+                              steps_per_epoch=5, durations=inst.durations)
+        res["fixed"] = islands.run_fixed(r2, epochs=8, exchange_every=4, E=2)[0]
+        res["fixed_best"] = islands.global_best(r2)
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
 
 
-def test_exchange_and_bf_split_world2():
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
+def _expected(srcs, dsts, E, n, mode, groups=1):
+    """oracle/pool.py: pack every rank's src, merge, inject into each dst."""
+    msgs = b"".join(opool.island_pack(t, k, E, n) for t, k in srcs)
+    mt, mk = opool.island_merge(msgs, len(srcs), E, n)
+    return [opool.pool_inject(t, k, mode, mt, mk, groups) for t, k in dsts], mk
+
+
+def test_island_exchange_world2_real_runners():
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [mpc.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    out = dict(q.get(timeout=120) for _ in procs)
+    out = dict(q.get(timeout=300) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # rank 0 keys 1, 11, 21 ... ; rank 1 keys 4, 14, 24 -> global best three: 1, 4, 11
-    assert out[0]["keys"] == [1, 4, 11] == out[1]["keys"]
-    assert out[0]["tours"] == out[1]["tours"]          # identical merge on every rank
-    want = min(((x * 7919) % 113, x) for x in range(math.factorial(5)))
-    assert out[0]["bf"] == out[1]["bf"] == want
-    assert out[0]["gb"] == out[1]["gb"] and out[0]["gb"][0] == 1
+    n = _inst().n
+    # SA: WORST injection of the global 3 best of both ranks' bests
+    want, mk = _expected([out[r]["sa_src"] for r in (0, 1)], [out[r]["sa_dst"] for r in (0, 1)],
+                         3, n, opool.INJECT_WORST)
+    for r in (0, 1):
+        assert [list(x) for x in out[r]["sa_after"][0]] == want[r][0]
+        assert out[r]["sa_after"][1] == want[r][1]
+    assert mk == sorted(mk)
+    # GA: SORTED injection, both islands re-sorted
+    want, _ = _expected([out[r]["ga_src"] for r in (0, 1)], [out[r]["ga_src"] for r in (0, 1)],
+                        3, n, opool.INJECT_SORTED, groups=2)
+    for r in (0, 1):
+        assert [list(x) for x in out[r]["ga_after"][0]] == want[r][0]
+        assert out[r]["ga_after"][1] == want[r][1]
+        ks = out[r]["ga_after"][1]
+        assert ks[:6] == sorted(ks[:6]) and ks[6:] == sorted(ks[6:])
+    assert out[0]["gb"] == out[1]["gb"]
+    assert out[0]["gb"][0] == min(min(out[r]["sa_after"][1] + out[r]["sa_src"][1]) for r in (0, 1))
+    want_bf = min(((x * 7919) % 113, x) for x in range(math.factorial(5)))
+    assert out[0]["bf"] == out[1]["bf"] == want_bf
+    assert out[0]["fixed"] == out[1]["fixed"] == 2
+    assert out[0]["fixed_best"] == out[1]["fixed_best"]
 
 
 @pytest.mark.parametrize("n,world", [(5, 2), (7, 3), (10, 8)])
@@ -91,63 +131,41 @@ def test_bf_rank_ranges_partition(n, world):
     assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
 
 
-def test_select_global_orders_as_uint64():
-    keys = torch.tensor([5, -1, 3, 3], dtype=torch.int64)   # -1 is UINT64_MAX
-    tours = torch.arange(8, dtype=torch.int16).reshape(4, 2)
-    t, k = islands.select_global(tours, keys, 3)
-    assert k.tolist() == [3, 3, 5]
-    assert t[:, 0].tolist() == [4, 6, 0]
+def test_merge_orders_as_uint64_then_rank_then_position():
+    n, E = 2, 3
+    a = opool.island_pack([[1, 2], [2, 1], [1, 2]], [5, M64, 3], E, n)   # M64 sorts last
+    b = opool.island_pack([[2, 1], [1, 2], [2, 1]], [3, 7, 9], E, n)
+    t, k = opool.island_merge(a + b, 2, E, n)
+    assert k == [3, 3, 5]
+    assert t == [[1, 2], [2, 1], [1, 2]]      # rank 0's 3 before rank 1's 3
 
 
-class CountingRunner(FakeRunner):
-    """Epochs lower one member's key, so migrations carry changing elites."""
-
-    def __init__(self, rank):
-        super().__init__(rank)
-        self.epochs = 0
-        self.log = []
-
-    def epoch(self):
-        self.epochs += 1
-        self.keys[self.epochs % self.keys.shape[0]] -= 1
-
-    def inject(self, tours, keys):
-        super().inject(tours, keys)
-        self.log.append(keys.tolist())
-
-
-def _fixed_worker(rank, world, port, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        r = CountingRunner(rank)
-        n_ex, t_ex = islands.run_fixed(r, epochs=12, exchange_every=4, E=2)
-        q.put((rank, {"n_ex": n_ex, "epochs": r.epochs, "log": r.log, "t_ex": t_ex}))
-    finally:
-        dist.destroy_process_group()
-
-
-def test_run_fixed_world2_same_collectives_and_merges():
-    """The bench's island leg (cfg 4) at N > 1: a fixed epoch count, so every
-    rank enters the same number of all-gathers and injects identical elites."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_fixed_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    out = dict(q.get(timeout=120) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    assert out[0]["n_ex"] == out[1]["n_ex"] == 3
-    assert out[0]["epochs"] == out[1]["epochs"] == 12
-    assert out[0]["log"] == out[1]["log"] and len(out[0]["log"]) == 3
-    assert all(k == sorted(k) for k in out[0]["log"])
+def test_pool_inject_modes():
+    tours = [[1, 2], [2, 1], [1, 2], [2, 1]]
+    keys = [9, 4, 9, 1]
+    t, k = opool.pool_inject(tours, keys, opool.INJECT_WORST, [[7, 7], [8, 8]], [2, 3])
+    assert k == [2, 4, 3, 1]                  # the two 9s (lowest index first) replaced
+    t, k = opool.pool_inject(tours, keys, opool.INJECT_BETTER, [[7, 7], [8, 8]], [2, 5])
+    assert k == [2, 4, 9, 1] and t[0] == [7, 7]
+    t, k = opool.pool_inject(tours, [1, 4, 2, 6], opool.INJECT_SORTED, [[7, 7], [8, 8]], [0, 3],
+                             groups=2)
+    assert k == [0, 1, 2, 3] and t[0] == [7, 7] and t[3] == [8, 8]
 
 
 def test_run_fixed_single_rank_injects_locally():
-    r = CountingRunner(0)
-    n_ex, _ = islands.run_fixed(r, epochs=10, exchange_every=5, E=2)
-    assert n_ex == 2 and len(r.log) == 2 and r.epochs == 10
+    inst = _inst()
+    ctx = StandInContext(inst)
+    r = runners.SARunner(ctx, inst.n, chains=4, seed=3, total_steps=20, steps_per_epoch=5,
+                         durations=inst.durations)
+    n_ex, _ = islands.run_fixed(r, epochs=4, exchange_every=2, E=2)
+    assert n_ex == 2 and r.step == 20
+    keys = _u64(r.cur_key)
+    assert all(k < M64 for k in keys)
+
+
+def test_philox_tours_are_permutations():
+    rows = [opool.philox_tour(13, 99, r, 2) for r in range(20)]
+    assert all(sorted(t) == list(range(1, 14)) for t in rows)
+    assert len({tuple(t) for t in rows}) == 20
+    assert opool.philox_tour(1, 5, 0) == [1] and opool.philox_tour(0, 5, 0) == []
+    assert np.all(np.array(opool.philox_tour(13, 99, 4, 2)) == np.array(rows[4]))

@@ -31,6 +31,9 @@ OPT_WORDS_ILP = 4
 OPT_WORDS_LOOKAHEAD = 5
 OBJ_SUM = 0
 OBJ_MAX = 1
+INJECT_WORST = 0
+INJECT_SORTED = 1
+INJECT_BETTER = 2
 
 _c = ctypes
 _vp = _c.c_void_p
@@ -54,6 +57,11 @@ class AcoParams(ctypes.Structure):
                 ("iter", _u64)]
 
 
+class Pool(ctypes.Structure):
+    _fields_ = [("tours", ctypes.c_void_p), ("keys", ctypes.c_void_p), ("count", _i32),
+                ("n", _i32), ("groups", _i32)]
+
+
 # name -> (restype, argtypes); mirrors include/vrpms.h one-for-one.
 SIGNATURES = {
     "vrpms_version": (_c.c_int, []),
@@ -72,12 +80,23 @@ SIGNATURES = {
     "vrpms_ga_generation": (_c.c_int, [_vp, _c.POINTER(GaParams), _vp, _vp, _i32, _vp]),
     "vrpms_aco_init": (_c.c_int, [_vp, _i32, _c.c_uint32, _vp, _vp, _vp]),
     "vrpms_aco_iteration": (_c.c_int, [_vp, _c.POINTER(AcoParams), _vp, _vp, _vp, _vp, _vp,
-                                       _i32, _vp]),
+                                       _vp, _vp, _i32, _vp]),
     "vrpms_bf_run": (_c.c_int, [_vp, _i32, _u64, _u64, _vp, _vp]),
     "vrpms_probe_lds_gather": (_c.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp]),
     "vrpms_probe_l2_gather": (_c.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp]),
     "vrpms_tsp_batch_sa": (_c.c_int, [_vp, _vp, _i32, _i32, _c.POINTER(SaParams), _vp, _vp,
                                       _vp]),
+    "vrpms_random_tours": (_c.c_int, [_vp, _i64, _i32, _i64, _i32, _u64, _c.c_uint32, _vp, _vp]),
+    "vrpms_pool_elites": (_c.c_int, [_vp, _c.POINTER(Pool), _i32, _vp, _vp, _vp]),
+    "vrpms_pool_inject": (_c.c_int, [_vp, _c.POINTER(Pool), _i32, _vp, _vp, _i32, _vp]),
+    "vrpms_island_msg_bytes": (_i64, [_i32, _i32]),
+    "vrpms_island_pack": (_c.c_int, [_vp, _c.POINTER(Pool), _i32, _vp, _vp]),
+    "vrpms_island_merge": (_c.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp]),
+    "vrpms_island_unique_id": (_c.c_int, [_vp]),
+    "vrpms_island_init": (_c.c_int, [_vp, _vp, _i32, _i32]),
+    "vrpms_island_world": (_c.c_int, [_vp]),
+    "vrpms_island_exchange": (_c.c_int, [_vp, _c.POINTER(Pool), _c.POINTER(Pool), _i32, _i32,
+                                         _vp]),
 }
 
 

@@ -13,7 +13,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libvrpms.so")
-SOURCES = ["capi.hip", "eval.hip", "eval_staged.hip", "eval_words.hip", "search.hip", "probe.hip"]
+SOURCES = ["capi.hip", "eval.hip", "eval_staged.hip", "eval_words.hip", "search.hip", "probe.hip",
+           "pool.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "--offload-arch=gfx950",
          "-ffp-contract=off", "-Wall", "-Werror"]
@@ -32,7 +33,9 @@ def _newest_input():
 def build_library(force: bool = False, verbose: bool = False) -> str:
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _newest_input():
         return LIB
-    cmd = [HIPCC, *FLAGS, "-o", LIB + ".tmp", *sources()]
+    # RCCL (island all-gather): NEEDED librccl.so.1 binds to the copy torch
+    # already loaded (same SONAME), like libamdhip64.so.7
+    cmd = [HIPCC, *FLAGS, "-o", LIB + ".tmp", *sources(), "-L/opt/rocm/lib", "-lrccl"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     res = subprocess.run(cmd, capture_output=True, text=True)

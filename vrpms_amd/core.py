@@ -9,7 +9,8 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import CVRP, OBJ_MAX, OBJ_SUM, TSP, VrpmsError, check  # noqa: F401
+from ._lib import (CVRP, INJECT_BETTER, INJECT_SORTED, INJECT_WORST, OBJ_MAX,  # noqa: F401
+                   OBJ_SUM, TSP, VrpmsError, check)
 
 
 def _torch():
@@ -235,7 +236,11 @@ class Context:
         return tau, eta
 
     def aco_iteration(self, tau, eta, ants: int, seed: int, it: int, evap_shift: int = 3,
-                      tau_min: int = 1 << 10, tau_max: int = 1 << 30):
+                      tau_min: int = 1 << 10, tau_max: int = 1 << 30, best_tours=None,
+                      best_keys=None):
+        """One ACO iteration -> (tours, keys, iteration-best (key, ant) per
+        colony); `best_tours`/`best_keys` (per colony) are updated in place
+        on the device when given."""
         torch = _torch()
         colonies = tau.shape[0]
         n = self.N - 1
@@ -244,9 +249,11 @@ class Context:
         ib = torch.empty((colonies, 2), dtype=torch.int64, device=self.dev)
         p = _lib.AcoParams(colonies, ants, evap_shift, tau_min, tau_max,
                            int(seed) & (2**64 - 1), int(it))
+        ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
         check(self.lib.vrpms_aco_iteration(self._ctx, ctypes.byref(p), tau.data_ptr(),
                                            eta.data_ptr(), tours.data_ptr(), keys.data_ptr(),
-                                           ib.data_ptr(), n, self.stream()))
+                                           ib.data_ptr(), ptr(best_tours), ptr(best_keys), n,
+                                           self.stream()))
         return tours, keys, ib
 
     def bf_run(self, n: int, rank_begin: int, rank_end: int):
@@ -271,6 +278,89 @@ class Context:
         check(self.lib.vrpms_tsp_batch_sa(self._ctx, mats.data_ptr(), R, N, ctypes.byref(p),
                                           tours.data_ptr(), keys.data_ptr(), self.stream()))
         return tours, keys
+
+    # -- populations and the island model (pool.hip) ---------------------------
+    def random_tours(self, count: int, n: int, seed: int, stream_id: int = 0, ld: int | None = None,
+                     dtype=None):
+        """Philox Fisher-Yates permutations of 1..n (vrpms_random_tours) as
+        int16 (default) or uint8 rows of `ld` elements."""
+        torch = _torch()
+        dtype = torch.int16 if dtype is None else dtype
+        ld = n if ld is None else int(ld)
+        out = torch.zeros((int(count), ld), dtype=dtype, device=self.dev)
+        check(self.lib.vrpms_random_tours(self._ctx, int(count), int(n), ld, perm_dtype_bytes(out),
+                                          int(seed) & (2**64 - 1), int(stream_id) & 0xFFFFFFFF,
+                                          out.data_ptr(), self.stream()))
+        return out
+
+    @staticmethod
+    def pool(tours, keys, groups: int = 1):
+        """vrpms_pool over an int16 [count][n] (or [g][p][n]) tour tensor and its keys."""
+        count = keys.numel()
+        n = tours.shape[-1]
+        if tours.numel() != count * n or not tours.is_contiguous() or not keys.is_contiguous():
+            raise ValueError("pool: tours must be a contiguous [count][n] tensor matching keys")
+        return _lib.Pool(tours.data_ptr(), keys.data_ptr(), count, n, int(groups))
+
+    def pool_elites(self, tours, keys, E: int):
+        """The E best rows by (key, index) -> (tours [E][n], keys [E])."""
+        torch = _torch()
+        n = tours.shape[-1]
+        t = torch.empty((E, n), dtype=torch.int16, device=self.dev)
+        k = torch.empty(E, dtype=torch.int64, device=self.dev)
+        p = self.pool(tours, keys)
+        check(self.lib.vrpms_pool_elites(self._ctx, ctypes.byref(p), int(E), t.data_ptr(),
+                                         k.data_ptr(), self.stream()))
+        return t, k
+
+    def pool_inject(self, tours, keys, mode: int, mig_tours, mig_keys, groups: int = 1):
+        p = self.pool(tours, keys, groups)
+        mt = mig_tours.to(_torch().int16).contiguous()
+        mk = mig_keys.contiguous()
+        check(self.lib.vrpms_pool_inject(self._ctx, ctypes.byref(p), int(mode), mt.data_ptr(),
+                                         mk.data_ptr(), int(mk.numel()), self.stream()))
+
+    def island_msg_bytes(self, E: int, n: int) -> int:
+        return int(self.lib.vrpms_island_msg_bytes(int(E), int(n)))
+
+    def island_pack(self, tours, keys, E: int):
+        """The E elites as one island message (uint8 device tensor)."""
+        torch = _torch()
+        n = tours.shape[-1]
+        msg = torch.empty(self.island_msg_bytes(E, n), dtype=torch.uint8, device=self.dev)
+        p = self.pool(tours, keys)
+        check(self.lib.vrpms_island_pack(self._ctx, ctypes.byref(p), int(E), msg.data_ptr(),
+                                         self.stream()))
+        return msg
+
+    def island_merge(self, msgs, world: int, E: int, n: int):
+        """The E best of `world` gathered messages -> (tours [E][n], keys [E])."""
+        torch = _torch()
+        msgs = msgs.to(self.dev).contiguous()
+        t = torch.empty((E, n), dtype=torch.int16, device=self.dev)
+        k = torch.empty(E, dtype=torch.int64, device=self.dev)
+        check(self.lib.vrpms_island_merge(self._ctx, msgs.data_ptr(), int(world), int(E), int(n),
+                                          t.data_ptr(), k.data_ptr(), self.stream()))
+        return t, k
+
+    def island_unique_id(self) -> bytes:
+        buf = ctypes.create_string_buffer(128)
+        check(self.lib.vrpms_island_unique_id(buf))
+        return buf.raw
+
+    def island_init(self, unique_id: bytes, rank: int, world: int):
+        buf = ctypes.create_string_buffer(bytes(unique_id), 128)
+        check(self.lib.vrpms_island_init(self._ctx, buf, int(rank), int(world)))
+
+    def island_world(self) -> int:
+        return int(self.lib.vrpms_island_world(self._ctx))
+
+    def island_exchange(self, src, dst, mode: int, E: int, groups: int = 1):
+        """vrpms_island_exchange: src/dst are (tours, keys) pairs."""
+        ps = self.pool(*src)
+        pd = self.pool(*dst, groups=groups)
+        check(self.lib.vrpms_island_exchange(self._ctx, ctypes.byref(ps), ctypes.byref(pd),
+                                             int(mode), int(E), self.stream()))
 
     def probe_lds_gather(self, slots: int = 101 * 101, iters: int = 4096, blocks: int | None = None,
                          reps: int = 5):

@@ -198,6 +198,7 @@ int vrpms_ctx_create(int device, vrpms_ctx** out) {
 int vrpms_ctx_destroy(vrpms_ctx* ctx) {
   if (!ctx) return VRPMS_OK;
   (void)hipSetDevice(ctx->device); (void)hipDeviceSynchronize();
+  island_release(ctx);
   free_instance(ctx->inst);
   (void)hipFree(ctx->d_stats);
   (void)hipFree(ctx->d_scratch);

@@ -57,12 +57,17 @@ struct vrpms_ctx {
   uint64_t* d_scratch = nullptr;  // small reduction scratch
   void* search_scratch = nullptr;  // GA children / BF block results (grown on demand)
   size_t search_scratch_bytes = 0;
+  void* pool_scratch = nullptr;    // elite selection / island messages (pool.hip, grown on demand)
+  size_t pool_scratch_bytes = 0;
+  void* comm = nullptr;            // ncclComm_t of the island model (vrpms_island_init)
+  int comm_rank = 0, comm_world = 1;
 };
 
 namespace vrpms {
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);
 int hip_fail(hipError_t e, const char* what);
+void island_release(vrpms_ctx* ctx);  // pool.hip: communicator + pool scratch
 }  // namespace vrpms
 
 #define VRPMS_HIP(call)                                               \

@@ -29,6 +29,7 @@
 #include "ctx.hpp"
 #include "split.hpp"
 #include "tour.hpp"
+#include "words.hpp"
 
 namespace vrpms {
 
@@ -398,7 +399,8 @@ struct GaBreedArgs {
   uint64_t gen;
   const uint16_t* pop_tours;  // [islands][pop][n]
   const uint64_t* pop_keys;   // [islands][pop]
-  uint16_t* child;            // [islands][pop][n]
+  uint16_t* child;            // rows [islands][pop][n]            (WORDS == false)
+  uint32_t* child_w;          // words [ceil(n/4)][islands * pop]  (WORDS == true)
 };
 
 // Tournament of two: the lower (key, index) wins.
@@ -408,6 +410,12 @@ VRPMS_DEV int tourney(const uint64_t* keys, int pop, uint32_t r0, uint32_t r1) {
   return (ky < kx || (ky == kx && y < x)) ? y : x;
 }
 
+// One child per wavefront.  WORDS (n <= 255): the child is assembled in a
+// wave-private LDS byte buffer and leaves as ceil(n/4) words of the
+// word-interleaved layout, which eval_cvrp_words2 -- the headline scoring
+// kernel -- reads with one coalesced wave load per word.  Otherwise the
+// child is written straight into its uint16 row.
+template <bool WORDS>
 __global__ __launch_bounds__(256) void ga_breed_kernel(GaBreedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = threadIdx.x >> 6, lane = lane_id();
@@ -415,78 +423,97 @@ __global__ __launch_bounds__(256) void ga_breed_kernel(GaBreedArgs a) {
   const int n = a.n;
   const uint32_t words = ((uint32_t)a.N + 31u) / 32u;
   uint32_t* used = reinterpret_cast<uint32_t*>(smem) + wave * words;
-  if (gid >= (int64_t)a.islands * a.pop) return;
+  uint8_t* cbuf = smem + ((4u * words * 4u + 15u) & ~15u) + wave * 256;
+  const int64_t members = (int64_t)a.islands * a.pop;
+  if (gid >= members) return;
   const int island = (int)(gid / a.pop), child = (int)(gid % a.pop);
   const uint16_t* P = a.pop_tours + (int64_t)island * a.pop * n;
   const uint64_t* Kk = a.pop_keys + (int64_t)island * a.pop;
   uint16_t* out = a.child + gid * n;
+  auto put = [&](int q, uint32_t g) {
+    if constexpr (WORDS) cbuf[q] = (uint8_t)g;
+    else out[q] = (uint16_t)g;
+  };
+  auto get = [&](int q) -> uint32_t {
+    if constexpr (WORDS) return cbuf[q];
+    else return out[q];
+  };
   const uint32_t cid = (uint32_t)(island * a.pop + child);
   const u32x4 r = philox((uint32_t)a.gen, (uint32_t)(a.gen >> 32), cid, 0u, a.seed_lo, a.seed_hi);
   const u32x4 r2 = philox((uint32_t)a.gen, (uint32_t)(a.gen >> 32), cid, 1u, a.seed_lo, a.seed_hi);
   const int pa = tourney(Kk, a.pop, r.x, r.y), pb = tourney(Kk, a.pop, r.z, r.w);
   const uint16_t* A = P + (int64_t)pa * n;
   const uint16_t* B = P + (int64_t)pb * n;
+  if constexpr (WORDS) {
+    for (int q = n + lane; q < 256; q += 64) cbuf[q] = 0;  // zero pad of the last word
+  }
   if (n < 2) {
-    for (int q = lane; q < n; q += 64) out[q] = A[q];
-    return;
-  }
-  // OX1: child[lo..hi] = A[lo..hi]; the rest, in order from position hi+1
-  // (wrapping), are B's genes from B[hi+1] onwards (wrapping) not yet used.
-  int lo = (int)(r2.x % (uint32_t)n), hi = (int)(r2.y % (uint32_t)n);
-  if (lo > hi) {
-    const int t = lo;
-    lo = hi;
-    hi = t;
-  }
-  for (uint32_t w = lane; w < words; w += 64) used[w] = 0u;
-  wave_sync();
-  for (int q = lo + lane; q <= hi; q += 64) {
-    const uint32_t g = A[q];
-    out[q] = (uint16_t)g;
-    atomicOr(&used[g >> 5], 1u << (g & 31u));
-  }
-  wave_sync();
-  const int seg = hi - lo + 1, rest = n - seg;
-  int filled = 0;
-  for (int base = 0; base < n; base += 64) {
-    const int q = base + lane;
-    uint32_t g = 0;
-    bool keep = false;
-    if (q < n) {
-      g = B[(hi + 1 + q) % n];
-      keep = ((used[g >> 5] >> (g & 31u)) & 1u) == 0u;
+    for (int q = lane; q < n; q += 64) put(q, A[q]);
+  } else {
+    // OX1: child[lo..hi] = A[lo..hi]; the rest, in order from position hi+1
+    // (wrapping), are B's genes from B[hi+1] onwards (wrapping) not yet used.
+    int lo = (int)(r2.x % (uint32_t)n), hi = (int)(r2.y % (uint32_t)n);
+    if (lo > hi) {
+      const int t = lo;
+      lo = hi;
+      hi = t;
     }
-    const uint64_t ball = __ballot(keep);
-    const int before = __popcll(ball & ((1ull << lane) - 1ull));
-    if (keep) {
-      const int slot = filled + before;  // slot-th free position after hi
-      if (slot < rest) out[(hi + 1 + slot) % n] = (uint16_t)g;
+    for (uint32_t w = lane; w < words; w += 64) used[w] = 0u;
+    wave_sync();
+    for (int q = lo + lane; q <= hi; q += 64) {
+      const uint32_t g = A[q];
+      put(q, g);
+      atomicOr(&used[g >> 5], 1u << (g & 31u));
     }
-    filled += __popcll(ball);
-  }
-  wave_sync();
-  // mutation: one sampled move, applied by lane 0 (rare, O(n))
-  if (r2.z < a.pmut && lane == 0) {
-    const Move m = decode_move(r2.w, r.x ^ r2.x, r.y ^ r2.y, n);
-    if (m.typ == kMoveSwap) {
-      const uint16_t t = out[m.i];
-      out[m.i] = out[m.j];
-      out[m.j] = t;
-    } else if (m.typ == kMove2Opt) {
-      for (int x = m.i, y = m.j; x < y; ++x, --y) {
-        const uint16_t t = out[x];
-        out[x] = out[y];
-        out[y] = t;
+    wave_sync();
+    const int seg = hi - lo + 1, rest = n - seg;
+    int filled = 0;
+    for (int base = 0; base < n; base += 64) {
+      const int q = base + lane;
+      uint32_t g = 0;
+      bool keep = false;
+      if (q < n) {
+        g = B[(hi + 1 + q) % n];
+        keep = ((used[g >> 5] >> (g & 31u)) & 1u) == 0u;
       }
-    } else if (m.i < m.j) {
-      const uint16_t v = out[m.i];
-      for (int x = m.i; x < m.j; ++x) out[x] = out[x + 1];
-      out[m.j] = v;
-    } else {
-      const uint16_t v = out[m.i];
-      for (int x = m.i; x > m.j; --x) out[x] = out[x - 1];
-      out[m.j] = v;
+      const uint64_t ball = __ballot(keep);
+      const int before = __popcll(ball & ((1ull << lane) - 1ull));
+      if (keep) {
+        const int slot = filled + before;  // slot-th free position after hi
+        if (slot < rest) put((hi + 1 + slot) % n, g);
+      }
+      filled += __popcll(ball);
     }
+    wave_sync();
+    // mutation: one sampled move, applied by lane 0 (rare, O(n))
+    if (r2.z < a.pmut && lane == 0) {
+      const Move m = decode_move(r2.w, r.x ^ r2.x, r.y ^ r2.y, n);
+      if (m.typ == kMoveSwap) {
+        const uint32_t t = get(m.i);
+        put(m.i, get(m.j));
+        put(m.j, t);
+      } else if (m.typ == kMove2Opt) {
+        for (int x = m.i, y = m.j; x < y; ++x, --y) {
+          const uint32_t t = get(x);
+          put(x, get(y));
+          put(y, t);
+        }
+      } else if (m.i < m.j) {
+        const uint32_t v = get(m.i);
+        for (int x = m.i; x < m.j; ++x) put(x, get(x + 1));
+        put(m.j, v);
+      } else {
+        const uint32_t v = get(m.i);
+        for (int x = m.i; x > m.j; --x) put(x, get(x - 1));
+        put(m.j, v);
+      }
+    }
+  }
+  if constexpr (WORDS) {
+    wave_sync();
+    const int nw = (n + 3) >> 2;
+    for (int w = lane; w < nw; w += 64)
+      a.child_w[(int64_t)w * members + gid] = reinterpret_cast<const uint32_t*>(cbuf)[w];
   }
 }
 
@@ -494,7 +521,8 @@ struct GaSelectArgs {
   int islands, pop, n;
   const uint16_t* pop_tours;   // [islands][pop][n]
   const uint64_t* pop_keys;
-  const uint16_t* child;       // [islands][pop][n]
+  const uint16_t* child;       // rows [islands][pop][n]            (WORDS == false)
+  const uint32_t* child_w;     // words [ceil(n/4)][islands * pop]  (WORDS == true)
   const uint64_t* child_keys;
   uint16_t* out_tours;         // [islands][pop][n]
   uint64_t* out_keys;
@@ -502,6 +530,7 @@ struct GaSelectArgs {
 
 // (mu + lambda): the pop best of parents (index i) and children (index pop + i)
 // by (key, index); bitonic sort over the next power of two >= 2 * pop.
+template <bool WORDS>
 __global__ __launch_bounds__(1024) void ga_select_kernel(GaSelectArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint64_t* sk = reinterpret_cast<uint64_t*>(smem);
@@ -537,13 +566,21 @@ __global__ __launch_bounds__(1024) void ga_select_kernel(GaSelectArgs a) {
     }
   }
   const uint16_t* P = a.pop_tours + (int64_t)island * pop * n;
-  const uint16_t* Cc = a.child + (int64_t)island * pop * n;
+  const int64_t members = (int64_t)a.islands * pop;
   uint16_t* O = a.out_tours + (int64_t)island * pop * n;
   for (int i = threadIdx.x; i < pop; i += blockDim.x) a.out_keys[(int64_t)island * pop + i] = sk[i];
   for (int64_t e = threadIdx.x; e < (int64_t)pop * n; e += blockDim.x) {
     const int i = (int)(e / n), q = (int)(e % n);
     const uint32_t src = si[i];
-    O[e] = src < (uint32_t)pop ? P[(int64_t)src * n + q] : Cc[(int64_t)(src - pop) * n + q];
+    uint32_t g;
+    if (src < (uint32_t)pop) {
+      g = P[(int64_t)src * n + q];
+    } else {
+      const int64_t c = (int64_t)island * pop + (src - pop);
+      if constexpr (WORDS) g = (a.child_w[(int64_t)(q >> 2) * members + c] >> (8 * (q & 3))) & 0xffu;
+      else g = a.child[c * n + q];
+    }
+    O[e] = (uint16_t)g;
   }
 }
 
@@ -557,11 +594,16 @@ struct AcoArgs {
   const uint32_t* tau;   // [colonies][N][N]
   const uint32_t* eta;   // [N][N] (static part of the weight)
   uint16_t* tours;       // [colonies][ants][n]
+  uint32_t* words;       // WORDS: the same tours, word-interleaved [ceil(n/4)][colonies * ants]
 };
 
 // Ant: starts at node 0; each step picks j among unvisited customers with
 // probability w_j / sum w, w_j = (tau[i][j] >> 8) * eta[i][j] (uint64, exact),
 // r = philox64 % sum, the smallest j (index order) whose prefix sum exceeds r.
+// WORDS (n <= 255): the ant's tour is also kept in a wave-private LDS byte
+// buffer and written out in the word-interleaved layout, so the colony is
+// scored by eval_cvrp_words2 (the headline kernel).
+template <bool WORDS>
 __global__ __launch_bounds__(256) void aco_construct_kernel(AcoArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = threadIdx.x >> 6, lane = lane_id();
@@ -569,7 +611,12 @@ __global__ __launch_bounds__(256) void aco_construct_kernel(AcoArgs a) {
   const int N = a.N, n = a.n;
   const uint32_t words = ((uint32_t)N + 31u) / 32u;
   uint32_t* vis = reinterpret_cast<uint32_t*>(smem) + wave * words;
-  if (gid >= (int64_t)a.colonies * a.ants) return;
+  uint8_t* tbuf = smem + ((4u * words * 4u + 15u) & ~15u) + wave * 256;
+  const int64_t total_ants = (int64_t)a.colonies * a.ants;
+  if (gid >= total_ants) return;
+  if constexpr (WORDS) {
+    for (int q = n + lane; q < 256; q += 64) tbuf[q] = 0;
+  }
   const int colony = (int)(gid / a.ants), ant = (int)(gid % a.ants);
   const uint32_t* T = a.tau + (int64_t)colony * N * N;
   uint16_t* out = a.tours + gid * n;
@@ -622,10 +669,16 @@ __global__ __launch_bounds__(256) void aco_construct_kernel(AcoArgs a) {
     }
     if (lane == 0) {
       out[s] = (uint16_t)pick;
+      if constexpr (WORDS) tbuf[s] = (uint8_t)pick;
       atomicOr(&vis[pick >> 5], 1u << (pick & 31u));
     }
     wave_sync();
     cur = pick;
+  }
+  if constexpr (WORDS) {
+    const int nw = (n + 3) >> 2;
+    for (int w = lane; w < nw; w += 64)
+      a.words[(int64_t)w * total_ants + gid] = reinterpret_cast<const uint32_t*>(tbuf)[w];
   }
 }
 
@@ -662,6 +715,19 @@ __global__ void aco_deposit_kernel(AcoUpdateArgs a) {
     const uint32_t old = atomicAdd(&T[idx], dep);
     (void)old;
   }
+}
+
+// colony c's best-so-far <- its iteration-best ant when strictly better
+__global__ void aco_track_best_kernel(const uint16_t* __restrict__ tours, int ants, int n,
+                                      const uint64_t* __restrict__ ib, uint16_t* best_tours,
+                                      uint64_t* best_keys) {
+  const int c = blockIdx.x;
+  const uint64_t key = ib[2 * c];
+  if (!(key < best_keys[c])) return;  // block-uniform
+  const uint16_t* t = tours + ((int64_t)c * ants + (int64_t)ib[2 * c + 1]) * n;
+  for (int q = threadIdx.x; q < n; q += blockDim.x) best_tours[(int64_t)c * n + q] = t[q];
+  __syncthreads();
+  if (threadIdx.x == 0) best_keys[c] = key;
 }
 
 // per-colony argmin over ant keys -> ib[2c] = key, ib[2c+1] = ant
@@ -1044,34 +1110,72 @@ extern "C" int vrpms_ga_generation(vrpms_ctx* ctx, const vrpms_ga_params* p, uin
   hipStream_t s = (hipStream_t)stream;
   const int64_t members = (int64_t)p->islands * p->pop;
   const size_t tour_bytes = (size_t)members * n * 2;
-  const size_t need = 2 * tour_bytes + (size_t)members * 8 * 2 + 256;
+  // Children are scored by the headline kernel (eval_cvrp_words2) whenever
+  // its packed layout applies: the breed kernel then emits them in the
+  // word-interleaved layout directly.  Otherwise uint16 rows + vrpms_eval.
+  FastSplit f;
+  const bool words = n <= 255 && fast_split_params(ctx, n, &f);
+  const int nw = (n + 3) / 4;
+  const size_t child_bytes = words ? (size_t)nw * members * 4 : tour_bytes;
+  const size_t a16 = 255;
+  auto up = [&](size_t x) { return (x + a16) & ~a16; };
+  const size_t need = up(child_bytes) + up(tour_bytes) + 2 * up((size_t)members * 8);
   int err = VRPMS_OK;
   ensure_scratch(ctx, need, &err);
   if (err) return err;
   unsigned char* sp = static_cast<unsigned char*>(ctx->search_scratch);
-  uint16_t* child = reinterpret_cast<uint16_t*>(sp);
-  uint16_t* next = reinterpret_cast<uint16_t*>(sp + tour_bytes);
-  uint64_t* ckeys = reinterpret_cast<uint64_t*>(sp + 2 * tour_bytes);
-  uint64_t* nkeys = ckeys + members;
+  void* child = sp;
+  uint16_t* next = reinterpret_cast<uint16_t*>(sp + up(child_bytes));
+  uint64_t* ckeys = reinterpret_cast<uint64_t*>(sp + up(child_bytes) + up(tour_bytes));
+  uint64_t* nkeys = reinterpret_cast<uint64_t*>(reinterpret_cast<unsigned char*>(ckeys) +
+                                                up((size_t)members * 8));
+  int M = 1;
+  while (M < 2 * p->pop) M <<= 1;
+  const size_t lds_s = (size_t)M * 12;
+  const uint32_t bw = ((uint32_t)ctx->inst.N + 31u) / 32u;
+  const size_t lds_b = ((4 * (size_t)bw * 4 + 15) & ~(size_t)15) + (words ? 4 * 256 : 0);
+  if (lds_s > ctx->max_lds || lds_b > ctx->max_lds)
+    return fail(VRPMS_EINVAL, "vrpms_ga_generation: population too large for LDS");
+  auto breed = words ? ga_breed_kernel<true> : ga_breed_kernel<false>;
+  auto select = words ? ga_select_kernel<true> : ga_select_kernel<false>;
+  if (lds_b > 65536)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(breed),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_b);
+  if (lds_s > 65536)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(select),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_s);
+  // ping-pong between the caller's population and the scratch one: no copy
+  // per generation, one at the end when the result landed in scratch
+  uint16_t* src_t = d_pop;
+  uint64_t* src_k = d_keys;
+  uint16_t* dst_t = next;
+  uint64_t* dst_k = nkeys;
   for (int g = 0; g < p->generations; ++g) {
     const uint64_t gen = p->gen0 + (uint64_t)g;
-    GaBreedArgs b{p->islands, p->pop, n, ctx->inst.N, p->pmut, (uint32_t)p->seed, (uint32_t)(p->seed >> 32),
-                  gen, d_pop, d_keys, child};
-    const size_t lds_b = 4 * (((size_t)ctx->inst.N + 31) / 32) * 4;
-    ga_breed_kernel<<<(unsigned)((members + 3) / 4), 256, lds_b, s>>>(b);
+    GaBreedArgs b{p->islands, p->pop, n, ctx->inst.N, p->pmut, (uint32_t)p->seed,
+                  (uint32_t)(p->seed >> 32), gen, src_t, src_k,
+                  static_cast<uint16_t*>(child), static_cast<uint32_t*>(child)};
+    breed<<<(unsigned)((members + 3) / 4), 256, lds_b, s>>>(b);
     VRPMS_HIP(hipGetLastError());
-    int rc = vrpms_eval(ctx, child, 2, members, n, n, ckeys, nullptr, nullptr, nullptr, stream);
-    if (rc) return rc;
-    int M = 1;
-    while (M < 2 * p->pop) M <<= 1;
-    GaSelectArgs sa{p->islands, p->pop, n, d_pop, d_keys, child, ckeys, next, nkeys};
-    if ((size_t)M * 12 > 65536)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ga_select_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)((size_t)M * 12));
-    ga_select_kernel<<<p->islands, 1024, (size_t)M * 12, s>>>(sa);
+    if (words) {
+      WordsArgs w{f, static_cast<const uint32_t*>(child), members, n, ckeys, nullptr, nullptr,
+                  nullptr, members, 1u};
+      int rc = launch_words2(ctx, w, words2_ring(n), s);
+      if (rc) return rc;
+    } else {
+      int rc = vrpms_eval(ctx, child, 2, members, n, n, ckeys, nullptr, nullptr, nullptr, stream);
+      if (rc) return rc;
+    }
+    GaSelectArgs sa{p->islands, p->pop, n, src_t, src_k, static_cast<const uint16_t*>(child),
+                    static_cast<const uint32_t*>(child), ckeys, dst_t, dst_k};
+    select<<<p->islands, 1024, lds_s, s>>>(sa);
     VRPMS_HIP(hipGetLastError());
-    VRPMS_HIP(hipMemcpyAsync(d_pop, next, tour_bytes, hipMemcpyDeviceToDevice, s));
-    VRPMS_HIP(hipMemcpyAsync(d_keys, nkeys, (size_t)members * 8, hipMemcpyDeviceToDevice, s));
+    std::swap(src_t, dst_t);
+    std::swap(src_k, dst_k);
+  }
+  if (src_t != d_pop) {
+    VRPMS_HIP(hipMemcpyAsync(d_pop, src_t, tour_bytes, hipMemcpyDeviceToDevice, s));
+    VRPMS_HIP(hipMemcpyAsync(d_keys, src_k, (size_t)members * 8, hipMemcpyDeviceToDevice, s));
   }
   return VRPMS_OK;
 }
@@ -1081,7 +1185,8 @@ extern "C" int vrpms_aco_init(vrpms_ctx* ctx, int32_t colonies, uint32_t tau0, u
 
 extern "C" int vrpms_aco_iteration(vrpms_ctx* ctx, const vrpms_aco_params* p, uint32_t* d_tau,
                                    const uint32_t* d_eta, uint16_t* d_tours, uint64_t* d_keys,
-                                   uint64_t* d_iter_best, int32_t n, void* stream) {
+                                   uint64_t* d_iter_best, uint16_t* d_best_tours,
+                                   uint64_t* d_best_keys, int32_t n, void* stream) {
   if (!ctx || !p) return fail(VRPMS_EINVAL, "vrpms_aco_iteration: NULL ctx/params");
   if (!ctx->has_instance) return fail(VRPMS_ESTATE, "vrpms_aco_iteration: no instance loaded");
   const Instance& in = ctx->inst;
@@ -1096,14 +1201,35 @@ extern "C" int vrpms_aco_iteration(vrpms_ctx* ctx, const vrpms_aco_params* p, ui
   VRPMS_HIP(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
   const int64_t ants = (int64_t)p->colonies * p->ants;
+  FastSplit f;
+  const bool words = n <= 255 && fast_split_params(ctx, n, &f);
+  uint32_t* wbuf = nullptr;
+  if (words) {
+    int err = VRPMS_OK;
+    ensure_scratch(ctx, (size_t)((n + 3) / 4) * ants * 4, &err);
+    if (err) return err;
+    wbuf = static_cast<uint32_t*>(ctx->search_scratch);
+  }
   AcoArgs c{p->colonies, p->ants, n, in.N, (uint32_t)p->seed, (uint32_t)(p->seed >> 32), p->iter,
-            d_tau, d_eta, d_tours};
-  const size_t lds = 4 * (((size_t)in.N + 31) / 32) * 4;
-  aco_construct_kernel<<<(unsigned)((ants + 3) / 4), 256, lds, s>>>(c);
+            d_tau, d_eta, d_tours, wbuf};
+  const size_t lds = ((4 * (((size_t)in.N + 31) / 32) * 4 + 15) & ~(size_t)15) + (words ? 4 * 256 : 0);
+  if (words)
+    aco_construct_kernel<true><<<(unsigned)((ants + 3) / 4), 256, lds, s>>>(c);
+  else
+    aco_construct_kernel<false><<<(unsigned)((ants + 3) / 4), 256, lds, s>>>(c);
   VRPMS_HIP(hipGetLastError());
-  int rc = vrpms_eval(ctx, d_tours, 2, ants, n, n, d_keys, nullptr, nullptr, nullptr, stream);
-  if (rc) return rc;
+  if (words) {
+    WordsArgs w{f, wbuf, ants, n, d_keys, nullptr, nullptr, nullptr, ants, 1u};
+    int rc = launch_words2(ctx, w, words2_ring(n), s);
+    if (rc) return rc;
+  } else {
+    int rc = vrpms_eval(ctx, d_tours, 2, ants, n, n, d_keys, nullptr, nullptr, nullptr, stream);
+    if (rc) return rc;
+  }
   segment_argmin_kernel<<<p->colonies, 256, 0, s>>>(d_keys, p->ants, p->colonies, d_iter_best);
+  if (d_best_tours && d_best_keys)
+    aco_track_best_kernel<<<p->colonies, 128, 0, s>>>(d_tours, p->ants, n, d_iter_best,
+                                                      d_best_tours, d_best_keys);
   AcoUpdateArgs u{p->colonies, p->ants, n, in.N, (uint32_t)p->evap_shift, p->tau_min, p->tau_max,
                   d_tau, d_tours, d_iter_best};
   const int64_t total = (int64_t)p->colonies * in.N * in.N;

@@ -1,14 +1,21 @@
 """Island model across GPUs: one process per GPU, each runs
 independent SA chains / GA populations / ant colonies; every few epochs the
-E best tours of every rank are all-gathered (torch.distributed: "nccl" is
-RCCL over xGMI on the MI355X node, "gloo" in the CPU tests) and each rank
-injects the global E best into its own search.  The payload is tiny
-(E x (2n + 8) bytes per rank), so the exchange is latency-bound and runs
-only every `exchange_every` epochs.  Brute force shards lexicographic rank
-ranges instead and reduces the (key, rank) minimum.
+E best tours of every rank are all-gathered and every rank injects the same
+global E best into its own search.
 
-The merge order is deterministic: global elites are ranked by
-(key, source rank, position), identical on every rank.
+The exchange is the library's (include/vrpms.h):
+  * ``vrpms_island_exchange`` -- pack the E elites (device top-E), one RCCL
+    ``ncclAllGather`` of the messages over xGMI, merge by (key, rank,
+    position) on the device, inject; used once ``init_comm`` has given the
+    context its communicator;
+  * without a communicator but with a multi-rank torch.distributed group
+    (e.g. "gloo"), the same library pack / merge / inject run around a
+    torch.distributed all-gather of the message bytes (the fallback
+    communicator);
+  * with one rank, the exchange is local (pack -> merge -> inject).
+The payload is tiny (E x (2n + 8) bytes per rank), so the exchange is
+latency-bound and runs only every `exchange_every` epochs.  Brute force
+shards lexicographic rank ranges instead and reduces the (key, rank) minimum.
 """
 from __future__ import annotations
 
@@ -20,48 +27,58 @@ def _torch():
     return torch
 
 
-def _u64_order(keys):
-    """int64 tensor holding uint64 keys -> int64 values with the same order."""
-    torch = _torch()
-    return keys ^ torch.tensor(-(2**63), dtype=keys.dtype, device=keys.device)
+def _dist_world(group=None) -> int:
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1
+    return dist.get_world_size(group)
 
 
-def gather_elites(tours, keys, group=None):
-    """All-gather (tours [E][n], keys [E]) from every rank, concatenated in rank order."""
+def init_comm(ctx, group=None) -> int:
+    """Give `ctx` an RCCL communicator spanning the torch.distributed group:
+    rank 0 draws the unique id (vrpms_island_unique_id), the group
+    broadcasts it, every rank calls vrpms_island_init.  Returns the world."""
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    obj = [ctx.island_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    ctx.island_init(obj[0], rank, world)
+    return world
+
+
+def all_gather_bytes(msg, group=None):
+    """The fallback communicator: all-gather one uint8 message per rank
+    through torch.distributed, concatenated in rank order (CPU tensors for
+    gloo, device tensors for nccl)."""
     import torch.distributed as dist
     torch = _torch()
     world = dist.get_world_size(group)
-    t32 = tours.to(torch.int32).contiguous()          # gloo has no int16 collectives
-    tl = [t32.new_empty(t32.shape) for _ in range(world)]
-    kl = [keys.new_empty(keys.shape) for _ in range(world)]
-    dist.all_gather(tl, t32, group=group)
-    dist.all_gather(kl, keys.contiguous(), group=group)
-    return torch.cat(tl).to(tours.dtype), torch.cat(kl)
-
-
-def select_global(tours, keys, E: int):
-    """The E best of the gathered elites by (key, gathered position)."""
-    torch = _torch()
-    order = torch.argsort(_u64_order(keys), stable=True)[:E]
-    return tours[order], keys[order]
+    send = msg if dist.get_backend(group) == "nccl" else msg.cpu()
+    parts = [torch.empty_like(send) for _ in range(world)]
+    dist.all_gather(parts, send.contiguous(), group=group)
+    return torch.cat(parts)
 
 
 def exchange(runner, E: int, group=None):
-    """One migration epoch: gather every rank's E elites, inject the global E best."""
-    tours, keys = runner.elites(E)
-    gt, gk = gather_elites(tours, keys, group)
-    bt, bk = select_global(gt, gk, E)
-    runner.inject(bt, bk)
-    return bk
+    """One migration epoch: every rank's E elites of runner.src() are
+    gathered, the global E best by (key, rank, position) are injected into
+    runner.dst() by runner.inject_mode.  Returns nothing (device state)."""
+    ctx = runner.ctx
+    world = _dist_world(group)
+    if world == 1 or ctx.island_world() == world:
+        ctx.island_exchange(runner.src(), runner.dst(), runner.inject_mode, E, runner.groups)
+        return
+    msg = ctx.island_pack(*runner.src(), E)
+    msgs = all_gather_bytes(msg, group)
+    tours, keys = ctx.island_merge(msgs, world, E, runner.n)
+    ctx.pool_inject(*runner.dst(), runner.inject_mode, tours, keys, runner.groups)
 
 
 def run_islands(runner, epochs: int, exchange_every: int = 5, E: int = 8, group=None):
     """Advance `runner` for `epochs`, migrating every `exchange_every` epochs."""
-    import torch.distributed as dist
-    dist_on = dist.is_available() and dist.is_initialized()
     for e in range(1, epochs + 1):
         runner.epoch()
-        if dist_on and dist.get_world_size(group) > 1 and e % exchange_every == 0:
+        if _dist_world(group) > 1 and e % exchange_every == 0:
             exchange(runner, E, group)
     return runner.best()
 
@@ -70,13 +87,10 @@ def run_fixed(runner, epochs: int, exchange_every: int = 5, E: int = 8, group=No
     """`epochs` island epochs with a migration every `exchange_every` epochs,
     on a FIXED count: every rank runs the identical control flow (no
     wall-clock exit), so every rank enters every collective.  With one rank
-    the migration is local (the E best re-injected into the worst chains).
-    `sync` (e.g. torch.cuda.synchronize) brackets each exchange so its time
-    is measured apart.  Returns (exchanges, exchange_seconds)."""
+    the migration is local (the E best re-injected).  `sync` (e.g.
+    torch.cuda.synchronize) brackets each exchange so its time is measured
+    apart.  Returns (exchanges, exchange_seconds)."""
     import time
-
-    import torch.distributed as dist
-    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
     n_ex, t_ex = 0, 0.0
     for e in range(1, epochs + 1):
         runner.epoch()
@@ -84,10 +98,7 @@ def run_fixed(runner, epochs: int, exchange_every: int = 5, E: int = 8, group=No
             if sync:
                 sync()
             t0 = time.perf_counter()
-            if multi:
-                exchange(runner, E, group)
-            else:
-                runner.inject(*runner.elites(E))
+            exchange(runner, E, group)
             if sync:
                 sync()
             t_ex += time.perf_counter() - t0
@@ -95,16 +106,15 @@ def run_fixed(runner, epochs: int, exchange_every: int = 5, E: int = 8, group=No
     return n_ex, t_ex
 
 
-def global_best(key: int, tour, n: int, group=None, device=None):
-    """Reduce the per-rank best (key, tour) to the global best on every rank."""
-    import torch.distributed as dist
-    torch = _torch()
-    t = torch.as_tensor(list(tour), dtype=torch.int16, device=device).reshape(1, n)
-    k = torch.tensor([key - (1 << 64) if key >= (1 << 63) else key], dtype=torch.int64,
-                     device=device)
-    gt, gk = gather_elites(t, k, group)
-    bt, bk = select_global(gt, gk, 1)
-    return int(bk[0]) & (2**64 - 1), bt[0].tolist()
+def global_best(runner, group=None):
+    """The best (key, tour) over every rank's runner.src(), identical on
+    every rank: a one-elite pack / all-gather / merge."""
+    ctx = runner.ctx
+    world = _dist_world(group)
+    msg = ctx.island_pack(*runner.src(), 1)
+    msgs = msg if world == 1 else all_gather_bytes(msg, group)
+    tours, keys = ctx.island_merge(msgs, world, 1, runner.n)
+    return int(keys[0]) & (2**64 - 1), [int(x) for x in tours[0].cpu().tolist()]
 
 
 def bf_rank_range(n: int, rank: int, world: int):

@@ -1,12 +1,19 @@
 """Epoch-driven search runners over the HIP kernels.
 
 Each runner owns its device state (tours, keys) as torch tensors, advances
-it with one C-ABI call per epoch, and exposes the three operations the
-island model and the front-end need:
+it with one C-ABI call per epoch, and exposes the operations the island
+model and the front-end need:
 
   epoch()            advance the search (GPU kernels only)
   best()             (key, tour) of the best solution seen (device argmin)
-  elites(E) / inject(tours, keys)   migration hooks (islands.py)
+  elites(E) / inject(tours, keys)   migration hooks (islands.py), both
+                     library kernels (vrpms_pool_elites / vrpms_pool_inject)
+  src() / dst() / inject_mode / groups   the pools vrpms_island_exchange
+                     reads the elites from and injects the migrants into
+
+torch only owns buffers here: start tours come from the library's Philox
+Fisher-Yates kernel, elite selection / injection / ACO best tracking from
+its pool kernels.
 
 Defaults follow the reference's knobs where it has any
 (api/parameters.py:18-23: randomPermutationCount -> population,
@@ -19,6 +26,7 @@ import math
 
 import numpy as np
 
+from ._lib import INJECT_BETTER, INJECT_SORTED, INJECT_WORST
 from .core import Context
 
 
@@ -27,13 +35,10 @@ def _torch():
     return torch
 
 
-def random_tours(ctx: Context, count: int, n: int, seed: int):
-    """count random permutations of 1..n as int16 rows, generated on the device."""
-    torch = _torch()
-    g = torch.Generator(device=ctx.dev)
-    g.manual_seed(int(seed) & (2**63 - 1))
-    r = torch.rand((count, n), generator=g, device=ctx.dev)
-    return (r.argsort(dim=1) + 1).to(torch.int16).contiguous()
+def random_tours(ctx: Context, count: int, n: int, seed: int, stream_id: int = 0):
+    """count Philox Fisher-Yates permutations of 1..n as int16 rows
+    (vrpms_random_tours, oracle/pool.py philox_tour)."""
+    return ctx.random_tours(count, n, seed, stream_id)
 
 
 def typical_edge(durations) -> float:
@@ -43,18 +48,21 @@ def typical_edge(durations) -> float:
 
 
 class _Base:
+    inject_mode = INJECT_WORST
+    groups = 1
+
     def best(self):
-        keys, tours = self._keys_tours()
+        tours, keys = self.src()
         k, i = self.ctx.argmin(keys.reshape(-1))
         return k, tours.reshape(-1, self.n)[i]
 
     def elites(self, E: int):
-        torch = _torch()
-        keys, tours = self._keys_tours()
-        flat = keys.reshape(-1)
-        # uint64 order == int64 order after flipping the sign bit
-        order = torch.argsort(flat ^ torch.tensor(-(2**63), device=flat.device), stable=True)[:E]
-        return tours.reshape(-1, self.n)[order].clone(), flat[order].clone()
+        """The E best (tour, key) rows of src() by (key, index)."""
+        return self.ctx.pool_elites(*self.src(), E)
+
+    def inject(self, tours, keys):
+        """Migrants into dst() by inject_mode (vrpms_pool_inject)."""
+        self.ctx.pool_inject(*self.dst(), self.inject_mode, tours, keys, self.groups)
 
 
 class SARunner(_Base):
@@ -87,21 +95,19 @@ class SARunner(_Base):
             self.inv_t = np.float32(self.inv_t * self.inv_alpha)
         self.step += s
 
-    def _keys_tours(self):
-        return self.best_key, self.best_t
+    # elites come from the best-so-far; migrants restart the worst chains
+    def src(self):
+        return self.best_t, self.best_key
 
-    def inject(self, tours, keys):
-        """Restart the worst chains from migrant tours."""
-        torch = _torch()
-        E = tours.shape[0]
-        order = torch.argsort(self.cur_key ^ torch.tensor(-(2**63), device=self.cur_key.device),
-                              descending=True, stable=True)[:E]
-        self.cur[order] = tours.to(self.cur.dtype)
-        self.cur_key[order] = keys
+    def dst(self):
+        return self.cur, self.cur_key
 
 
 class GARunner(_Base):
-    """Island GA: `islands` populations of `pop` members."""
+    """Island GA: `islands` populations of `pop` members, each kept sorted by
+    (key, index); migrants take the worst slots of the islands round robin."""
+
+    inject_mode = INJECT_SORTED
 
     def __init__(self, ctx: Context, n: int, islands: int = 8, pop: int = 256, seed: int = 0,
                  pmut: float = 0.2, gens_per_epoch: int = 20):
@@ -109,6 +115,7 @@ class GARunner(_Base):
         self.islands, self.pop, self.pmut = islands, pop, pmut
         self.gens_per_epoch = gens_per_epoch
         self.gen = 0
+        self.groups = islands
         self.tours = random_tours(ctx, islands * pop, n, seed).view(islands, pop, n).contiguous()
         self.keys = ctx.eval(self.tours.view(-1, n)).view(islands, pop)
 
@@ -117,30 +124,18 @@ class GARunner(_Base):
         self.ctx.ga_generation(self.tours, self.keys, g, self.pmut, self.seed, self.gen)
         self.gen += g
 
-    def _keys_tours(self):
-        return self.keys, self.tours
+    def src(self):
+        return self.tours, self.keys
 
-    def inject(self, tours, keys):
-        """Migrants replace the worst member of each island (round robin)."""
-        E = tours.shape[0]
-        for e in range(E):
-            isl = e % self.islands
-            slot = self.pop - 1 - (e // self.islands)
-            if slot < 0:
-                break
-            self.tours[isl, slot] = tours[e].to(self.tours.dtype)
-            self.keys[isl, slot] = keys[e]
-        # keep each island sorted by (key, index): the kernel's invariant
-        torch = _torch()
-        for isl in range(self.islands):
-            k = self.keys[isl]
-            order = torch.argsort(k ^ torch.tensor(-(2**63), device=k.device), stable=True)
-            self.keys[isl] = k[order]
-            self.tours[isl] = self.tours[isl][order]
+    def dst(self):
+        return self.tours, self.keys
 
 
 class ACORunner(_Base):
-    """Integer max-min ant colonies (one pheromone matrix per colony)."""
+    """Integer max-min ant colonies (one pheromone matrix per colony); each
+    colony's best-so-far is tracked on the device."""
+
+    inject_mode = INJECT_BETTER
 
     def __init__(self, ctx: Context, n: int, colonies: int = 4, ants: int = 64, seed: int = 0,
                  iters_per_epoch: int = 5, evap_shift: int = 3):
@@ -157,33 +152,18 @@ class ACORunner(_Base):
         self.best_t = torch.zeros((colonies, n), dtype=torch.int16, device=ctx.dev)
 
     def epoch(self, iters: int | None = None):
-        torch = _torch()
         for _ in range(self.iters_per_epoch if iters is None else iters):
-            tours, keys, ib = self.ctx.aco_iteration(self.tau, self.eta, self.ants, self.seed,
-                                                     self.it, self.evap_shift, self.tau_min,
-                                                     self.tau_max)
+            self.ctx.aco_iteration(self.tau, self.eta, self.ants, self.seed, self.it,
+                                   self.evap_shift, self.tau_min, self.tau_max,
+                                   best_tours=self.best_t, best_keys=self.best_key)
             self.it += 1
-            k = ib[:, 0]
-            better = (k ^ torch.tensor(-(2**63), device=k.device)) < \
-                (self.best_key ^ torch.tensor(-(2**63), device=k.device))
-            idx = ib[:, 1].clamp(0, self.ants - 1)
-            cand = tours[torch.arange(self.colonies, device=k.device), idx]
-            self.best_key = torch.where(better, k, self.best_key)
-            self.best_t = torch.where(better[:, None], cand, self.best_t)
 
-    def _keys_tours(self):
-        return self.best_key, self.best_t
+    # migrant e replaces colony e's best-so-far when better
+    def src(self):
+        return self.best_t, self.best_key
 
-    def inject(self, tours, keys):
-        """Migrant tours are deposited on every colony like an iteration-best."""
-        torch = _torch()
-        m = min(tours.shape[0], self.colonies)
-        k = keys[:m]
-        better = (k ^ torch.tensor(-(2**63), device=k.device)) < \
-            (self.best_key[:m] ^ torch.tensor(-(2**63), device=k.device))
-        self.best_key[:m] = torch.where(better, k, self.best_key[:m])
-        self.best_t[:m] = torch.where(better[:, None], tours[:m].to(self.best_t.dtype),
-                                      self.best_t[:m])
+    def dst(self):
+        return self.best_t, self.best_key
 
 
 def brute_force(ctx: Context, n: int, rank_begin: int = 0, rank_end: int | None = None):
