@@ -12,12 +12,15 @@ process per GPU via torch.distributed.run.
 
 Reported beside the value:
   roofline      the dominant kernel (eval_cvrp_words2, word-interleaved
-                tours) timed with HIP events on the stream it runs on;
-                achieved = algorithmic HBM bytes per launch (C x (100 B tour +
-                8 B key)) / mean launch time.  The kernel is LDS-gather bound:
-                lds_gather_roofline prices it against the measured random
-                ds_read_b64 rate.  rows_layout times the same batch in the
-                API's row-major layout (eval_cvrp_rows2).
+                tours: the layout the GA / ACO kernels emit) timed with HIP
+                events on the stream it runs on.  It is LDS-gather bound, so
+                achieved = evals/s x G (G = n + K gathers per eval, SURVEY.md
+                §8d) against the measured random ds_read_b64 rate R_gather;
+                hbm_roofline = algorithmic HBM bytes (C x (100 B tour + 8 B
+                key)) / mean launch time against 8 TB/s.  rows_layout times
+                the same batch in the API's row-major layout (eval_cvrp_rows2).
+  search        GA / ACO / BF throughput on cfg 2 (the endpoints' algorithms).
+  cfg1_main_py  BASELINE cfg 1: main.py's calls through the drop-in.
   cpu_baseline  the C restatement of the spec (oracle/oracle_c.c, OpenMP)
                 on a bounded sample of the same workload, rank 0 only.
 """
@@ -25,6 +28,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -57,18 +61,12 @@ def parse():
     return ap.parse_args()
 
 
-def make_batch(torch, C, n, dev, seed):
-    """C random permutations of 1..n as uint8 rows, generated on the device
-    in chunks (argsort of uniform keys)."""
-    g = torch.Generator(device=dev)
-    g.manual_seed(seed)
-    out = torch.empty((C, n), dtype=torch.uint8, device=dev)
-    chunk = 1 << 20
-    for s in range(0, C, chunk):
-        e = min(C, s + chunk)
-        r = torch.rand((e - s, n), generator=g, device=dev)
-        out[s:e] = (r.argsort(dim=1) + 1).to(torch.uint8)
-    return out
+def make_batch(ctx, C, n, seed, dtype=None):
+    """C Philox Fisher-Yates permutations of 1..n (vrpms_random_tours, the
+    library's start-tour kernel; SURVEY.md §8d "candidate perms are
+    Philox-seeded") as uint8 rows, generated on the device."""
+    import torch
+    return ctx.random_tours(C, n, seed, stream_id=0xBE7C, dtype=dtype or torch.uint8)
 
 
 def cpu_baseline(inst, perms_dev, seconds):
@@ -252,7 +250,7 @@ def other_configs(ctx, torch, dev, seed=0):
     td = synth.td_cvrp(200, 16, seed=seed)
     ctx.set_instance(CVRP, td.durations, td.demand, td.capacities, td.start_times)
     C = 1 << 21
-    perms = make_batch(torch, C, td.n, dev, seed + 11)
+    perms = make_batch(ctx, C, td.n, seed + 11)
     keys = torch.empty(C, dtype=torch.int64, device=dev)
     t = kernel_time(lambda: ctx.eval(perms, out=keys))
     out["cfg3_tdvrp200_h24"] = {"kernel": "eval_staged<u16 L2, H=24, u8 tours>",
@@ -264,12 +262,7 @@ def other_configs(ctx, torch, dev, seed=0):
     x = synth.x_style(1000, seed=seed)
     ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
     C = 1 << 18
-    g = torch.Generator(device=dev)
-    g.manual_seed(seed + 13)
-    p16 = torch.empty((C, x.n), dtype=torch.int16, device=dev)
-    for s in range(0, C, 1 << 15):
-        r = torch.rand((min(C, s + (1 << 15)) - s, x.n), generator=g, device=dev)
-        p16[s:s + r.shape[0]] = (r.argsort(dim=1) + 1).to(torch.int16)
+    p16 = make_batch(ctx, C, x.n, seed + 13, dtype=torch.int16)
     keys = torch.empty(C, dtype=torch.int64, device=dev)
     t = kernel_time(lambda: ctx.eval(p16, out=keys))
     out["cfg4_x1000"] = {"kernel": "eval_staged<u16 L2, H=1, u16 tours>", "evals_per_s": C / t,
@@ -348,6 +341,110 @@ def island_leg(ctx, torch, dev, world, rank, dist, epochs=20, steps=25, chains=1
             "best": {"unvisited": key >> 56, "duration_sum": (key >> 28) & (2**28 - 1)}}
 
 
+def search_lines(ctx, torch, dev, r_gather, seed=0):
+    """Throughput of the GA / ACO / BF endpoints' algorithms on BASELINE cfg 2
+    (CVRP-100, K = 8) -- the slots api/vrp/{ga,aco,bf}/index.py fill.  GA and
+    ACO score their children / ants with eval_cvrp_words2 (the headline
+    kernel) inside vrpms_ga_generation / vrpms_aco_iteration; evals/s counts
+    full tour evaluations, the LDS-gather fraction prices them at G = n + K
+    gathers against the measured R_gather (the whole generation's time, so
+    breeding / construction and selection are inside it)."""
+    from vrpms_amd import runners, synth
+    from vrpms_amd.core import CVRP
+    inst = synth.cvrp(100, 8, seed=seed)
+    ctx.set_instance(CVRP, inst.durations, inst.demand, inst.capacities, inst.start_times)
+    G = inst.n + inst.K
+    out = {}
+
+    def timed(fn, reps):
+        fn()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / reps, e0.elapsed_time(e1) * 1e-3 / reps
+
+    # GA: 64 islands x 256 (randomPermutationCount), 10 generations per call
+    islands_, pop, gens = 64, 256, 10
+    ga = runners.GARunner(ctx, inst.n, islands=islands_, pop=pop, seed=seed, gens_per_epoch=gens)
+    wall, dev_s = timed(ga.epoch, 5)
+    children = islands_ * pop * gens
+    out["ga"] = {"workload": "cfg2 CVRP-100, island GA", "islands": islands_, "pop": pop,
+                 "generations_per_call": gens, "scoring_kernel": "eval_cvrp_words2",
+                 "generations_per_s": gens / dev_s, "child_evals_per_s": children / dev_s,
+                 "wall_generations_per_s": gens / wall,
+                 "lds_gather_frac_whole_generation": children / dev_s * G / r_gather,
+                 "best": {"duration_sum": (ga.best()[0] >> 28) & (2**28 - 1),
+                          "unvisited": ga.best()[0] >> 56}}
+    del ga
+    # ACO: 64 colonies x 64 ants (one wavefront per ant), 5 iterations per epoch
+    colonies, ants, iters = 64, 64, 5
+    aco = runners.ACORunner(ctx, inst.n, colonies=colonies, ants=ants, seed=seed,
+                            iters_per_epoch=iters)
+    wall, dev_s = timed(aco.epoch, 3)
+    out["aco"] = {"workload": "cfg2 CVRP-100, integer max-min ACO", "colonies": colonies,
+                  "ants": ants, "scoring_kernel": "eval_cvrp_words2",
+                  "iterations_per_s": iters / dev_s, "ant_tours_per_s": colonies * ants * iters / dev_s,
+                  "wall_iterations_per_s": iters / wall,
+                  "best": {"duration_sum": (aco.best()[0] >> 28) & (2**28 - 1)}}
+    del aco
+    # BF: exhaustive lexicographic ranks on CVRP-n sub-instances (K = 3)
+    bf = {}
+    for n in (10, 11, 12):
+        sub = synth.cvrp(n, 3, seed=seed)
+        ctx.set_instance(CVRP, sub.durations, sub.demand, sub.capacities, sub.start_times)
+        total = math.factorial(n)
+        t0 = time.perf_counter()
+        ctx.bf_run(n, 0, total)
+        dt = time.perf_counter() - t0
+        bf[f"n{n}"] = {"permutations": total, "seconds": dt, "evals_per_s": total / dt}
+    out["bf"] = {"workload": "CVRP-n, K = 3, all n! giant tours", **bf}
+    return out
+
+
+def cfg1_leg():
+    """BASELINE cfg 1: main.py's two calls (reference main.py:5-6) through the
+    drop-in front-end -- calculate_duration("A", "B") (no matrix loaded: the
+    reference's stub behaviour) and solve_vrp_problem() (no arguments: the
+    15-node instance, solved on the GPU) -- plus a TSP-20 solve per
+    algorithm.  The reference stub itself measured 144,054 / 1,541,860
+    calls/s on the survey container; it computes no cost."""
+    from vrpms_amd import solver, synth
+    out = {}
+    t0, n = time.perf_counter(), 0
+    while time.perf_counter() - t0 < 0.5:
+        solver.calculate_duration("A", "B")
+        n += 1
+    out["calculate_duration_calls_per_s"] = n / (time.perf_counter() - t0)
+    solver.solve_vrp_problem(seed=1)                  # warm: code objects, context
+    t0, n = time.perf_counter(), 0
+    while time.perf_counter() - t0 < 2.0 or n < 3:
+        r = solver.solve_vrp_problem(seed=n)
+        n += 1
+    out["solve_vrp_problem"] = {"calls_per_s": n / (time.perf_counter() - t0),
+                                "total_time_last": r["total_time"], "tour_len": len(r["tour"])}
+    t = synth.tsp20(0)
+    algos = {}
+    for algo in ("bf", "ga", "sa", "aco"):
+        kw = {"time_limit": None}
+        if algo == "bf":
+            D = t.durations[0][:12, :12]               # 11 customers: exhaustive
+            cust = list(range(1, 12))
+        else:
+            D, cust = t.durations[0], list(range(1, 20))
+        solver.solve_tsp(algo, D, cust, 0, 0, seed=0, **kw)
+        t0 = time.perf_counter()
+        res = solver.solve_tsp(algo, D, cust, 0, 0, seed=0, **kw)
+        algos[algo] = {"seconds": time.perf_counter() - t0, "duration": res["duration"],
+                       "customers": len(cust)}
+    out["solve_tsp_tsp20"] = algos
+    return out
+
+
 def pmc_traffic(kernel, grid):
     """HBM bytes per launch from the committed PMC pass of this same command
     (profiles/pmc_traffic.json, written by tools/summarize_profiles.py from
@@ -381,7 +478,7 @@ def main():
     ctx = Context(local)
     ctx.set_instance(CVRP, inst.durations, inst.demand, inst.capacities, inst.start_times)
     C, n = args.candidates, inst.n
-    perms = make_batch(torch, C, n, dev, args.seed * 1000 + rank)
+    perms = make_batch(ctx, C, n, args.seed * 1000 + rank)
     words = ctx.to_words(perms, n)           # word-interleaved layout, resident in HBM
     keys = torch.empty(C, dtype=torch.int64, device=dev)
     keys_rows = torch.empty(C, dtype=torch.int64, device=dev)
@@ -443,6 +540,12 @@ def main():
         nbytes = 4 * ((n + 3) // 4)
         bytes_per_launch = C * (nbytes + 8)
         achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+        # north-star roofline: random LDS gathers, G = n + K per eval
+        # (the K route-closure legs ride in the same packed
+        # entries, so the kernel issues n ds_read_b64 per eval), against
+        # R_gather measured by vrpms_probe_lds_gather on this device
+        evals_s = C / (kernel_ms * 1e-3)
+        G = n + inst.K
         out = {
             "metric": METRIC,
             "value": value,
@@ -455,33 +558,32 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int32",
-            "data": "synthetic (seeded CVRP-100 instance, device-generated random giant tours)",
+            "data": "synthetic (seeded CVRP-100 instance, Philox random giant tours from "
+                    "vrpms_random_tours)",
             "config": {"workload": "cvrp100_k8_full_tour_eval", "customers": n, "vehicles": 8,
                        "candidates_per_step": C, "tour_dtype": "u8",
-                       "tour_layout": "words [n/4][C] u32", "per_rank_batch": C,
-                       "parallelism": f"islands{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                       "tour_layout": "words [n/4][C] u32 (the layout GA/ACO emit)",
+                       "per_rank_batch": C, "parallelism": f"islands{world}"},
+            "roofline": {"bound": "lds_gather", "achieved": evals_s * G, "peak": r_gather,
+                         "unit": "gathers/s", "frac": evals_s * G / r_gather,
+                         "peak_source": "measured random ds_read_b64 ceiling "
+                                        "(vrpms_probe_lds_gather, 1024-lane WGs, 2/CU); the "
+                                        "guide's conflict-free ds_read_b64 rate is ~19.7 T/s",
+                         "G_per_eval": G, "issued_per_eval": n,
+                         "frac_issued": evals_s * n / r_gather,
                          # launch_words2's auto grid: two tours per lane, one
                          # 1024-lane workgroup per CU
                          "traffic": pmc_traffic("eval_cvrp_words2",
                                                 min((C + 2047) // 2048, cus) * 1024),
-                         "traffic_unit": "bytes/launch (PMC, profiles/pmc_traffic.json)",
-                         "kernel": "eval_cvrp_words2", "kernel_ms": kernel_ms,
-                         "bytes_per_launch": bytes_per_launch,
-                         "lds_gathers_per_s": C * n / (kernel_ms * 1e-3)},
+                         "traffic_unit": "HBM bytes/launch (PMC, profiles/pmc_traffic.json)",
+                         "kernel": "eval_cvrp_words2", "kernel_ms": kernel_ms},
+            "hbm_roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                             "bytes_per_launch": bytes_per_launch},
             "rows_layout": {"kernel": "eval_cvrp_rows2", "evals_per_s": C / (rows_ms * 1e-3),
-                            "kernel_ms": rows_ms},
+                            "kernel_ms": rows_ms,
+                            "lds_gather_frac": C / (rows_ms * 1e-3) * G / r_gather},
         }
-        # north-star roofline: random LDS gathers, G = n + K per eval,
-        # R_gather measured by vrpms_probe_lds_gather on this device
-        evals_s = C / (kernel_ms * 1e-3)
-        G = n + inst.K
-        out["lds_gather_roofline"] = {
-            "r_gather_measured": r_gather, "unit": "gathers/s", "G_per_eval": G,
-            "achieved": evals_s * G, "frac": evals_s * G / r_gather,
-            "issued_per_eval": n, "frac_issued": evals_s * n / r_gather,
-            "probe": "random ds_read_b64 over an N*N u64 LDS table, 1024-lane WGs, 2/CU"}
         import numpy as np
         same = bool(torch.equal(keys, keys_rows))
         out["rows_vs_words_identical"] = same
@@ -500,6 +602,14 @@ def main():
                 out["other_configs"] = other_configs(ctx, torch, dev)
             except Exception:
                 out["other_configs"] = {"error": traceback.format_exc(limit=3)}
+            try:
+                out["search"] = search_lines(ctx, torch, dev, r_gather)
+            except Exception:
+                out["search"] = {"error": traceback.format_exc(limit=3)}
+            try:
+                out["cfg1_main_py"] = cfg1_leg()
+            except Exception:
+                out["cfg1_main_py"] = {"error": traceback.format_exc(limit=3)}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -169,8 +169,9 @@ __global__ void inject_better_kernel(uint16_t* tours, uint64_t* keys, int n, int
                                      const uint64_t* __restrict__ in_keys) {
   const int e = blockIdx.x;
   if (e >= E) return;
-  if (!(in_keys[e] < keys[e])) return;  // block-uniform
+  if (!(in_keys[e] < keys[e])) return;  // block-uniform: every thread tests before the barrier
   for (int q = threadIdx.x; q < n; q += blockDim.x) tours[(int64_t)e * n + q] = in_tours[(int64_t)e * n + q];
+  __syncthreads();                       // ... and keys[e] changes only after it
   if (threadIdx.x == 0) keys[e] = in_keys[e];
 }
 
@@ -377,10 +378,15 @@ int vrpms_random_tours(vrpms_ctx* ctx, int64_t count, int32_t n, int64_t ld, int
   if (count == 0 || n == 0) return VRPMS_OK;
   if (!d_tours) return fail(VRPMS_EINVAL, "vrpms_random_tours: d_tours is NULL");
   VRPMS_HIP(hipSetDevice(ctx->device));
+  // each lane shuffles its row in LDS when 64 rows fit, else in place in HBM
   const size_t lds = (size_t)64 * n * 2;
-  RandArgs a{count, n, (int)ld, tour_bytes, lds <= 64 * 1024 ? 1 : 0, (uint32_t)seed,
+  const bool in_lds = lds <= ctx->max_lds;
+  RandArgs a{count, n, (int)ld, tour_bytes, in_lds ? 1 : 0, (uint32_t)seed,
              (uint32_t)(seed >> 32), stream_id, d_tours};
-  random_tours_kernel<<<(unsigned)((count + 63) / 64), 64, a.in_lds ? lds : 0,
+  if (in_lds && lds > 65536)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(random_tours_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  random_tours_kernel<<<(unsigned)((count + 63) / 64), 64, in_lds ? lds : 0,
                         (hipStream_t)stream>>>(a);
   VRPMS_HIP(hipGetLastError());
   return VRPMS_OK;
