@@ -114,17 +114,20 @@ int vrpms_eval_path(vrpms_ctx* ctx, int32_t perm_bytes, int64_t ld, const void* 
 /*   VRPMS_OPT_STAGED_M: candidates interleaved per lane in eval_staged
  *   (0 = auto: 2 for hour-indexed matrices, 1 for static; 1 or 2 force). */
 #define VRPMS_OPT_STAGED_M 2
-/*   VRPMS_OPT_WORDS_KERNEL: LDS-packed kernel generation (0 = auto:
- *   eval_cvrp_words2 for vrpms_eval_words, eval_cvrp_rows2 for path 0 of
- *   vrpms_eval; 1 = the first-generation eval_cvrp_words / eval_cvrp_packed,
- *   A/B only). */
+/*   VRPMS_OPT_WORDS_KERNEL: LDS-packed kernel for path 0 of vrpms_eval
+ *   (0 = auto: eval_cvrp_rows2; 1 = eval_cvrp_packed, the LDS-tile kernel
+ *   also used for heterogeneous fleets, A/B only). */
 #define VRPMS_OPT_WORDS_KERNEL 3
 /*   VRPMS_OPT_WORDS_ILP: candidates per lane in eval_cvrp_words2 (0 = auto:
- *   2; 1, 2 or 3 force, A/B). */
+ *   2; 1 or 2 force, A/B). */
 #define VRPMS_OPT_WORDS_ILP 4
 /*   VRPMS_OPT_WORDS_LOOKAHEAD: words ahead whose gathers eval_cvrp_words2
  *   keeps in flight (0 = auto, 1 or 2 force; A/B). */
 #define VRPMS_OPT_WORDS_LOOKAHEAD 5
+/*   VRPMS_OPT_ROWS_CONFIG: eval_cvrp_rows2's (chunk words, candidates per
+ *   lane): 0 = auto (fewest chunks that fit the LDS), 1 = (8, 2),
+ *   2 = (16, 1), 3 = (4, 2), 4 = (8, 1), 5 = (4, 1); A/B. */
+#define VRPMS_OPT_ROWS_CONFIG 6
 int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value);
 
 /* Decode ONE giant tour into the result dict of api/vrp/ga/index.py:49-53

@@ -34,6 +34,8 @@ def load():
         lib.oracle_sa_run.restype = ctypes.c_int
         lib.oracle_sa_run.argtypes = [i32, vp, i32, i32, vp, vp, vp, i32, i32, vp, vp, vp, vp, i32,
                                       i32, i32, f32, f32, u64, u64, i32]
+        lib.oracle_bf.restype = ctypes.c_int
+        lib.oracle_bf.argtypes = [i32, vp, i32, i32, vp, vp, vp, i32, i32, i32, u64, u64, vp, i32]
         lib.oracle_tsp_batch_sa.restype = ctypes.c_int
         lib.oracle_tsp_batch_sa.argtypes = [vp, i32, i32, i32, f32, f32, u64, vp, vp, i32]
         _lib = lib
@@ -105,6 +107,23 @@ def tsp_batch_sa(mats, steps, inv_t0, inv_alpha, seed, threads: int = 0):
     lib.oracle_tsp_batch_sa(_p(M), R, N, int(steps), float(inv_t0), float(inv_alpha),
                             int(seed) & (2**64 - 1), _p(tours), _p(keys), threads)
     return tours, keys
+
+
+def bf(durations, n, r0=0, r1=None, demand=None, capacities=None, start_times=(0,),
+       problem: int = 1, objective: int = 0, threads: int = 0):
+    """C/OpenMP brute force over lexicographic ranks [r0, r1) -> (key, rank)."""
+    import math
+    lib = load()
+    D = np.ascontiguousarray(np.asarray(durations, dtype=np.int32).reshape(
+        (-1,) + np.asarray(durations).shape[-2:]))
+    st = np.ascontiguousarray(np.asarray(start_times, dtype=np.int32).reshape(-1))
+    dem = None if demand is None else np.ascontiguousarray(np.asarray(demand, dtype=np.int32))
+    cap = None if capacities is None else np.ascontiguousarray(np.asarray(capacities, dtype=np.int32))
+    r1 = math.factorial(n) if r1 is None else r1
+    out = np.zeros(2, dtype=np.uint64)
+    lib.oracle_bf(problem, _p(D), D.shape[0], D.shape[1], _p(dem), _p(cap), _p(st), st.shape[0],
+                  objective, n, int(r0), int(r1), _p(out), threads)
+    return int(out[0]), int(out[1])
 
 
 def max_threads() -> int:

@@ -392,6 +392,92 @@ int oracle_tsp_batch_sa(const int32_t* mats, int R, int N, int steps, float inv_
   return 0;
 }
 
+/* Brute force restatement (oracle/search.py bf, vrpms_bf_run): the minimum
+ * (key, rank) over lexicographic ranks [r0, r1) of the permutations of
+ * 1..n (n <= 20), OpenMP over contiguous rank blocks.  out[0] = key,
+ * out[1] = rank (UINT64_MAX, UINT64_MAX when the range is empty). */
+static void unrank_perm(uint64_t r, int n, uint16_t* p) {
+  uint64_t f[21];
+  f[0] = 1;
+  for (int i = 1; i <= 20; ++i) f[i] = f[i - 1] * (uint64_t)i;
+  int avail[20];
+  for (int i = 0; i < n; ++i) avail[i] = i + 1;
+  int m = n;
+  for (int i = 0; i < n; ++i) {
+    uint64_t d = r / f[n - 1 - i];
+    r %= f[n - 1 - i];
+    p[i] = (uint16_t)avail[d];
+    for (int x = (int)d; x < m - 1; ++x) avail[x] = avail[x + 1];
+    --m;
+  }
+}
+
+static void next_perm16(uint16_t* p, int n) {
+  int i = n - 2;
+  while (i >= 0 && p[i] >= p[i + 1]) --i;
+  if (i < 0) return;
+  int j = n - 1;
+  while (p[j] <= p[i]) --j;
+  uint16_t t = p[i];
+  p[i] = p[j];
+  p[j] = t;
+  for (int a = i + 1, b = n - 1; a < b; ++a, --b) {
+    t = p[a];
+    p[a] = p[b];
+    p[b] = t;
+  }
+}
+
+int oracle_bf(int problem, const int32_t* D, int H, int N, const int32_t* dem, const int32_t* cap,
+              const int32_t* st, int K, int objective, int n, uint64_t r0, uint64_t r1,
+              uint64_t* out, int threads) {
+  inst_t I = {problem, H, N, K, objective, D, dem, cap, st};
+  uint64_t bk = ~0ull, br = ~0ull;
+  if (n < 1 || n > 20 || r1 <= r0) {
+    out[0] = bk;
+    out[1] = br;
+    return 0;
+  }
+  const int64_t blocks = 4096;
+  const uint64_t span = r1 - r0;
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel
+#endif
+  {
+    uint64_t lk = ~0ull, lr = ~0ull;
+    uint16_t p[20];
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+    for (int64_t b = 0; b < blocks; ++b) {
+      const uint64_t ub = (uint64_t)b, q = span / (uint64_t)blocks, rem = span % (uint64_t)blocks;
+      const uint64_t lo = r0 + q * ub + (ub < rem ? ub : rem);
+      const uint64_t hi = lo + q + (ub < rem ? 1u : 0u);
+      if (lo >= hi) continue;
+      unrank_perm(lo, n, p);
+      for (uint64_t rk = lo; rk < hi; ++rk) {
+        const uint64_t k = tour_key(&I, p, n, NULL);
+        if (k < lk || (k == lk && rk < lr)) {
+          lk = k;
+          lr = rk;
+        }
+        next_perm16(p, n);
+      }
+    }
+#ifdef _OPENMP
+#pragma omp critical
+#endif
+    if (lk < bk || (lk == bk && lr < br)) {
+      bk = lk;
+      br = lr;
+    }
+  }
+  out[0] = bk;
+  out[1] = br;
+  return 0;
+}
+
 int oracle_max_threads(void) {
 #ifdef _OPENMP
   return omp_get_max_threads();

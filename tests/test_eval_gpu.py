@@ -112,26 +112,34 @@ def words_gen(ctx):
     """Reset the LDS-packed kernel generation after a test forces one."""
     yield ctx
     ctx.set_words_kernel(0)
+    ctx.set_rows_config(0)
     ctx.set_words_ilp(0)
     ctx.set_words_lookahead(0)
 
 
-# eval_cvrp_rows2 (row-major tiles staged through LDS) against the first
-# generation eval_cvrp_packed and the oracle: CW = 8 (N <= 101), CW = 4
-# (N = 111), ragged tiles, short tours, and N = 121 where no tile fits next
-# to the matrix (falls back to eval_cvrp_packed).
+# eval_cvrp_rows2 (row-major tiles staged through LDS) in every (CW, ILP)
+# configuration that fits, against eval_cvrp_packed and the oracle: N <= 101
+# (all five fit), N = 111 (the ILP-2 CW-8 tile no longer fits), ragged
+# tiles, short tours, and N = 121 where no tile fits next to the matrix
+# (falls back to eval_cvrp_packed).
 @pytest.mark.parametrize("n,K,ld,C", [(100, 8, 100, 20037), (97, 7, 100, 5000), (30, 3, 32, 4099),
                                       (5, 2, 8, 3000), (110, 9, 112, 5000), (120, 10, 120, 6000)])
 def test_rows2_matches_packed_and_oracle(words_gen, coracle, n, K, ld, C):
+    from vrpms_amd.core import VrpmsError
     ctx = words_gen
     inst = synth.cvrp(n, K, seed=n)
     P = synth.random_perms(C, inst.n, seed=K, ld=ld)
-    got = {}
-    for gen in (0, 1, 2):    # rows2, eval_cvrp_packed, words2 reading the rows in place
-        ctx.set_words_kernel(gen)
-        got[gen] = check_batch(ctx, coracle, inst, P, n=inst.n, objective=n % 2, expect_path=0)
-    np.testing.assert_array_equal(got[0], got[1])
-    np.testing.assert_array_equal(got[0], got[2])
+    ctx.set_words_kernel(1)         # eval_cvrp_packed
+    ref = check_batch(ctx, coracle, inst, P, n=inst.n, objective=n % 2, expect_path=0)
+    ctx.set_words_kernel(0)
+    for cfg in range(6):            # auto, then every forced (CW, ILP)
+        ctx.set_rows_config(cfg)
+        try:
+            got = check_batch(ctx, coracle, inst, P, n=inst.n, objective=n % 2, expect_path=0)
+        except VrpmsError as e:     # a forced tile that does not fit is refused, never wrong
+            assert cfg > 0 and "does not fit" in str(e)
+            continue
+        np.testing.assert_array_equal(got, ref)
 
 
 @pytest.mark.parametrize("ilp,la", [(1, 1), (2, 1), (1, 2), (2, 2)])
@@ -318,6 +326,6 @@ def test_rows2_mixed_exhaustion(words_gen, coracle, n, ld, slack):
     ctx = words_gen
     inst = synth.cvrp(n, 8 if n > 50 else 3, seed=n + 1, slack=slack)
     P = synth.random_perms(6001, inst.n, seed=3, ld=ld)
-    for gen in (0, 2):
-        ctx.set_words_kernel(gen)
+    for cfg in range(6):
+        ctx.set_rows_config(cfg)
         check_batch(ctx, coracle, inst, P, n=inst.n, expect_path=0)

@@ -165,6 +165,22 @@ def test_c_tsp_batch_matches_python_replay(coracle, kind):
     assert tours.tolist() == rt and [int(k) for k in keys] == rk
 
 
+@pytest.mark.parametrize("kind", ["cvrp", "tsp"])
+def test_c_bf_matches_python_replay(coracle, kind):
+    from oracle import search
+    if kind == "cvrp":
+        inst = synth.cvrp(7, 3, seed=8, slack=0.9)
+        kw = dict(demand=inst.demand, capacities=inst.capacities, start_times=inst.start_times)
+    else:
+        inst = synth.Instance("t7", synth.tsp20(1).durations[:, :8, :8], None, None,
+                              np.array([0]), "tsp")
+        kw = dict(start_times=inst.start_times, problem=0)
+    sc = search.Scorer(inst.durations, inst.demand, inst.capacities, inst.start_times,
+                       inst.problem)
+    assert coracle.bf(inst.durations, 7, **kw) == search.bf(sc, 7)
+    assert coracle.bf(inst.durations, 7, 33, 4000, **kw) == search.bf(sc, 7, 33, 4000)
+
+
 def test_accept_threshold_tracks_exp():
     from oracle import search
     for dp in [1, 5, 37, 400, 2000]:

@@ -366,6 +366,26 @@ def test_bf_matches_oracle(ctx, name, maker):
     assert scorer(sub)(tour) == best[0]
 
 
+@pytest.mark.parametrize("problem", ["cvrp", "tsp"])
+def test_bf_n11_matches_c_restatement(ctx, coracle, problem):
+    """The largest brute force the C restatement finishes in about a second
+    (11! = 39.9 M tours): the full range and a ragged sub-range."""
+    import math
+    from vrpms_amd.core import CVRP, TSP
+    if problem == "cvrp":
+        inst = synth.cvrp(11, 3, seed=0)
+        ctx.set_instance(CVRP, inst.durations, inst.demand, inst.capacities, inst.start_times)
+        kw = dict(demand=inst.demand, capacities=inst.capacities, start_times=inst.start_times)
+    else:
+        D = synth.tsp20(5).durations[:, :12, :12]
+        inst = synth.Instance("t11", D, None, None, np.array([0]), "tsp")
+        ctx.set_instance(TSP, inst.durations, start_times=inst.start_times)
+        kw = dict(start_times=inst.start_times, problem=0)
+    full = math.factorial(11)
+    assert ctx.bf_run(11, 0, full) == coracle.bf(inst.durations, 11, 0, full, **kw)
+    assert ctx.bf_run(11, 12345, 9876543) == coracle.bf(inst.durations, 11, 12345, 9876543, **kw)
+
+
 def test_bf_n10_optimum_le_every_sampled_tour(ctx, coracle):
     inst = synth.cvrp(10, 3, seed=9)
     load(ctx, inst)

@@ -28,7 +28,7 @@ def child(path):
     inst = synth.cvrp(100, 8, seed=0)
     ctx.set_instance(CVRP, inst.durations, inst.demand, inst.capacities, inst.start_times)
     C = 16 << 20
-    words = ctx.to_words(bench.make_batch(torch, C, inst.n, ctx.dev, 0), inst.n)
+    words = ctx.to_words(bench.make_batch(ctx, C, inst.n, 0), inst.n)
     keys = torch.empty(C, dtype=torch.int64, device=ctx.dev)
     for _ in range(3):
         ctx.eval_words(words, inst.n, out=keys)

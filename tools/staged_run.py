@@ -22,7 +22,7 @@ dev = ctx.dev
 td = synth.td_cvrp(200, 16, seed=0)
 ctx.set_instance(CVRP, td.durations, td.demand, td.capacities, td.start_times)
 C = 1 << 21
-perms = bench.make_batch(torch, C, td.n, dev, 11)
+perms = bench.make_batch(ctx, C, td.n, 11)
 keys = torch.empty(C, dtype=torch.int64, device=dev)
 for _ in range(reps):
     ctx.eval(perms, out=keys)

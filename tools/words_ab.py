@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """A/B of the LDS-packed scoring kernels on the bench workload (CVRP-100,
-K = 8, C = 16 Mi tours): eval_cvrp_words (gen1) vs eval_cvrp_words2 with one
-or two candidates per lane on the word-interleaved layout, and
-eval_cvrp_packed (gen1) vs eval_cvrp_rows2 on the API's row-major layout.
+K = 8, C = 16 Mi tours): eval_cvrp_words2 with one or two candidates per
+lane and one or two words of gathers in flight on the word-interleaved
+layout, and eval_cvrp_packed vs eval_cvrp_rows2 on the API's row-major
+layout (tools/rows_ab.py sweeps rows2's configurations).  (Round 1 also
+timed the first-generation eval_cvrp_words, since removed.)
 Prints kernel time, evals/s and whether every variant agrees bit for bit
 (and with the C oracle on a sample)."""
 import json
@@ -39,13 +41,12 @@ def main():
     for seed, (n, K) in enumerate([(100, 8), (100, 8), (97, 7), (110, 9), (101, 9)]):
         inst = synth.cvrp(n, K, seed=seed)
         ctx.set_instance(CVRP, inst.durations, inst.demand, inst.capacities, inst.start_times)
-        perms = bench.make_batch(torch, C, inst.n, ctx.dev, seed)
+        perms = bench.make_batch(ctx, C, inst.n, seed)
         words = ctx.to_words(perms, inst.n)
         out = {}
         keys = {}
-        for name, gen, ilp, la in (("words_gen1", 1, 0, 0), ("words2_i1", 0, 1, 1),
-                                   ("words2_i2", 0, 2, 1), ("words2_i1_la2", 0, 1, 2),
-                                   ("words2_i2_la2", 0, 2, 2), ("words2_i3", 0, 3, 1)):
+        for name, gen, ilp, la in (("words2_i1", 0, 1, 1), ("words2_i2", 0, 2, 1),
+                                   ("words2_i1_la2", 0, 1, 2), ("words2_i2_la2", 0, 2, 2)):
             ctx.set_words_kernel(gen)
             ctx.set_words_ilp(ilp)
             ctx.set_words_lookahead(la)
@@ -53,7 +54,7 @@ def main():
             t = timed(lambda: ctx.eval_words(words, inst.n, out=k))
             out[name] = {"ms": t * 1e3, "evals_per_s": C / t}
             keys[name] = k
-        for name, gen in (("rows_packed_gen1", 1), ("rows2", 0), ("rows_direct", 2)):
+        for name, gen in (("rows_packed", 1), ("rows2", 0)):
             ctx.set_words_kernel(gen)
             k = torch.empty(C, dtype=torch.int64, device=ctx.dev)
             t = timed(lambda: ctx.eval(perms, n=inst.n, out=k))
@@ -65,7 +66,7 @@ def main():
         S = 1 << 16
         ref = coracle.eval_batch(inst.durations, perms[:S].cpu().numpy(), inst.demand,
                                  inst.capacities, inst.start_times)[0]
-        out["identical"] = all(bool(torch.equal(keys["words_gen1"], v)) for v in keys.values())
+        out["identical"] = all(bool(torch.equal(keys["words2_i2"], v)) for v in keys.values())
         out["oracle_sample_ok"] = all(bool((v[:S].cpu().numpy().view(np.uint64) == ref).all())
                                       for v in keys.values())
         out["n"], out["K"] = n, K

@@ -20,7 +20,7 @@ ctx = Context(0)
 inst = synth.cvrp(100, 8, seed=0)
 ctx.set_instance(CVRP, inst.durations, inst.demand, inst.capacities, inst.start_times)
 C = 16 << 20
-perms = bench.make_batch(torch, C, inst.n, ctx.dev, 0)
+perms = bench.make_batch(ctx, C, inst.n, 0)
 words = ctx.to_words(perms, inst.n)
 del perms
 ctx.set_words_kernel(gen)

@@ -167,9 +167,13 @@ class Context:
         check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_SPLIT_MODE, int(mode)))
 
     def set_words_kernel(self, gen: int):
-        """LDS-packed kernels: 0 = auto (eval_cvrp_words2 / eval_cvrp_rows2),
-        1 = first generation (eval_cvrp_words / eval_cvrp_packed)."""
+        """Path 0 of vrpms_eval: 0 = auto (eval_cvrp_rows2), 1 = eval_cvrp_packed."""
         check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_WORDS_KERNEL, int(gen)))
+
+    def set_rows_config(self, cfg: int):
+        """eval_cvrp_rows2 (CW, ILP): 0 = auto, 1 = (8, 2), 2 = (16, 1),
+        3 = (4, 2), 4 = (8, 1), 5 = (4, 1)."""
+        check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_ROWS_CONFIG, int(cfg)))
 
     def set_words_ilp(self, ilp: int):
         """Candidates per lane in eval_cvrp_words2: 0 = auto, 1 or 2 force."""

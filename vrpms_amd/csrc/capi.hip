@@ -222,9 +222,15 @@ int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value) {
     return VRPMS_OK;
   }
   if (option == VRPMS_OPT_WORDS_KERNEL) {
-    if (value < 0 || value > 2)
-      return fail(VRPMS_EINVAL, "vrpms_set_option: words kernel must be 0 (auto), 1 or 2");
+    if (value < 0 || value > 1)
+      return fail(VRPMS_EINVAL, "vrpms_set_option: words kernel must be 0 (auto) or 1");
     ctx->opt_words_kernel = value;
+    return VRPMS_OK;
+  }
+  if (option == VRPMS_OPT_ROWS_CONFIG) {
+    if (value < 0 || value > 5)
+      return fail(VRPMS_EINVAL, "vrpms_set_option: rows config must be 0 (auto) or 1..5");
+    ctx->opt_rows_config = value;
     return VRPMS_OK;
   }
   if (option == VRPMS_OPT_WORDS_LOOKAHEAD) {
@@ -234,8 +240,8 @@ int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value) {
     return VRPMS_OK;
   }
   if (option == VRPMS_OPT_WORDS_ILP) {
-    if (value < 0 || value > 3)
-      return fail(VRPMS_EINVAL, "vrpms_set_option: words ILP must be 0 (auto), 1, 2 or 3");
+    if (value < 0 || value > 2)
+      return fail(VRPMS_EINVAL, "vrpms_set_option: words ILP must be 0 (auto), 1 or 2");
     ctx->opt_words_ilp = value;
     return VRPMS_OK;
   }

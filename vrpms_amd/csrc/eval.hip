@@ -13,6 +13,8 @@
 //                     per customer carries the edge, the demand test and
 //                     both depot legs of a route closure.
 //   eval_tsp_staged   static TSP with the (u16/i32) matrix LDS-resident.
+//   (the headline uniform-fleet kernels eval_cvrp_words2 / eval_cvrp_rows2
+//   live in eval_words.hip)
 //   eval_generic      everything else: hour-indexed matrices (H = 24),
 //                     uint16 tours, L2-resident matrices (N >= ~180),
 //                     heterogeneous fleets.
@@ -329,102 +331,6 @@ __global__ __launch_bounds__(BLOCK) void eval_cvrp_packed(PackedArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// Word-interleaved tour layout (VRPMS_LAYOUT_WORDS): uint32 W[ceil(n/4)][C],
-// word w of candidate c holds customers 4w..4w+3 (one byte each).  Lane c's
-// loads of word w are one contiguous 256-B wave access, so tours go straight
-// from HBM to registers: no LDS tile, the LDS holds only the matrix and a
-// workgroup can be 1024 lanes (16 waves per CU instead of 8).
-//
-// Split arithmetic: split.hpp (SplitAcc over the biased prefix-ret matrix).
-// Each lane walks its candidates through an R-deep ring of tour words
-// (R divides the word count when possible, so no slot is wasted); ring slot
-// indices are compile-time constants.
-// ---------------------------------------------------------------------------
-template <int R>
-__global__ __launch_bounds__(1024) void eval_cvrp_words(WordsArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int N = a.f.N;
-  {
-    const uint32_t ebytes = (uint32_t)N * N * 8;
-    const v4u* src = reinterpret_cast<const v4u*>(a.f.pack);
-    v4u* dst = reinterpret_cast<v4u*>(smem);
-    for (uint32_t i = threadIdx.x; i < ebytes / 16; i += blockDim.x) dst[i] = src[i];
-    if ((ebytes & 8u) && threadIdx.x == 0)
-      reinterpret_cast<uint64_t*>(smem)[ebytes / 8 - 1] = a.f.pack[ebytes / 8 - 1];
-  }
-  __syncthreads();
-  const unsigned char* Eb = smem;
-  const uint32_t N8 = 8u * (uint32_t)N;
-  auto gat = [&](uint32_t x, uint32_t y) {
-    return *reinterpret_cast<const uint64_t*>(Eb + (__umul24(x, N8) + (y << 3)));
-  };
-  const int64_t C = a.C;
-  const int n = a.n, nw = (n + 3) >> 2, nfull = n >> 2;
-  const uint32_t smask = a.f.smask, kinc = 1u << a.f.ks, deadacc = a.f.dead;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-
-  const int nblk = nfull / R;                 // blocks of R full words: the fast loop
-  const int64_t last_off = (int64_t)(nw - 1) * C;
-
-  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < C; c += stride) {
-    const uint32_t* Wc = a.words + c;
-    uint32_t ring[R];
-    // every load is unconditional (clamped to the last word) so the
-    // compiler can keep counted vmcnt waits instead of draining to 0
-#pragma unroll
-    for (int u = 0; u < R; ++u) ring[u] = Wc[min((int64_t)u * C, last_off)];
-    int64_t nxt = (int64_t)R * C;               // offset of the next word to fetch
-
-    SplitAcc sa;
-    sa.init(a.f);
-    auto step = [&](uint64_t e) { sa.step(e, smask, kinc, deadacc); };
-    uint32_t wd = ring[0];
-    uint32_t c3 = wd >> 24, lastc = 0;
-    uint64_t e0 = gat(0, wd & 0xffu), e1 = gat(wd & 0xffu, (wd >> 8) & 0xffu),
-             e2 = gat((wd >> 8) & 0xffu, (wd >> 16) & 0xffu), e3 = gat((wd >> 16) & 0xffu, c3);
-    for (int b = 0; b < nblk; ++b) {
-      // only the last block's refills can run past the tour: clamp them there
-      const int64_t cap_off = b + 1 < nblk ? INT64_MAX : last_off;
-#pragma unroll
-      for (int u = 0; u < R; ++u) {
-        ring[u] = Wc[min(nxt, cap_off)];  // word w + R
-        nxt += C;
-        // gathers of the next word, issued before this word's split steps
-        const uint32_t wn = ring[(u + 1) % R];
-        const uint32_t n0 = wn & 0xffu, n1 = (wn >> 8) & 0xffu, n2 = (wn >> 16) & 0xffu,
-                       n3 = wn >> 24;
-        const uint64_t f0 = gat(c3, n0), f1 = gat(n0, n1), f2 = gat(n1, n2), f3 = gat(n2, n3);
-        step(e0);
-        step(e1);
-        step(e2);
-        step(e3);
-        lastc = c3;  // last customer of the word just processed
-        c3 = n3;
-        e0 = f0;
-        e1 = f1;
-        e2 = f2;
-        e3 = f3;
-      }
-    }
-    // ragged tail (n not a multiple of 4R): plain per-word loads and gathers
-    uint32_t prev = lastc;  // last customer of the fast loop (depot if it ran no block)
-    for (int w = nblk * R; w < nw; ++w) {
-      const uint32_t x = Wc[(int64_t)w * C];
-      const int rem = min(4, n - 4 * w);
-      for (int q = 0; q < rem; ++q) {
-        const uint32_t cq = (x >> (8 * q)) & 0xffu;
-        step(gat(prev, cq));
-        prev = cq;
-      }
-    }
-    const TourCost tc = sa.finish(a.f, n);
-    a.keys[c] = tc.key;
-    if (a.sums) a.sums[c] = tc.sum;
-    if (a.maxs) a.maxs[c] = tc.max;
-    if (a.unv) a.unv[c] = tc.unv;
-  }
-}
 // rows (uint8 [C][ld]) -> words (uint32 [ceil(n/4)][C]); one lane per (word, candidate)
 __global__ void rows_to_words_kernel(const uint8_t* __restrict__ rows, int64_t C, int n,
                                      int64_t ld, uint32_t* __restrict__ words) {
@@ -741,14 +647,8 @@ extern "C" int vrpms_eval(vrpms_ctx* ctx, const void* d_perms, int32_t perm_byte
   const int path = vrpms_eval_path(ctx, perm_bytes, ld, d_perms);
   if (path == 0) {
     FastSplit f;
-    if (ctx->opt_words_kernel == 2 && fast_split_params(ctx, n, &f)) {
-      // rows read in place by eval_cvrp_words2 (one dword per word per lane)
-      WordsArgs w{f, static_cast<const uint32_t*>(d_perms), C, n, d_keys, d_sum, d_max, d_unv,
-                  1, (uint32_t)(ld / 4)};
-      return launch_words2(ctx, w, words2_ring(n), s);
-    }
     if (ctx->opt_words_kernel != 1 && fast_split_params(ctx, n, &f) &&
-        rows2_chunk_words(ctx, f) > 0) {
+        rows2_chunk_words(ctx, f, n) > 0) {
       RowsArgs r{f, static_cast<const unsigned char*>(d_perms), C, n, (int)ld,
                  d_keys, d_sum, d_max, d_unv};
       return launch_rows2(ctx, r, s);
@@ -811,27 +711,9 @@ extern "C" int vrpms_eval_words(vrpms_ctx* ctx, const uint32_t* d_words, int64_t
   hipStream_t s = (hipStream_t)stream;
   FastSplit f;
   if (fast_split_params(ctx, n, &f)) {
-    WordsArgs w{f, d_words, C, n, d_keys, d_sum, d_max, d_unv, C, 1u};
-    const size_t lds = ((size_t)in.N * in.N * 8 + 15) & ~(size_t)15;
-    const int per_cu = std::max<int>(1, std::min<int>(2, (int)(ctx->max_lds / lds)));
-    const int64_t blocks = (C + 1023) / 1024;
-    const int grid = (int)std::min<int64_t>(blocks, (int64_t)ctx->num_cus * per_cu);
     // ring depth: the R in [4, 8] that wastes the fewest slots on ceil(n/4) words
-    const int R = words2_ring(n);
-    if (ctx->opt_words_kernel != 1) return launch_words2(ctx, w, R, s);
-    auto go = [&](auto kern) {
-      allow_lds(kern, lds);
-      kern<<<grid, 1024, lds, s>>>(w);
-    };
-    switch (R) {
-      case 4: go(eval_cvrp_words<4>); break;
-      case 5: go(eval_cvrp_words<5>); break;
-      case 6: go(eval_cvrp_words<6>); break;
-      case 7: go(eval_cvrp_words<7>); break;
-      default: go(eval_cvrp_words<8>); break;
-    }
-    VRPMS_HIP(hipGetLastError());
-    return VRPMS_OK;
+    WordsArgs w{f, d_words, C, n, d_keys, d_sum, d_max, d_unv, C, 1u};
+    return launch_words2(ctx, w, words2_ring(n), s);
   }
   EvalArgs a{nullptr, in.N, in.H, in.K, in.dem, in.cap, in.start, d_words, C, n, 0,
              in.objective, d_keys, d_sum, d_max, d_unv};

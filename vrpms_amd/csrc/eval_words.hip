@@ -1,7 +1,7 @@
 // Headline scoring kernels, second generation: eval_cvrp_words2 (word-
 // interleaved tours) and eval_cvrp_rows2 (the API's row-major uint8 tours).
 //
-// Same contract as eval_cvrp_words (eval.hip): uniform-fleet CVRP with the
+// Contract: uniform-fleet CVRP with the
 // biased prefix-ret matrix E (u64 [N][N], split.hpp) resident in LDS, one
 // lane per candidate, bit-exact keys.  What changes is the instruction
 // budget per customer (the kernels are LDS-gather / VALU issue bound,
@@ -19,10 +19,14 @@
 //   * the next word's address math is interleaved into the current word's
 //     split chain (sched_group_barrier), so ds_reads issue well before use.
 //
-// eval_cvrp_rows2 reads the row-major layout directly: a 2048-row tile is
-// staged through LDS CW words at a time (coalesced 32-byte row segments,
-// register prefetch of the next chunk), and each lane then walks its two
-// rows out of LDS with conflict-free ds_read_b32 (odd row stride CW + 1).
+// eval_cvrp_rows2 reads the row-major layout directly: a 1024 * ILP-row tile
+// is staged through LDS CW words at a time (coalesced 4*CW-byte row
+// segments, register prefetch of the next chunk), and each lane then walks
+// its ILP rows out of LDS with conflict-free ds_read_b32 (odd row stride
+// CW + 1).  (Reading the rows in place -- one-dword or 16-byte loads per
+// lane, no staging -- was measured at 10.3 and 12.5-16.0 G evals/s: each
+// wave load touches ~50 128-B lines and the address path, not the LDS,
+// bounds it; tools/rows_ab.py)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -31,170 +35,10 @@
 #include "common.hpp"
 #include "ctx.hpp"
 #include "split.hpp"
+#include "chains.hpp"
 #include "words.hpp"
 
 namespace vrpms {
-
-// VALU per ds_read slot in the interleaved schedule (A/B builds override)
-#ifndef VRPMS_IL_VALU
-#define VRPMS_IL_VALU 10
-#endif
-
-typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) const uint64_t lds_u64;
-typedef __attribute__((address_space(3))) unsigned char lds_uc;
-
-// v_perm selectors: bytes (x, 0, y, 0) of the 8-byte value {hi_word, lo_word}
-constexpr uint32_t kSel01 = 0x0c010c00u;  // (c0, c1) of one word
-constexpr uint32_t kSel12 = 0x0c020c01u;
-constexpr uint32_t kSel23 = 0x0c030c02u;
-constexpr uint32_t kSel30 = 0x0c040c03u;  // (c3 of lo_word = previous, c0 of hi_word = current)
-
-// One customer of the branch-free split (split.hpp SplitAcc::step), with the
-// route-closure value formed by v_and_or_b32 on a VGPR-resident smask.
-// (A v_ashrrev/v_bfi form with VGPR lane masks was measured 1-9 % slower:
-// inline asm makes LLVM pad every use with s_nop.)
-VRPMS_DEV void split_step(SplitAcc& s, uint64_t e, uint32_t vsmask, uint32_t kinc,
-                          uint32_t deadacc) {
-  const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
-  const uint32_t t = s.acc + lo;
-  const bool fits = (int32_t)t < 0;
-  const uint32_t rdm = fits ? 0u : ((s.acc & vsmask) | kinc);
-  s.dsum += rdm;
-  s.dmax = max(s.dmax, rdm);
-  const bool exhausted = (int32_t)s.dsum < 0;
-  s.acc = fits ? t : (exhausted ? deadacc : hi);
-}
-
-// The same step without the fleet-exhaustion test: a customer that does not
-// fit always opens a new route, and dsum's vehicle counter keeps counting.
-// Identical to split_step until the K-th route closes, which sets dsum's
-// sign bit (the counter starts at 2^B - K) -- and that bit stays set, since
-// the counter only grows and 2^B > n keeps it below 2^32.  So a chain whose
-// dsum is non-negative at the end never met the exhaustion branch and its
-// result is exact; the rare chain that did is re-walked with split_step
-// (redo_exact).  Random CVRP-100 giant tours never exhaust the bench's
-// fleet (0 of 200k), and this drops a compare + select per customer.
-VRPMS_DEV void split_step_fast(SplitAcc& s, uint64_t e, uint32_t vsmask, uint32_t kinc) {
-  const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
-  const uint32_t t = s.acc + lo;
-  const bool fits = (int32_t)t < 0;
-  const uint32_t rdm = fits ? 0u : ((s.acc & vsmask) | kinc);
-  s.dsum += rdm;
-  s.dmax = max(s.dmax, rdm);
-  s.acc = fits ? t : hi;
-}
-
-// Copy the packed matrix E into LDS (16-byte vectors + an 8-byte tail).
-VRPMS_DEV void stage_table(const uint64_t* pack, int N, unsigned char* smem) {
-  const uint32_t ebytes = (uint32_t)N * N * 8;
-  const v4u* src = reinterpret_cast<const v4u*>(pack);
-  v4u* dst = reinterpret_cast<v4u*>(smem);
-  for (uint32_t i = threadIdx.x; i < ebytes / 16; i += blockDim.x) dst[i] = src[i];
-  if ((ebytes & 8u) && threadIdx.x == 0)
-    reinterpret_cast<uint64_t*>(smem)[ebytes / 8 - 1] = pack[ebytes / 8 - 1];
-  __syncthreads();
-}
-
-// ILP independent split chains of one lane, fed four customers (one word)
-// at a time.
-template <int ILP>
-struct WordChains {
-  SplitAcc sa[ILP];
-  uint32_t wprev[ILP];  // previous word (its byte 3 is the depot before the first word)
-  uint32_t vsmask, kinc, deadacc, ebase;
-  us2 w8;
-
-  VRPMS_DEV void setup(const FastSplit& f, unsigned char* smem) {
-    ebase = (uint32_t)(uintptr_t)(lds_uc*)smem;
-    w8 = {(unsigned short)(8 * f.N), (unsigned short)8};
-    kinc = 1u << f.ks;
-    deadacc = f.dead;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(vsmask) : "s"(f.smask));
-  }
-  VRPMS_DEV void reset(const FastSplit& f) {
-#pragma unroll
-    for (int i = 0; i < ILP; ++i) {
-      sa[i].init(f);
-      wprev[i] = 0;
-    }
-  }
-  // E entry of the customer pair v_perm laid out as u16 halves; the table's
-  // LDS base rides in the dot's accumulator, so the read needs no add.
-  VRPMS_DEV uint64_t gat(uint32_t pair) const {
-    const uint32_t addr = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, pair), w8, ebase, false);
-    return *(lds_u64*)(uintptr_t)addr;
-  }
-  // the four gathers of word wd (wp = the word before it)
-  VRPMS_DEV void issue(uint64_t (&g)[ILP][4], const uint32_t (&wd)[ILP],
-                       const uint32_t (&wp)[ILP]) const {
-#pragma unroll
-    for (int i = 0; i < ILP; ++i) {
-      g[i][0] = gat(__builtin_amdgcn_perm(wd[i], wp[i], kSel30));
-      g[i][1] = gat(__builtin_amdgcn_perm(wd[i], wd[i], kSel01));
-      g[i][2] = gat(__builtin_amdgcn_perm(wd[i], wd[i], kSel12));
-      g[i][3] = gat(__builtin_amdgcn_perm(wd[i], wd[i], kSel23));
-    }
-  }
-  VRPMS_DEV void steps(const uint64_t (&g)[ILP][4]) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int i = 0; i < ILP; ++i) split_step_fast(sa[i], g[i][q], vsmask, kinc);
-  }
-  // The exact split of one tour, word by word (word(w) returns tour word w):
-  // the slow path for a chain whose fast walk met the fleet limit.
-  template <class WordAt>
-  VRPMS_DEV SplitAcc redo_exact(const FastSplit& f, int n, WordAt word) const {
-    SplitAcc s;
-    s.init(f);
-    uint32_t prev = 0;  // byte 3 = the depot before the first customer
-    const int nw = (n + 3) >> 2;
-    for (int w = 0; w < nw; ++w) {
-      const uint32_t x = word(w);
-      const int rem = min(4, n - 4 * w);
-      if (rem > 0) split_step(s, gat(__builtin_amdgcn_perm(x, prev, kSel30)), vsmask, kinc, deadacc);
-      if (rem > 1) split_step(s, gat(__builtin_amdgcn_perm(x, x, kSel01)), vsmask, kinc, deadacc);
-      if (rem > 2) split_step(s, gat(__builtin_amdgcn_perm(x, x, kSel12)), vsmask, kinc, deadacc);
-      if (rem > 3) split_step(s, gat(__builtin_amdgcn_perm(x, x, kSel23)), vsmask, kinc, deadacc);
-      prev = x;
-    }
-    return s;
-  }
-  // next word's address math (perm + dot2) interleaved into this word's
-  // split chain, each ds_read well after its dot2
-  VRPMS_DEV static void interleave() {
-#if VRPMS_IL_VALU > 0
-#pragma unroll
-    for (int q = 0; q < 4 * ILP; ++q) {
-      __builtin_amdgcn_sched_group_barrier(0x2, VRPMS_IL_VALU, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-#endif
-  }
-  // a partial last word of rem (1..3) customers
-  VRPMS_DEV void partial(const uint32_t (&x)[ILP], int rem) {
-#pragma unroll
-    for (int i = 0; i < ILP; ++i) {
-      const uint32_t sel[3] = {kSel30, kSel01, kSel12};
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
-        if (q < rem)
-          split_step(sa[i], gat(__builtin_amdgcn_perm(x[i], q ? x[i] : wprev[i], sel[q])), vsmask,
-                     kinc, deadacc);
-      wprev[i] = x[i];
-    }
-  }
-};
-
-VRPMS_DEV void store_cost(const FastSplit& f, const SplitAcc& s, int n, int64_t c,
-                          uint64_t* keys, int32_t* sums, int32_t* maxs, int32_t* unv) {
-  const TourCost tc = s.finish(f, n);
-  keys[c] = tc.key;
-  if (sums) sums[c] = tc.sum;
-  if (maxs) maxs[c] = tc.max;
-  if (unv) unv[c] = tc.unv;
-}
 
 template <int R, int ILP, int LA>
 __global__ __launch_bounds__(1024) void eval_cvrp_words2(WordsArgs a) {
@@ -317,18 +161,21 @@ __global__ __launch_bounds__(1024) void eval_cvrp_words2(WordsArgs a) {
   }
 }
 
-// Row-major tours: 2048-row tiles, 128 rows per wave (rows l and l + 64 of
-// the wave's slice on lane l), staged through a wave-private LDS slice CW
-// words per row at a time.  Wave-private staging needs no workgroup
-// barrier: the 16 waves drift apart, so one wave's chunk transition
-// (prefetch wait, LDS store, pipeline refill) overlaps the others' gathers.
-template <int CW>
+// Row-major tours: tiles of 1024 * ILP rows, 64 * ILP rows per wave (rows l
+// + 64 i of the wave's slice on lane l), staged through a wave-private LDS
+// slice CW words per row at a time.  Wave-private staging needs no
+// workgroup barrier: the 16 waves drift apart, so one wave's chunk
+// transition (prefetch wait, LDS store, pipeline refill) overlaps the
+// others' gathers.  (ILP, CW) trades chunk count against candidates per
+// lane within the LDS left beside the packed matrix: (2, 8) = 2048-row tiles
+// of 8-word chunks, (1, 16) = 1024-row tiles of 16-word chunks.
+template <int CW, int ILP>
 __global__ __launch_bounds__(1024) void eval_cvrp_rows2(RowsArgs a) {
-  constexpr int RS = CW + 1;     // LDS row stride in dwords: odd, so b32 reads are conflict-free
-  constexpr int TR = 2048;       // rows per tile
-  constexpr int WR = 128;        // rows per wave
-  constexpr int LPT = 2 * CW;    // staging dwords per lane per chunk
-  constexpr int RPJ = 64 / CW;   // wave-slice rows per staging step
+  constexpr int RS = CW + 1;        // LDS row stride in dwords: odd, so b32 reads are conflict-free
+  constexpr int WR = 64 * ILP;      // rows per wave
+  constexpr int TR = 1024 * ILP;    // rows per tile
+  constexpr int LPT = ILP * CW;     // staging dwords per lane per chunk
+  constexpr int RPJ = 64 / CW;      // wave-slice rows per staging step
   static_assert(64 % CW == 0, "CW must divide 64");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = a.f.N;
@@ -336,7 +183,7 @@ __global__ __launch_bounds__(1024) void eval_cvrp_rows2(RowsArgs a) {
   const uint32_t e16 = ((uint32_t)N * N * 8 + 15u) & ~15u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63u;
   uint32_t* T = reinterpret_cast<uint32_t*>(smem + e16) + wave * WR * RS;
-  WordChains<2> ch;
+  WordChains<ILP> ch;
   ch.setup(a.f, smem);
   const int64_t C = a.C;
   const int n = a.n, nw = (n + 3) >> 2, nfull = n >> 2;
@@ -391,21 +238,23 @@ __global__ __launch_bounds__(1024) void eval_cvrp_rows2(RowsArgs a) {
       if (k < fullch) {
         // software pipeline: the gathers of word j + 1 are issued before
         // the split steps of word j consume theirs
-        uint64_t e[2][4];
-        uint32_t cur[2] = {tw(0, 0), tw(1, 0)};
+        uint64_t e[ILP][4];
+        uint32_t cur[ILP];
+#pragma unroll
+        for (int i = 0; i < ILP; ++i) cur[i] = tw(i, 0);
         ch.issue(e, cur, ch.wprev);
 #pragma unroll
         for (int j = 0; j < CW; ++j) {
-          uint64_t f[2][4];
-          uint32_t nx[2];
+          uint64_t f[ILP][4];
+          uint32_t nx[ILP];
           if (j + 1 < CW) {
-            nx[0] = tw(0, j + 1);
-            nx[1] = tw(1, j + 1);
+#pragma unroll
+            for (int i = 0; i < ILP; ++i) nx[i] = tw(i, j + 1);
             ch.issue(f, nx, cur);
           }
           ch.steps(e);
 #pragma unroll
-          for (int i = 0; i < 2; ++i) {
+          for (int i = 0; i < ILP; ++i) {
             ch.wprev[i] = cur[i];
             if (j + 1 < CW) {
               cur[i] = nx[i];
@@ -419,13 +268,15 @@ __global__ __launch_bounds__(1024) void eval_cvrp_rows2(RowsArgs a) {
 #pragma unroll
         for (int j = 0; j < CW; ++j) {
           const int w = k * CW + j;
-          const uint32_t cur[2] = {w < nw ? tw(0, j) : 0u, w < nw ? tw(1, j) : 0u};
+          uint32_t cur[ILP];
+#pragma unroll
+          for (int i = 0; i < ILP; ++i) cur[i] = w < nw ? tw(i, j) : 0u;
           if (w < nfull) {
-            uint64_t g[2][4];
+            uint64_t g[ILP][4];
             ch.issue(g, cur, ch.wprev);
             ch.steps(g);
-            ch.wprev[0] = cur[0];
-            ch.wprev[1] = cur[1];
+#pragma unroll
+            for (int i = 0; i < ILP; ++i) ch.wprev[i] = cur[i];
           } else if (w < nw) {
             ch.partial(cur, n - 4 * w);
           }
@@ -433,7 +284,7 @@ __global__ __launch_bounds__(1024) void eval_cvrp_rows2(RowsArgs a) {
       }
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < ILP; ++i) {
       const int64_t c = t0 + wave * WR + l + 64 * i;
       if (c < C && (int32_t)ch.sa[i].dsum < 0)  // met the fleet limit: exact re-walk
         ch.sa[i] = ch.redo_exact(a.f, n, [&](int w) {
@@ -478,9 +329,7 @@ int launch_words2(const vrpms_ctx* ctx, const WordsArgs& w, int R, hipStream_t s
   using one = std::integral_constant<int, 1>;
   using two = std::integral_constant<int, 2>;
   const bool la2 = la == 2;
-  using three = std::integral_constant<int, 3>;
-  if (ilp == 3) pick(three{}, one{});  // (ILP3 with two words ahead spills)
-  else if (ilp == 2) la2 ? pick(two{}, two{}) : pick(two{}, one{});
+  if (ilp == 2) la2 ? pick(two{}, two{}) : pick(two{}, one{});
   else la2 ? pick(one{}, two{}) : pick(one{}, one{});
   VRPMS_HIP(hipGetLastError());
   return VRPMS_OK;
@@ -496,28 +345,61 @@ int words2_ring(int n) {
   return R;
 }
 
-int rows2_chunk_words(const vrpms_ctx* ctx, const FastSplit& f) {
-  const size_t e16 = ((size_t)f.N * f.N * 8 + 15) & ~(size_t)15;
-  if (e16 + 2048 * (8 + 1) * 4 <= ctx->max_lds) return 8;
-  if (e16 + 2048 * (4 + 1) * 4 <= ctx->max_lds) return 4;
-  return 0;
+// LDS bytes of an eval_cvrp_rows2<CW, ILP> launch on this instance
+static size_t rows2_lds(const FastSplit& f, int cw, int ilp) {
+  return (((size_t)f.N * f.N * 8 + 15) & ~(size_t)15) + (size_t)1024 * ilp * (cw + 1) * 4;
+}
+
+// (CW, ILP) of eval_cvrp_rows2 for this instance: the configuration with the
+// fewest chunk transitions per tour that fits the LDS, ILP 2 on ties
+// (measured, tools/rows_ab.py); opt = VRPMS_OPT_ROWS_CONFIG forces one.
+static bool rows2_config(const vrpms_ctx* ctx, const FastSplit& f, int n, int* cw, int* ilp) {
+  static const int kCfg[][2] = {{8, 2}, {16, 1}, {4, 2}, {8, 1}, {4, 1}};
+  const int force = ctx->opt_rows_config;
+  if (force > 0) {
+    if (force > 5) return false;
+    *cw = kCfg[force - 1][0];
+    *ilp = kCfg[force - 1][1];
+    return rows2_lds(f, *cw, *ilp) <= ctx->max_lds;
+  }
+  const int nw = (n + 3) / 4;
+  int best = -1, best_chunks = 1 << 30;
+  for (int c = 0; c < 5; ++c) {
+    if (rows2_lds(f, kCfg[c][0], kCfg[c][1]) > ctx->max_lds) continue;
+    const int chunks = (nw + kCfg[c][0] - 1) / kCfg[c][0];
+    if (chunks < best_chunks || (chunks == best_chunks && kCfg[c][1] > kCfg[best][1])) {
+      best = c;
+      best_chunks = chunks;
+    }
+  }
+  if (best < 0) return false;
+  *cw = kCfg[best][0];
+  *ilp = kCfg[best][1];
+  return true;
+}
+
+int rows2_chunk_words(const vrpms_ctx* ctx, const FastSplit& f, int n) {
+  int cw = 0, ilp = 0;
+  return rows2_config(ctx, f, n, &cw, &ilp) ? cw : 0;
 }
 
 int launch_rows2(const vrpms_ctx* ctx, const RowsArgs& r, hipStream_t s) {
-  const int cw = rows2_chunk_words(ctx, r.f);
-  if (cw == 0 || (r.ld & 3) != 0 || ((uintptr_t)r.perms & 3u) != 0)
+  int cw = 0, ilp = 0;
+  if (!rows2_config(ctx, r.f, r.n, &cw, &ilp) || (r.ld & 3) != 0 || ((uintptr_t)r.perms & 3u) != 0)
     return fail(VRPMS_EINVAL, "launch_rows2: tile does not fit LDS or rows unaligned");
-  const size_t e16 = ((size_t)r.f.N * r.f.N * 8 + 15) & ~(size_t)15;
-  const size_t lds = e16 + (size_t)2048 * (cw + 1) * 4;
-  const int64_t tiles = (r.C + 2047) / 2048;
+  const size_t lds = rows2_lds(r.f, cw, ilp);
+  const int64_t tiles = (r.C + 1024 * ilp - 1) / (1024 * ilp);
   const int grid = (int)std::min<int64_t>(tiles, (int64_t)ctx->num_cus);
   auto go = [&](auto kern) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     kern<<<grid, 1024, lds, s>>>(r);
   };
-  if (cw == 8) go(eval_cvrp_rows2<8>);
-  else go(eval_cvrp_rows2<4>);
+  if (cw == 8 && ilp == 2) go(eval_cvrp_rows2<8, 2>);
+  else if (cw == 16) go(eval_cvrp_rows2<16, 1>);
+  else if (cw == 4 && ilp == 2) go(eval_cvrp_rows2<4, 2>);
+  else if (cw == 8) go(eval_cvrp_rows2<8, 1>);
+  else go(eval_cvrp_rows2<4, 1>);
   VRPMS_HIP(hipGetLastError());
   return VRPMS_OK;
 }

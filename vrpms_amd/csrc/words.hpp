@@ -33,8 +33,8 @@ int words2_ring(int n);
 
 // Row-major uint8 tours (the vrpms_eval layout, perm_bytes == 1): candidate
 // c at perms[c * ld .. c * ld + n), ld % 4 == 0, perms 16-byte aligned.
-// eval_cvrp_rows2 stages 2048-row tiles through LDS in chunks of CW words,
-// so the API layout needs no transpose.
+// eval_cvrp_rows2 stages 1024 * ILP-row tiles through LDS in chunks of CW
+// words, so the API layout needs no transpose.
 struct RowsArgs {
   FastSplit f;
   const unsigned char* perms;
@@ -50,11 +50,12 @@ struct RowsArgs {
 // Launch eval_cvrp_words2 with ring depth R (4..8) on stream s.
 int launch_words2(const vrpms_ctx* ctx, const WordsArgs& w, int R, hipStream_t s);
 
-// Words per row per LDS stage eval_cvrp_rows2 can use beside the packed
-// matrix: 8, 4, or 0 when no tile fits the LDS budget.
-int rows2_chunk_words(const vrpms_ctx* ctx, const FastSplit& f);
+// Words per row per LDS stage eval_cvrp_rows2 uses beside the packed
+// matrix for tours of n customers (16, 8 or 4), or 0 when no tile fits.
+int rows2_chunk_words(const vrpms_ctx* ctx, const FastSplit& f, int n);
 
 // Launch eval_cvrp_rows2 on stream s (caller checked rows2_chunk_words > 0).
 int launch_rows2(const vrpms_ctx* ctx, const RowsArgs& r, hipStream_t s);
+
 
 }  // namespace vrpms

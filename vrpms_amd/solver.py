@@ -31,7 +31,10 @@ from . import runners
 from .core import CVRP, OBJ_MAX, OBJ_SUM, TSP, Context
 
 ALGORITHMS = ("bf", "ga", "sa", "aco")
-BF_MAX_CUSTOMERS = 11
+# exhaustive search over n! giant tours: 13! = 6.2 G tours is ~0.1 s at the
+# measured ~64 G evals/s of bf_kernel on one MI355X (bench "search.bf");
+# vrpms_bf_run itself accepts n <= 15 (nibble-packed tours)
+BF_MAX_CUSTOMERS = 13
 
 
 @dataclass
