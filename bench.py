@@ -368,19 +368,29 @@ def search_lines(ctx, torch, dev, r_gather, seed=0):
         torch.cuda.synchronize(dev)
         return (time.perf_counter() - t0) / reps, e0.elapsed_time(e1) * 1e-3 / reps
 
-    # GA: 64 islands x 256 (randomPermutationCount), 10 generations per call
-    islands_, pop, gens = 64, 256, 10
-    ga = runners.GARunner(ctx, inst.n, islands=islands_, pop=pop, seed=seed, gens_per_epoch=gens)
-    wall, dev_s = timed(ga.epoch, 5)
-    children = islands_ * pop * gens
+    # GA: 256 islands x 256 (randomPermutationCount) -- one island per CU --
+    # 20 generations per call, fused (one workgroup per island for the whole
+    # call) and, for comparison, the three-launch path on the same islands
+    islands_, pop = 256, 256
+    ga_out = {}
+    for mode, gens, reps in ((0, 20, 5), (2, 5, 3)):
+        ctx.set_ga_fused(mode)
+        ga = runners.GARunner(ctx, inst.n, islands=islands_, pop=pop, seed=seed,
+                              gens_per_epoch=gens)
+        wall, dev_s = timed(ga.epoch, reps)
+        children = islands_ * pop * gens
+        ga_out["fused" if mode == 0 else "three_kernel"] = {
+            "generations_per_call": gens, "generations_per_s": gens / dev_s,
+            "child_evals_per_s": children / dev_s, "wall_generations_per_s": gens / wall,
+            "lds_gather_frac_whole_generation": children / dev_s * G / r_gather}
+        best = ga.best()[0]
+        del ga
+    ctx.set_ga_fused(0)
     out["ga"] = {"workload": "cfg2 CVRP-100, island GA", "islands": islands_, "pop": pop,
-                 "generations_per_call": gens, "scoring_kernel": "eval_cvrp_words2",
-                 "generations_per_s": gens / dev_s, "child_evals_per_s": children / dev_s,
-                 "wall_generations_per_s": gens / wall,
-                 "lds_gather_frac_whole_generation": children / dev_s * G / r_gather,
-                 "best": {"duration_sum": (ga.best()[0] >> 28) & (2**28 - 1),
-                          "unvisited": ga.best()[0] >> 56}}
-    del ga
+                 "kernel": "ga_fused_kernel (breed + score + select per island in LDS)",
+                 **ga_out, "speedup_fused": ga_out["fused"]["child_evals_per_s"]
+                 / ga_out["three_kernel"]["child_evals_per_s"],
+                 "best": {"duration_sum": (best >> 28) & (2**28 - 1), "unvisited": best >> 56}}
     # ACO: 64 colonies x 64 ants (one wavefront per ant), 5 iterations per epoch
     colonies, ants, iters = 64, 64, 5
     aco = runners.ACORunner(ctx, inst.n, colonies=colonies, ants=ants, seed=seed,

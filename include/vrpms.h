@@ -128,6 +128,10 @@ int vrpms_eval_path(vrpms_ctx* ctx, int32_t perm_bytes, int64_t ld, const void* 
  *   lane): 0 = auto (fewest chunks that fit the LDS), 1 = (8, 2),
  *   2 = (16, 1), 3 = (4, 2), 4 = (8, 1), 5 = (4, 1); A/B. */
 #define VRPMS_OPT_ROWS_CONFIG 6
+/*   VRPMS_OPT_GA_FUSED: 0 = auto (the fused one-workgroup-per-island GA
+ *   kernel whenever the island fits the LDS), 2 = force the three-kernel
+ *   path (breed / score / select launches per generation); A/B. */
+#define VRPMS_OPT_GA_FUSED 7
 int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value);
 
 /* Decode ONE giant tour into the result dict of api/vrp/ga/index.py:49-53
@@ -183,9 +187,12 @@ typedef struct {
 } vrpms_ga_params;
 
 /* d_pop [islands][pop][n] and d_keys [islands][pop] in/out (keys must
- * score d_pop on entry, e.g. by vrpms_eval).  For CVRP with N <= 256 (the
- * packed-LDS instances) the breed kernel emits the children in the
- * word-interleaved layout and eval_cvrp_words2 scores them. */
+ * score d_pop on entry, e.g. by vrpms_eval).  For uniform-fleet CVRP on the
+ * packed-LDS instances (N <= 128) one 1024-lane workgroup per island runs
+ * all `generations` in LDS (ga_fused.hip) when the island fits beside the
+ * matrix (CVRP-100: pop <= 256); otherwise each generation is breed ->
+ * score -> select launches, the children emitted in the word-interleaved
+ * layout and scored by eval_cvrp_words2 when that kernel applies. */
 int vrpms_ga_generation(vrpms_ctx* ctx, const vrpms_ga_params* p, uint16_t* d_pop,
                         uint64_t* d_keys, int32_t n, void* stream);
 

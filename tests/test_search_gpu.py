@@ -394,3 +394,60 @@ def test_bf_n10_optimum_le_every_sampled_tour(ctx, coracle):
     keys = coracle.eval_batch(inst.durations, P, inst.demand, inst.capacities, inst.start_times)[0]
     assert k <= int(keys.min())
     assert scorer(inst)(search.unrank(r, 10)) == k
+
+
+GA_FUSED_CASES = [
+    # (n, K, slack, islands, pop, gens, pmut): ragged tours, tight fleets
+    # (exact re-walks), odd population sizes, the cfg-2 size, and a large
+    # island of a small instance
+    (100, 8, 1.1, 3, 64, 6, 0.3),
+    (97, 7, 1.03, 2, 50, 5, 0.5),
+    (30, 3, 0.8, 5, 33, 7, 0.9),
+    (1, 1, 1.0, 2, 4, 3, 0.5),
+    (2, 2, 1.0, 2, 6, 4, 0.5),
+    (19, 2, 1.0, 2, 1000, 3, 0.2),
+]
+
+
+@pytest.mark.parametrize("n,K,slack,islands,pop,gens,pmut", GA_FUSED_CASES)
+def test_ga_fused_equals_three_kernel_path(ctx, n, K, slack, islands, pop, gens, pmut):
+    """The fused one-workgroup-per-island GA (ga_fused.hip) and the
+    breed / score / select launches produce identical populations and keys."""
+    torch = torch_()
+    inst = synth.cvrp(n, K, seed=n + pop, slack=slack)
+    load(ctx, inst)
+    P = synth.random_perms(islands * pop, n, seed=pop).astype(np.int16)
+    out = []
+    for mode in (0, 2):
+        ctx.set_ga_fused(mode)
+        try:
+            dpop = torch.from_numpy(P.reshape(islands, pop, n).copy()).to(ctx.dev)
+            keys = ctx.eval(dpop.view(islands * pop, n)).view(islands, pop)
+            ctx.ga_generation(dpop, keys, generations=gens, pmut=pmut, seed=7 + n, gen0=3)
+            out.append((dpop.cpu().numpy(), u64(keys)))
+        finally:
+            ctx.set_ga_fused(0)
+    assert (out[0][0] == out[1][0]).all()
+    assert out[0][1] == out[1][1]
+    flat = out[0][0].reshape(-1, n)
+    assert all(sorted(r) == list(range(1, n + 1)) for r in flat[:: max(1, len(flat) // 50)])
+
+
+def test_ga_fused_small_matches_python_oracle(ctx):
+    """Fused kernel vs the pure-Python GA replay, several generations."""
+    torch = torch_()
+    inst = synth.cvrp(13, 3, seed=2, slack=0.9)
+    load(ctx, inst)
+    islands, pop, n = 3, 10, inst.n
+    P = synth.random_perms(islands * pop, n, seed=4).astype(np.int16)
+    dpop = torch.from_numpy(P.reshape(islands, pop, n).copy()).to(ctx.dev)
+    keys = ctx.eval(dpop.view(-1, n)).view(islands, pop)
+    sc = scorer(inst)
+    rpop = [[list(r) for r in P.reshape(islands, pop, n)[i]] for i in range(islands)]
+    rkeys = [[sc(t) for t in rpop[i]] for i in range(islands)]
+    pm = min(int(round(0.6 * 2**32)), 2**32 - 1)
+    for g in range(6):
+        rpop, rkeys = search.ga_generation(sc, rpop, rkeys, 55, g, pm)
+    ctx.ga_generation(dpop, keys, generations=6, pmut=0.6, seed=55, gen0=0)
+    assert dpop.cpu().numpy().tolist() == rpop
+    assert u64(keys) == [k for ks in rkeys for k in ks]

@@ -87,8 +87,15 @@ def test_solve_vrp_problem_default_and_bf_errors():
     assert set(r) == {"tour", "total_time", "unvisited", "date"}
     assert r["tour"][0] == r["tour"][-1] == 0 and sorted(r["tour"][1:-1]) == list(range(1, 15))
     assert r["unvisited"] == []
+    cap = solver.BF_MAX_CUSTOMERS
     with pytest.raises(ValueError, match="brute force"):
-        solver.solve_tsp("bf", tsp_matrix(14).tolist(), list(range(1, 14)), 0)
+        solver.solve_tsp("bf", tsp_matrix(cap + 2).tolist(), list(range(1, cap + 2)), 0)
+    # at the cap (13! = 6.2 G tours) the exhaustive optimum is below any SA tour
+    D = tsp_matrix(cap + 1).tolist()
+    bf = solver.solve_tsp("bf", D, list(range(1, cap + 1)), 0)
+    sa = solver.solve_tsp("sa", D, list(range(1, cap + 1)), 0, chains=64, steps=500)
+    assert sorted(bf["vehicle"][1:-1]) == list(range(1, cap + 1))
+    assert bf["duration"] <= sa["duration"]
     with pytest.raises(ValueError, match="unknown algorithm"):
         solver.solve_tsp("tabu", tsp_matrix().tolist(), [1, 2], 0)
 

@@ -30,6 +30,7 @@ OPT_WORDS_KERNEL = 3
 OPT_WORDS_ILP = 4
 OPT_WORDS_LOOKAHEAD = 5
 OPT_ROWS_CONFIG = 6
+OPT_GA_FUSED = 7
 OBJ_SUM = 0
 OBJ_MAX = 1
 INJECT_WORST = 0

@@ -170,6 +170,10 @@ class Context:
         """Path 0 of vrpms_eval: 0 = auto (eval_cvrp_rows2), 1 = eval_cvrp_packed."""
         check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_WORDS_KERNEL, int(gen)))
 
+    def set_ga_fused(self, mode: int):
+        """0 = auto (fused one-workgroup-per-island GA when it fits), 2 = three kernels."""
+        check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_GA_FUSED, int(mode)))
+
     def set_rows_config(self, cfg: int):
         """eval_cvrp_rows2 (CW, ILP): 0 = auto, 1 = (8, 2), 2 = (16, 1),
         3 = (4, 2), 4 = (8, 1), 5 = (4, 1)."""

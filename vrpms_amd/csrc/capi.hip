@@ -227,6 +227,12 @@ int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value) {
     ctx->opt_words_kernel = value;
     return VRPMS_OK;
   }
+  if (option == VRPMS_OPT_GA_FUSED) {
+    if (value != 0 && value != 2)
+      return fail(VRPMS_EINVAL, "vrpms_set_option: GA fused must be 0 (auto) or 2 (three kernels)");
+    ctx->opt_ga_fused = value;
+    return VRPMS_OK;
+  }
   if (option == VRPMS_OPT_ROWS_CONFIG) {
     if (value < 0 || value > 5)
       return fail(VRPMS_EINVAL, "vrpms_set_option: rows config must be 0 (auto) or 1..5");

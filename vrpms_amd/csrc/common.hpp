@@ -128,6 +128,13 @@ VRPMS_DEV uint64_t wave_argmin_lane(uint64_t key, int& who) {
   return m;
 }
 
+// Order this wavefront's LDS (and global) accesses before / after this point
+// across its lanes (a wave's own memory operations need no workgroup barrier).
+VRPMS_DEV void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 // x of lane `src` (a wave-uniform index) broadcast through v_readlane.
 VRPMS_DEV int wave_bcast(int x, int src) { return __builtin_amdgcn_readlane(x, src); }
 

@@ -351,8 +351,12 @@ static size_t rows2_lds(const FastSplit& f, int cw, int ilp) {
 }
 
 // (CW, ILP) of eval_cvrp_rows2 for this instance: the configuration with the
-// fewest chunk transitions per tour that fits the LDS, ILP 2 on ties
-// (measured, tools/rows_ab.py); opt = VRPMS_OPT_ROWS_CONFIG forces one.
+// fewest chunk transitions per tour that fits the LDS, one candidate per
+// lane on ties.  Measured on CVRP-100, 16 Mi tours (tools/rows_ab.py,
+// profiles/round2_rows_ab.log): (16, 1) 32.1, (8, 1) 30.4, (8, 2) 23.0,
+// (4, 2) 16.6 G evals/s -- fewer chunk restarts beat a second chain per
+// lane, which also doubles the staging registers.  VRPMS_OPT_ROWS_CONFIG
+// forces one.
 static bool rows2_config(const vrpms_ctx* ctx, const FastSplit& f, int n, int* cw, int* ilp) {
   static const int kCfg[][2] = {{8, 2}, {16, 1}, {4, 2}, {8, 1}, {4, 1}};
   const int force = ctx->opt_rows_config;
@@ -367,7 +371,7 @@ static bool rows2_config(const vrpms_ctx* ctx, const FastSplit& f, int n, int* c
   for (int c = 0; c < 5; ++c) {
     if (rows2_lds(f, kCfg[c][0], kCfg[c][1]) > ctx->max_lds) continue;
     const int chunks = (nw + kCfg[c][0] - 1) / kCfg[c][0];
-    if (chunks < best_chunks || (chunks == best_chunks && kCfg[c][1] > kCfg[best][1])) {
+    if (chunks < best_chunks || (chunks == best_chunks && kCfg[c][1] < kCfg[best][1])) {
       best = c;
       best_chunks = chunks;
     }

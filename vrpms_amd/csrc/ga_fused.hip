@@ -1,0 +1,308 @@
+// Fused GA island kernel: one 1024-lane workgroup per island runs whole
+// generations without leaving the CU (the reference's GA slot,
+// api/vrp/ga/index.py:48-53, knobs api/parameters.py:18-23).
+//
+// Same trajectory as the three-kernel path of vrpms_ga_generation
+// (ga_breed_kernel -> eval_cvrp_words2 -> ga_select_kernel, oracle/search.py
+// ga_generation): binary tournaments, OX1, Philox-gated mutation, (mu +
+// lambda) survivors by (key, index).  What changes is where the data lives:
+//
+//   * the packed prefix-ret matrix E, the island's parents AND children
+//     (2P uint8 rows) and every key sit in LDS for the whole call;
+//   * survivors are never copied: slot i of the population points at one
+//     of the 2P rows (prow), and the next children are written into the P
+//     rows no survivor holds (crow, rebuilt by a ballot compaction);
+//   * children are scored in place by the headline kernel's split step
+//     (chains.hpp: v_perm + v_dot2 gather addressing, branch-free split,
+//     exact re-walk of the rare lanes that meet the fleet limit);
+//   * a mutation is applied by all 64 lanes through moved_index (one LDS
+//     copy + one gathered write) instead of a serial lane-0 loop.
+//
+// The launch count per call drops from 3 per generation to 1, and no tour
+// crosses HBM between generations.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "chains.hpp"
+#include "common.hpp"
+#include "ctx.hpp"
+#include "sort.hpp"
+#include "split.hpp"
+#include "tour.hpp"
+
+namespace vrpms {
+
+struct GaFusedArgs {
+  FastSplit f;
+  int islands, pop, n, gens, M;
+  uint32_t pmut, seed_lo, seed_hi;
+  uint64_t gen0;
+  uint32_t rs;  // LDS bytes per tour row (multiple of 4, rs / 4 odd)
+  uint32_t off_rows, off_pk, off_ck, off_prow, off_crow, off_sk, off_si, off_used, off_tmp,
+      off_bits;
+  uint16_t* pop_tours;  // [islands][pop][n] in/out
+  uint64_t* pop_keys;   // [islands][pop] in/out
+};
+
+struct GaFusedLayout {
+  size_t bytes;
+  GaFusedArgs a;
+};
+
+static size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// LDS carve of the fused kernel for (N, n, P); bytes > max_lds: does not fit.
+static GaFusedLayout ga_fused_layout(int N, int n, int P) {
+  GaFusedLayout L{};
+  uint32_t rs = ((uint32_t)n + 3u) & ~3u;
+  if (((rs / 4) & 1u) == 0) rs += 4;  // odd dword stride: rows spread over the banks
+  int M = 1;
+  while (M < 2 * P) M <<= 1;
+  const uint32_t words = ((uint32_t)N + 31u) / 32u;
+  size_t off = al16((size_t)N * N * 8);
+  GaFusedArgs& a = L.a;
+  a.rs = rs;
+  a.M = M;
+  a.off_rows = (uint32_t)off;   off = al16(off + (size_t)2 * P * rs);
+  a.off_pk = (uint32_t)off;     off = al16(off + (size_t)P * 8);
+  a.off_ck = (uint32_t)off;     off = al16(off + (size_t)P * 8);
+  a.off_prow = (uint32_t)off;   off = al16(off + (size_t)P * 2);
+  a.off_crow = (uint32_t)off;   off = al16(off + (size_t)P * 2);
+  a.off_sk = (uint32_t)off;     off = al16(off + (size_t)M * 8);
+  a.off_si = (uint32_t)off;     off = al16(off + (size_t)M * 4);
+  a.off_used = (uint32_t)off;   off = al16(off + (size_t)16 * words * 4);
+  a.off_tmp = (uint32_t)off;    off = al16(off + (size_t)16 * rs);
+  a.off_bits = (uint32_t)off;   off = al16(off + ((size_t)2 * P / 32 + 1) * 4);
+  L.bytes = off;
+  return L;
+}
+
+// Tournament of two: the lower (key, index) wins (as ga_breed_kernel).
+VRPMS_DEV int tourney2(const uint64_t* keys, int pop, uint32_t r0, uint32_t r1) {
+  const int x = (int)(r0 % (uint32_t)pop), y = (int)(r1 % (uint32_t)pop);
+  const uint64_t kx = keys[x], ky = keys[y];
+  return (ky < kx || (ky == kx && y < x)) ? y : x;
+}
+
+__global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int P = a.pop, n = a.n, island = blockIdx.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t rs = a.rs;
+  const uint32_t words = ((uint32_t)a.f.N + 31u) / 32u;
+  uint8_t* rows = smem + a.off_rows;
+  uint64_t* pk = reinterpret_cast<uint64_t*>(smem + a.off_pk);
+  uint64_t* ck = reinterpret_cast<uint64_t*>(smem + a.off_ck);
+  uint16_t* prow = reinterpret_cast<uint16_t*>(smem + a.off_prow);
+  uint16_t* crow = reinterpret_cast<uint16_t*>(smem + a.off_crow);
+  uint64_t* sk = reinterpret_cast<uint64_t*>(smem + a.off_sk);
+  uint32_t* si = reinterpret_cast<uint32_t*>(smem + a.off_si);
+  uint32_t* used = reinterpret_cast<uint32_t*>(smem + a.off_used) + wave * words;
+  uint8_t* tmp = smem + a.off_tmp + wave * rs;
+  uint32_t* bits = reinterpret_cast<uint32_t*>(smem + a.off_bits);
+  uint16_t* gpop = a.pop_tours + (int64_t)island * P * n;
+  uint64_t* gkeys = a.pop_keys + (int64_t)island * P;
+
+  // rows zeroed (tour tails stay 0 for the word reads), parents loaded
+  for (uint32_t i = threadIdx.x; i < (uint32_t)P * rs / 2; i += blockDim.x)
+    reinterpret_cast<uint32_t*>(rows)[i] = 0u;
+  stage_table(a.f.pack, a.f.N, smem);  // ends with a barrier
+  for (int64_t e = threadIdx.x; e < (int64_t)P * n; e += blockDim.x) {
+    const int i = (int)(e / n), q = (int)(e % n);
+    rows[(uint32_t)i * rs + q] = (uint8_t)gpop[e];
+  }
+  for (int i = threadIdx.x; i < P; i += blockDim.x) {
+    prow[i] = (uint16_t)i;
+    crow[i] = (uint16_t)(P + i);
+    pk[i] = gkeys[i];
+  }
+  __syncthreads();
+
+  WordChains<1> ch;
+  ch.setup(a.f, smem);
+  const int nfull = n >> 2;
+  for (int g = 0; g < a.gens; ++g) {
+    const uint64_t gen = a.gen0 + (uint64_t)g;
+    // ---- breed: one child per wavefront at a time --------------------------
+    for (int child = wave; child < P; child += 16) {
+      const uint32_t cid = (uint32_t)(island * P + child);
+      const u32x4 r = philox((uint32_t)gen, (uint32_t)(gen >> 32), cid, 0u, a.seed_lo, a.seed_hi);
+      const u32x4 r2 = philox((uint32_t)gen, (uint32_t)(gen >> 32), cid, 1u, a.seed_lo, a.seed_hi);
+      const int pa = tourney2(pk, P, r.x, r.y), pb = tourney2(pk, P, r.z, r.w);
+      const uint8_t* A = rows + (uint32_t)prow[pa] * rs;
+      const uint8_t* B = rows + (uint32_t)prow[pb] * rs;
+      uint8_t* out = rows + (uint32_t)crow[child] * rs;
+      if (n < 2) {
+        for (int q = lane; q < n; q += 64) out[q] = A[q];
+        continue;
+      }
+      // OX1: out[lo..hi] = A[lo..hi]; the rest, from position hi+1 (wrapping),
+      // are B's genes from B[hi+1] onwards (wrapping) not yet used
+      int lo = (int)(r2.x % (uint32_t)n), hi = (int)(r2.y % (uint32_t)n);
+      if (lo > hi) {
+        const int t = lo;
+        lo = hi;
+        hi = t;
+      }
+      for (uint32_t w = lane; w < words; w += 64) used[w] = 0u;
+      wave_sync();
+      for (int q = lo + lane; q <= hi; q += 64) {
+        const uint32_t gq = A[q];
+        out[q] = (uint8_t)gq;
+        atomicOr(&used[gq >> 5], 1u << (gq & 31u));
+      }
+      wave_sync();
+      const int rest = n - (hi - lo + 1);
+      int filled = 0;
+      for (int base = 0; base < n; base += 64) {
+        const int q = base + lane;
+        uint32_t gq = 0;
+        bool keep = false;
+        if (q < n) {
+          int src = hi + 1 + q;
+          src = src >= n ? src - n : src;
+          gq = B[src];
+          keep = ((used[gq >> 5] >> (gq & 31u)) & 1u) == 0u;
+        }
+        const uint64_t ball = __ballot(keep);
+        const int before = __popcll(ball & ((1ull << lane) - 1ull));
+        if (keep) {
+          const int slot = filled + before;
+          if (slot < rest) {
+            int dst = hi + 1 + slot;
+            dst = dst >= n ? dst - n : dst;
+            out[dst] = (uint8_t)gq;
+          }
+        }
+        filled += __popcll(ball);
+      }
+      wave_sync();
+      if (r2.z < a.pmut) {  // wave-uniform: one move, applied by all lanes
+        const Move m = decode_move(r2.w, r.x ^ r2.x, r.y ^ r2.y, n);
+        for (int q = lane; q < n; q += 64) tmp[q] = out[q];
+        wave_sync();
+        for (int q = lane; q < n; q += 64) out[q] = tmp[moved_index(q, m)];
+        wave_sync();
+      }
+    }
+    __syncthreads();
+    // ---- score the P children in place ---------------------------------------
+    for (int t = threadIdx.x; t < P; t += blockDim.x) {
+      const uint32_t* rw = reinterpret_cast<const uint32_t*>(rows + (uint32_t)crow[t] * rs);
+      ch.reset(a.f);
+      uint64_t e[1][4];
+      if (nfull > 0) {
+        const uint32_t w0[1] = {rw[0]};
+        ch.issue(e, w0, ch.wprev);
+      }
+      for (int w = 0; w < nfull; ++w) {
+        const uint32_t cur[1] = {rw[w]};
+        uint64_t nx[1][4];
+        const bool more = w + 1 < nfull;
+        if (more) {
+          const uint32_t wn[1] = {rw[w + 1]};
+          ch.issue(nx, wn, cur);
+        }
+        ch.steps(e);
+        ch.wprev[0] = cur[0];
+        if (more)
+#pragma unroll
+          for (int x = 0; x < 4; ++x) e[0][x] = nx[0][x];
+      }
+      if (n & 3) {
+        const uint32_t x[1] = {rw[nfull]};
+        ch.partial(x, n & 3);
+      }
+      if ((int32_t)ch.sa[0].dsum < 0)  // met the fleet limit: exact re-walk
+        ch.sa[0] = ch.redo_exact(a.f, n, [&](int w) { return rw[w]; });
+      ck[t] = ch.sa[0].finish(a.f, n).key;
+    }
+    __syncthreads();
+    // ---- (mu + lambda) survivors by (key, index) -----------------------------
+    for (int i = threadIdx.x; i < a.M; i += blockDim.x) {
+      sk[i] = i < P ? pk[i] : (i < 2 * P ? ck[i - P] : ~0ull);
+      si[i] = (uint32_t)i;
+    }
+    __syncthreads();
+    block_sort_pairs(sk, si, a.M);
+    uint16_t nrow[2] = {0, 0};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = threadIdx.x + 1024 * k;
+      if (i < P) nrow[k] = si[i] < (uint32_t)P ? prow[si[i]] : crow[si[i] - P];
+    }
+    for (uint32_t w = threadIdx.x; w <= (uint32_t)(2 * P) / 32; w += blockDim.x) bits[w] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = threadIdx.x + 1024 * k;
+      if (i < P) {
+        prow[i] = nrow[k];
+        pk[i] = sk[i];
+        atomicOr(&bits[nrow[k] >> 5], 1u << (nrow[k] & 31u));
+      }
+    }
+    __syncthreads();
+    // the P rows no survivor holds, in row order, take the next children
+    if (wave == 0) {
+      const int nwords = (2 * P + 31) / 32;  // <= 64 (P <= 1024)
+      uint32_t fr = 0;
+      if (lane < nwords) {
+        fr = ~bits[lane];
+        const int tail = 2 * P - 32 * lane;
+        if (tail < 32) fr &= (1u << tail) - 1u;
+      }
+      const int cnt = __popc(fr);
+      int incl = cnt;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += o;
+      }
+      int slot = incl - cnt;
+      while (fr) {
+        const int b = __ffs((int)fr) - 1;
+        crow[slot++] = (uint16_t)(32 * lane + b);
+        fr &= fr - 1u;
+      }
+    }
+    __syncthreads();
+  }
+  for (int64_t e = threadIdx.x; e < (int64_t)P * n; e += blockDim.x) {
+    const int i = (int)(e / n), q = (int)(e % n);
+    gpop[e] = rows[(uint32_t)prow[i] * rs + q];
+  }
+  for (int i = threadIdx.x; i < P; i += blockDim.x) gkeys[i] = pk[i];
+}
+
+// Launch the fused kernel when the island fits the LDS beside the packed
+// matrix; returns 1 if launched, 0 if the caller must use the three-kernel
+// path, < 0 on error.
+int launch_ga_fused(const vrpms_ctx* ctx, const vrpms_ga_params* p, uint16_t* d_pop,
+                    uint64_t* d_keys, int n, hipStream_t s) {
+  if (ctx->opt_ga_fused == 2) return 0;
+  FastSplit f;
+  if (n > 255 || p->pop > 1024 || !fast_split_params(ctx, n, &f)) return 0;
+  GaFusedLayout L = ga_fused_layout(f.N, n, p->pop);
+  if (L.bytes > ctx->max_lds) return 0;
+  GaFusedArgs a = L.a;
+  a.f = f;
+  a.islands = p->islands;
+  a.pop = p->pop;
+  a.n = n;
+  a.gens = p->generations;
+  a.pmut = p->pmut;
+  a.seed_lo = (uint32_t)p->seed;
+  a.seed_hi = (uint32_t)(p->seed >> 32);
+  a.gen0 = p->gen0;
+  a.pop_tours = d_pop;
+  a.pop_keys = d_keys;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ga_fused_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.bytes);
+  ga_fused_kernel<<<p->islands, 1024, L.bytes, s>>>(a);
+  VRPMS_HIP(hipGetLastError());
+  return 1;
+}
+
+}  // namespace vrpms

@@ -23,6 +23,7 @@
 
 #include "common.hpp"
 #include "ctx.hpp"
+#include "sort.hpp"
 
 namespace vrpms {
 
@@ -71,33 +72,6 @@ __global__ __launch_bounds__(64) void random_tours_kernel(RandArgs a) {
     for (int q = 0; q < n; ++q) {
       if (a.out_bytes == 1) o8[q] = (uint8_t)T[q];
       else o16[q] = T[q];
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Block bitonic sort of M (power of two) (key, index) pairs in LDS, ascending
-// lexicographically.  Every thread of the block must call it.
-// ---------------------------------------------------------------------------
-VRPMS_DEV void block_sort_pairs(uint64_t* sk, uint32_t* si, int M) {
-  for (int size = 2; size <= M; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = threadIdx.x; i < M; i += blockDim.x) {
-        const int j = i ^ stride;
-        if (j > i) {
-          const bool up = (i & size) == 0;
-          const uint64_t ki = sk[i], kj = sk[j];
-          const uint32_t ii = si[i], ij = si[j];
-          const bool gt = ki > kj || (ki == kj && ii > ij);
-          if (gt == up) {
-            sk[i] = kj;
-            sk[j] = ki;
-            si[i] = ij;
-            si[j] = ii;
-          }
-        }
-      }
-      __syncthreads();
     }
   }
 }

@@ -33,11 +33,6 @@
 
 namespace vrpms {
 
-VRPMS_DEV void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
 VRPMS_DEV int lane_id() { return (int)(threadIdx.x & 63u); }
 
 // Instance staged for a search kernel: matrix in LDS when it fits, else L2.
@@ -1042,6 +1037,9 @@ struct BfK {
   static auto kernel() { return bf_kernel<MatT, HM, CVRP>; }
 };
 
+int launch_ga_fused(const vrpms_ctx* ctx, const vrpms_ga_params* p, uint16_t* d_pop,
+                    uint64_t* d_keys, int n, hipStream_t s);  // ga_fused.hip
+
 static void ensure_scratch(vrpms_ctx* ctx, size_t bytes, int* err) {
   if (ctx->search_scratch_bytes >= bytes) return;
   (void)hipFree(ctx->search_scratch);
@@ -1108,6 +1106,10 @@ extern "C" int vrpms_ga_generation(vrpms_ctx* ctx, const vrpms_ga_params* p, uin
   if (!d_pop || !d_keys) return fail(VRPMS_EINVAL, "vrpms_ga_generation: NULL population");
   VRPMS_HIP(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
+  // one workgroup per island for the whole call when the island fits the LDS
+  const int fused = launch_ga_fused(ctx, p, d_pop, d_keys, n, s);
+  if (fused < 0) return fused;
+  if (fused) return VRPMS_OK;
   const int64_t members = (int64_t)p->islands * p->pop;
   const size_t tour_bytes = (size_t)members * n * 2;
   // Children are scored by the headline kernel (eval_cvrp_words2) whenever
