@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Phase timing of the fused GA island kernel (ga_fused.hip built with
+-DVRPMS_GA_PROF into build_ab/gaprof/libvrpms.so): cycles per generation in
+breed / score / sort / survivor bookkeeping, from wall_clock64 (100 MHz
+constant clock on gfx950) stamps of thread 0 between workgroup barriers.
+
+usage: tools/ga_prof.py build   (CPU: compile the variant)
+       tools/ga_prof.py         (GPU: run CVRP-100, 256 islands x 256)"""
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+LIB = os.path.join(ROOT, "build_ab", "gaprof", "libvrpms.so")
+
+
+def build():
+    from vrpms_amd import build as b
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    cmd = [b.HIPCC, *b.FLAGS, "-DVRPMS_GA_PROF", "-o", LIB, *b.sources(), "-L/opt/rocm/lib",
+           "-lrccl"]
+    subprocess.run(cmd, check=True)
+
+
+def run():
+    import numpy as np
+    import torch
+
+    from vrpms_amd import _lib, runners, synth
+    from vrpms_amd.core import CVRP, Context
+    lib = _lib.load(LIB)
+    lib.vrpms_debug_ga_prof.restype = ctypes.c_int
+    lib.vrpms_debug_ga_prof.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    ctx = Context(0)
+    inst = synth.cvrp(100, 8, seed=0)
+    ctx.set_instance(CVRP, inst.durations, inst.demand, inst.capacities, inst.start_times)
+    for islands, pop, pmut in ((256, 256, 0.2), (256, 256, 0.0), (256, 128, 0.2)):
+        ga = runners.GARunner(ctx, inst.n, islands=islands, pop=pop, seed=1, gens_per_epoch=20,
+                              pmut=pmut)
+        ga.epoch()
+        torch.cuda.synchronize()
+        buf = (ctypes.c_ulonglong * (4 * 4096))()
+        lib.vrpms_debug_ga_prof(buf, 4 * 4096, 1)
+        ga.epoch()
+        torch.cuda.synchronize()
+        lib.vrpms_debug_ga_prof(buf, 4 * 4096, 1)
+        a = np.array(buf[:4 * islands], dtype=np.float64).reshape(islands, 4) / 20
+        names = ["breed", "score", "sort", "survivors"]
+        print(json.dumps({"islands": islands, "pop": pop, "pmut": pmut,
+                          "ticks_per_generation": dict(zip(names, a.mean(0).round(1).tolist())),
+                          "us_per_generation": round(a.mean(0).sum() / 100.0, 2)}), flush=True)
+        del ga
+
+
+if __name__ == "__main__":
+    build() if sys.argv[1:] == ["build"] else run()

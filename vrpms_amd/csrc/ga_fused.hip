@@ -33,6 +33,24 @@
 
 namespace vrpms {
 
+#ifdef VRPMS_GA_PROF
+// phase cycle counters per island (A/B builds only: tools/ga_prof.py)
+__device__ unsigned long long g_ga_prof[4 * 4096];
+#define GA_T(k)                                                                        \
+  do {                                                                                 \
+    __syncthreads();                                                                   \
+    if (threadIdx.x == 0) {                                                            \
+      const unsigned long long now = wall_clock64();                                   \
+      g_ga_prof[4 * blockIdx.x + (k)] += now - t_last;                                 \
+      t_last = now;                                                                    \
+    }                                                                                  \
+  } while (0)
+#else
+#define GA_T(k) \
+  do {          \
+  } while (0)
+#endif
+
 struct GaFusedArgs {
   FastSplit f;
   int islands, pop, n, gens, M;
@@ -122,29 +140,51 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
   WordChains<1> ch;
   ch.setup(a.f, smem);
   const int nfull = n >> 2;
+#ifdef VRPMS_GA_PROF
+  unsigned long long t_last = wall_clock64();
+#endif
   for (int g = 0; g < a.gens; ++g) {
     const uint64_t gen = a.gen0 + (uint64_t)g;
     // ---- breed: one child per wavefront at a time --------------------------
-    for (int child = wave; child < P; child += 16) {
-      const uint32_t cid = (uint32_t)(island * P + child);
-      const u32x4 r = philox((uint32_t)gen, (uint32_t)(gen >> 32), cid, 0u, a.seed_lo, a.seed_hi);
-      const u32x4 r2 = philox((uint32_t)gen, (uint32_t)(gen >> 32), cid, 1u, a.seed_lo, a.seed_hi);
-      const int pa = tourney2(pk, P, r.x, r.y), pb = tourney2(pk, P, r.z, r.w);
-      const uint8_t* A = rows + (uint32_t)prow[pa] * rs;
-      const uint8_t* B = rows + (uint32_t)prow[pb] * rs;
+    // Lane k of wave w first draws everything random about child w + 16k in
+    // parallel (two Philox blocks, both tournaments, the OX1 cut points, the
+    // mutation): 64 children per wave in one pass instead of 64 serial ones.
+    int v_pa = 0, v_pb = 0, v_lo = 0, v_hi = 0, v_mut = 0, v_mtyp = 0, v_mi = 0, v_mj = 0;
+    {
+      const int child = wave + 16 * lane;
+      if (child < P) {
+        const uint32_t cid = (uint32_t)(island * P + child);
+        const u32x4 r = philox((uint32_t)gen, (uint32_t)(gen >> 32), cid, 0u, a.seed_lo, a.seed_hi);
+        const u32x4 r2 =
+            philox((uint32_t)gen, (uint32_t)(gen >> 32), cid, 1u, a.seed_lo, a.seed_hi);
+        v_pa = prow[tourney2(pk, P, r.x, r.y)];
+        v_pb = prow[tourney2(pk, P, r.z, r.w)];
+        if (n >= 2) {
+          int lo = (int)(r2.x % (uint32_t)n), hi = (int)(r2.y % (uint32_t)n);
+          v_lo = lo < hi ? lo : hi;
+          v_hi = lo < hi ? hi : lo;
+          v_mut = r2.z < a.pmut ? 1 : 0;
+          if (v_mut) {
+            const Move m = decode_move(r2.w, r.x ^ r2.x, r.y ^ r2.y, n);
+            v_mtyp = (int)m.typ;
+            v_mi = m.i;
+            v_mj = m.j;
+          }
+        }
+      }
+    }
+    for (int k = 0; wave + 16 * k < P; ++k) {
+      const int child = wave + 16 * k;
+      const uint8_t* A = rows + (uint32_t)wave_bcast(v_pa, k) * rs;
+      const uint8_t* B = rows + (uint32_t)wave_bcast(v_pb, k) * rs;
       uint8_t* out = rows + (uint32_t)crow[child] * rs;
       if (n < 2) {
         for (int q = lane; q < n; q += 64) out[q] = A[q];
         continue;
       }
+      const int lo = wave_bcast(v_lo, k), hi = wave_bcast(v_hi, k);
       // OX1: out[lo..hi] = A[lo..hi]; the rest, from position hi+1 (wrapping),
       // are B's genes from B[hi+1] onwards (wrapping) not yet used
-      int lo = (int)(r2.x % (uint32_t)n), hi = (int)(r2.y % (uint32_t)n);
-      if (lo > hi) {
-        const int t = lo;
-        lo = hi;
-        hi = t;
-      }
       for (uint32_t w = lane; w < words; w += 64) used[w] = 0u;
       wave_sync();
       for (int q = lo + lane; q <= hi; q += 64) {
@@ -178,8 +218,11 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
         filled += __popcll(ball);
       }
       wave_sync();
-      if (r2.z < a.pmut) {  // wave-uniform: one move, applied by all lanes
-        const Move m = decode_move(r2.w, r.x ^ r2.x, r.y ^ r2.y, n);
+      if (wave_bcast(v_mut, k)) {  // wave-uniform: one move, applied by all lanes
+        Move m;
+        m.typ = (uint32_t)wave_bcast(v_mtyp, k);
+        m.i = wave_bcast(v_mi, k);
+        m.j = wave_bcast(v_mj, k);
         for (int q = lane; q < n; q += 64) tmp[q] = out[q];
         wave_sync();
         for (int q = lane; q < n; q += 64) out[q] = tmp[moved_index(q, m)];
@@ -187,6 +230,7 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
       }
     }
     __syncthreads();
+    GA_T(0);
     // ---- score the P children in place ---------------------------------------
     for (int t = threadIdx.x; t < P; t += blockDim.x) {
       const uint32_t* rw = reinterpret_cast<const uint32_t*>(rows + (uint32_t)crow[t] * rs);
@@ -219,13 +263,16 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
       ck[t] = ch.sa[0].finish(a.f, n).key;
     }
     __syncthreads();
+    GA_T(1);
     // ---- (mu + lambda) survivors by (key, index) -----------------------------
     for (int i = threadIdx.x; i < a.M; i += blockDim.x) {
       sk[i] = i < P ? pk[i] : (i < 2 * P ? ck[i - P] : ~0ull);
       si[i] = (uint32_t)i;
     }
     __syncthreads();
-    block_sort_pairs(sk, si, a.M);
+    if (a.M >= 64 && a.M <= 1024) block_sort_pairs_waves(sk, si, a.M);
+    else block_sort_pairs(sk, si, a.M);
+    GA_T(2);
     uint16_t nrow[2] = {0, 0};
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -268,6 +315,7 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
       }
     }
     __syncthreads();
+    GA_T(3);
   }
   for (int64_t e = threadIdx.x; e < (int64_t)P * n; e += blockDim.x) {
     const int i = (int)(e / n), q = (int)(e % n);
@@ -306,3 +354,16 @@ int launch_ga_fused(const vrpms_ctx* ctx, const vrpms_ga_params* p, uint16_t* d_
 }
 
 }  // namespace vrpms
+
+#ifdef VRPMS_GA_PROF
+extern "C" int vrpms_debug_ga_prof(unsigned long long* out, int count, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vrpms::g_ga_prof), sizeof(unsigned long long) * count) !=
+      hipSuccess)
+    return -2;
+  if (reset) {
+    static unsigned long long zero[4 * 4096];
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(vrpms::g_ga_prof), zero, sizeof(zero));
+  }
+  return 0;
+}
+#endif
