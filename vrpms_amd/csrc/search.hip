@@ -890,29 +890,16 @@ struct TspBatchArgs {
   uint64_t* best_keys;   // [R]
 };
 
-__global__ __launch_bounds__(256) void tsp_batch_sa_kernel(TspBatchArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// One request's 4 chains over its LDS-resident matrix D (MatT = uint16_t when
+// every entry fits, int32_t otherwise); `work` is the LDS after the matrix.
+template <typename MatT>
+VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, bool symmetric, bool small,
+                              unsigned char* work) {
   const int N = a.N, n = N - 1, r = blockIdx.x;
-  const uint32_t NN = (uint32_t)N * N;
-  int32_t* D = reinterpret_cast<int32_t*>(smem);
-  const int32_t* src = a.mats + (int64_t)r * NN;
-  for (uint32_t i = threadIdx.x; i < NN; i += blockDim.x) D[i] = src[i];
-  __syncthreads();
-  int asym = 0, big = 0;
-  // tour durations < 2^26 when every entry is below 2^26 / N: the 64-lane
-  // argmin of (duration, lane) then fits one dword
-  const int32_t lim26 = (int32_t)((1u << 26) / (uint32_t)N);
-  for (uint32_t i = threadIdx.x; i < NN; i += blockDim.x) {
-    const uint32_t x = i / N, y = i % N;
-    asym |= D[i] != D[y * N + x];
-    big |= D[i] < 0 || D[i] >= lim26;
-  }
-  const bool symmetric = __syncthreads_or(asym) == 0;
-  const bool small = __syncthreads_or(big) == 0;
   const uint32_t npad = ((uint32_t)n + 7u) & ~7u;
   const int wave = threadIdx.x >> 6, lane = lane_id();
-  uint16_t* buf = reinterpret_cast<uint16_t*>(smem + ((NN * 4 + 15u) & ~15u)) + wave * 3 * npad;
-  uint64_t* wbest = reinterpret_cast<uint64_t*>(smem + ((NN * 4 + 15u) & ~15u) + 4 * 3 * npad * 2);
+  uint16_t* buf = reinterpret_cast<uint16_t*>(work) + wave * 3 * npad;
+  uint64_t* wbest = reinterpret_cast<uint64_t*>(work + 4 * 3 * npad * 2);
   uint16_t* A = buf;
   uint16_t* B = buf + npad;
   uint16_t* Best = buf + 2 * npad;
@@ -929,7 +916,7 @@ __global__ __launch_bounds__(256) void tsp_batch_sa_kernel(TspBatchArgs a) {
       A[j] = t;
     }
   wave_sync();
-  auto dist = [&](uint32_t x, uint32_t y) { return D[__umul24(x, (uint32_t)N) + y]; };
+  auto dist = [&](uint32_t x, uint32_t y) { return (int)D[__umul24(x, (uint32_t)N) + y]; };
   auto full = [&](const uint16_t* T) {
     int s = 0;
     uint32_t prev = 0;
@@ -993,6 +980,44 @@ __global__ __launch_bounds__(256) void tsp_batch_sa_kernel(TspBatchArgs a) {
     uint16_t* out = a.best_tours + (int64_t)r * n;
     for (int q = lane; q < n; q += 64) out[q] = Best[q];
     if (lane == 0) a.best_keys[r] = bk;
+  }
+}
+
+// The request's matrix is checked in HBM (symmetric? every entry below
+// 2^26 / N, so the one-dword argmin applies? every entry below 2^16?) and
+// staged into LDS as uint16 when it fits -- half the LDS bytes per request
+// and two entries per dword for the 8 random gathers of each move -- else
+// as int32.
+__global__ __launch_bounds__(256) void tsp_batch_sa_kernel(TspBatchArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int N = a.N, r = blockIdx.x;
+  const uint32_t NN = (uint32_t)N * N;
+  const int32_t* src = a.mats + (int64_t)r * NN;
+  int asym = 0, big = 0, wide = 0;
+  // tour durations < 2^26 when every entry is below 2^26 / N: the 64-lane
+  // argmin of (duration, lane) then fits one dword
+  const int32_t lim26 = (int32_t)((1u << 26) / (uint32_t)N);
+  for (uint32_t i = threadIdx.x; i < NN; i += blockDim.x) {
+    const uint32_t x = i / N, y = i % N;
+    const int32_t v = src[i];
+    asym |= v != src[y * N + x];
+    big |= v < 0 || v >= lim26;
+    wide |= v < 0 || v > 65535;
+  }
+  const bool symmetric = __syncthreads_or(asym) == 0;
+  const bool small = __syncthreads_or(big) == 0;
+  const bool narrow = __syncthreads_or(wide) == 0;
+  unsigned char* work = smem + ((NN * 4 + 15u) & ~15u);
+  if (narrow) {
+    uint16_t* D = reinterpret_cast<uint16_t*>(smem);
+    for (uint32_t i = threadIdx.x; i < NN; i += blockDim.x) D[i] = (uint16_t)src[i];
+    __syncthreads();
+    tsp_batch_body<uint16_t>(a, D, symmetric, small, work);
+  } else {
+    int32_t* D = reinterpret_cast<int32_t*>(smem);
+    for (uint32_t i = threadIdx.x; i < NN; i += blockDim.x) D[i] = src[i];
+    __syncthreads();
+    tsp_batch_body<int32_t>(a, D, symmetric, small, work);
   }
 }
 
