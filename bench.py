@@ -146,28 +146,32 @@ class _TimedCooling:
 
 
 def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label="cvrp100_k8 seed 0",
-            gpu_seed=None):
+            gpu_seed=None, n_sep=None):
     """Best-cost gap at fixed wall time (the metric's second half): the same SA
     (Philox streams, 64 sampled moves per step, geometric cooling from
     0.5 to 0.002 x the mean edge spread over the wall-time budget by
     _TimedCooling) on the GPU -- `chains` chains with elite migration every 5
     epochs (across ranks when N > 1) -- and on the host cores
     (oracle/oracle_c.c, one chain per OpenMP thread).  Both legs run until
-    `seconds` of wall time are spent.  gap = (gpu - cpu) / cpu on the
+    `seconds` of wall time are spent.  Both legs search giant tours with
+    n_sep A10 route separators (default K - 1, the front-end's VRP SA), so
+    the moves place route boundaries too.  gap = (gpu - cpu) / cpu on the
     objective key's primary term (durationSum) with unvisited == 0."""
     import torch
     from vrpms_amd import islands, runners
     n = inst.n
+    n_sep = inst.K - 1 if n_sep is None else n_sep
     dev = ctx.dev
     edge = runners.typical_edge(inst.durations)
     t0, t_end = 0.5 * edge, 0.002 * edge
-    warm = runners.SARunner(ctx, n, chains=chains, total_steps=1000, durations=inst.durations)
+    warm = runners.SARunner(ctx, n, chains=chains, total_steps=1000, durations=inst.durations,
+                            n_sep=n_sep)
     warm.epoch(20)                       # first launch: code object load, LDS setup
     torch.cuda.synchronize(dev)
     del warm
     seed = (1000 + rank) if gpu_seed is None else gpu_seed
     r = runners.SARunner(ctx, n, chains=chains, seed=seed, total_steps=1000,
-                         durations=inst.durations, t0=t0, t_end=t_end)
+                         durations=inst.durations, t0=t0, t_end=t_end, n_sep=n_sep)
     if world > 1:
         dist.barrier()
     cool = _TimedCooling(seconds, t0, t_end)
@@ -191,13 +195,14 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
     if world > 1:
         key, _ = islands.global_best(r)
     out = {"T_s": seconds, "algorithm": "sa", "instance": label, "cooling": "wall-time geometric",
+           "separators": n_sep,
            "gpu": {"chains_per_gpu": chains, "steps_per_chain": r.step, "epochs": e,
                    "wall_s": gpu_wall, "unvisited": key >> 56,
                    "duration_sum": (key >> 28) & (2**28 - 1)}}
     if with_cpu:
         from oracle import coracle
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or coracle.max_threads()
-        cur = np.asarray(runners.random_tours(ctx, threads, n, 7).cpu().numpy()).view(np.uint16)
+        cur = np.asarray(ctx.random_tours(threads, n, 7, n_sep=n_sep).cpu().numpy()).view(np.uint16)
         cur = cur.copy()
         best = cur.copy()
         bk = np.full(threads, 2**64 - 1, dtype=np.uint64)

@@ -20,7 +20,9 @@
  *   - Nodes are compact indices: node 0 is the depot (VRP, A1) or the
  *     startNode (TSP, A4); customers are 1..N-1.  Tours are "giant tours":
  *     a permutation of customers without the depot, stored as uint8 (N<=256)
- *     or uint16 rows of `ld` elements.
+ *     or uint16 rows of `ld` elements.  A CVRP tour may also hold the token
+ *     0 any number of times (A10 route separator: it closes the current
+ *     vehicle's route and opens the next); `n` then counts tokens.
  *   - Semantics are SURVEY.md Appendix A (frozen in oracle/spec.py).
  */
 #ifndef VRPMS_H
@@ -169,7 +171,10 @@ typedef struct {
 } vrpms_sa_params;
 
 /* d_cur [chains][n] in/out (cur_key out); d_best/d_best_key in/out (set
- * d_best_key to UINT64_MAX before the first call). */
+ * d_best_key to UINT64_MAX before the first call).  CVRP tours may carry
+ * A10 separator tokens (n <= N - 1 + K): the moves then also shift route
+ * boundaries (relocating a separator), exchange customers across routes and
+ * reverse route sequences. */
 int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* d_cur, uint64_t* d_cur_key,
                  uint16_t* d_best, uint64_t* d_best_key, int32_t n, void* stream);
 
@@ -266,11 +271,14 @@ typedef struct {
 
 /* Start tours (the front-end's initial SA chains / GA population, the
  * bench's candidate batch): row r of `count` is the Philox Fisher-Yates
- * permutation of 1..n -- for i = n-1 .. 1 swap t[i] and t[w % (i+1)], w word
- * (i & 3) of philox4x32_10((i >> 2, 0xfffffffe, r, stream_id), seed) --
- * written as uint8 (tour_bytes 1, n <= 255) or uint16 rows of `ld` elements. */
-int vrpms_random_tours(vrpms_ctx* ctx, int64_t count, int32_t n, int64_t ld, int32_t tour_bytes,
-                       uint64_t seed, uint32_t stream_id, void* d_tours, void* stream);
+ * permutation of the tokens 1..n+n_sep -- for i = n+n_sep-1 .. 1 swap t[i]
+ * and t[w % (i+1)], w word (i & 3) of philox4x32_10((i >> 2, 0xfffffffe, r,
+ * stream_id), seed) -- with tokens above n written as 0 (A10 route
+ * separators; n_sep = 0 for plain permutations), as uint8 (tour_bytes 1,
+ * n + n_sep <= 255) or uint16 rows of `ld` elements. */
+int vrpms_random_tours(vrpms_ctx* ctx, int64_t count, int32_t n, int32_t n_sep, int64_t ld,
+                       int32_t tour_bytes, uint64_t seed, uint32_t stream_id, void* d_tours,
+                       void* stream);
 
 /* The E best rows of a pool by (key, index), ascending: d_tours [E][n],
  * d_keys [E] (0 < E <= min(count, 1024)). */

@@ -7,7 +7,8 @@
  *
  * Semantics follow oracle/spec.py line by line:
  *   eval_tsp   <- spec.eval_tsp   (A4; anchors api/parameters.py:41-43, src/solver.py:24)
- *   eval_cvrp  <- spec.eval_cvrp  (A5-A7; anchors api/parameters.py:11-12, src/solver.py:27)
+ *   eval_cvrp  <- spec.eval_cvrp  (A5-A7 + A10 separators; anchors api/parameters.py:11-12,
+ *                                  src/solver.py:24,27)
  *   pack_key   <- spec.pack_key   (A8)
  * Arithmetic is int64 here (the spec uses unbounded ints); the A9 guard
  * keeps every value inside int32 for the device.
@@ -58,6 +59,23 @@ static void eval_cvrp(const int32_t* D, int H, int N, const int32_t* dem, const 
   int64_t load = 0, t = K ? st[0] : 0, s = 0, m = 0, u = 0;
   for (int i = 0; i < n; ++i) {
     int x = perm_at(p8, p16, c, ld, i);
+    if (x == 0) { /* A10 separator: close the route, open the next vehicle */
+      if (k < K) {
+        if (prev != 0) {
+          int64_t te = t + edge(D, H, N, t, prev, 0);
+          int64_t rd = te - st[k];
+          s += rd;
+          if (rd > m) m = rd;
+        }
+        ++k;
+        if (k < K) {
+          load = 0;
+          t = st[k];
+          prev = 0;
+        }
+      }
+      continue;
+    }
     while (k < K && load + dem[x] > cap[k]) {
       if (prev != 0) {
         int64_t te = t + edge(D, H, N, t, prev, 0);
@@ -199,6 +217,22 @@ static uint64_t tour_key(const inst_t* I, const uint16_t* T, int n, const move_t
   int64_t load = 0, t = K ? I->st[0] : 0, s = 0, mx = 0, u = 0;
   for (int q = 0; q < n; ++q) {
     int x = T[m ? moved_index(q, m) : q];
+    if (x == 0) { /* A10 separator */
+      if (k < K) {
+        if (prev != 0) {
+          int64_t rd = t + edge(I->D, I->H, I->N, t, prev, 0) - I->st[k];
+          s += rd;
+          if (rd > mx) mx = rd;
+        }
+        ++k;
+        if (k < K) {
+          load = 0;
+          t = I->st[k];
+          prev = 0;
+        }
+      }
+      continue;
+    }
     while (k < K && load + I->dem[x] > I->cap[k]) {
       if (prev != 0) {
         int64_t rd = t + edge(I->D, I->H, I->N, t, prev, 0) - I->st[k];

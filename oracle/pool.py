@@ -17,19 +17,20 @@ from . import spec
 INJECT_WORST, INJECT_SORTED, INJECT_BETTER = 0, 1, 2
 
 
-def philox_tour(n: int, seed: int, row: int, stream_id: int = 0):
-    """vrpms_random_tours row `row`: Fisher-Yates over 1..n, i = n-1 .. 1,
-    j = w % (i + 1), w = word (i & 3) of philox((i >> 2, 0xfffffffe, row,
-    stream_id), seed)."""
+def philox_tour(n: int, seed: int, row: int, stream_id: int = 0, n_sep: int = 0):
+    """vrpms_random_tours row `row`: Fisher-Yates over the tokens 1..n+n_sep,
+    i = n+n_sep-1 .. 1, j = w % (i + 1), w = word (i & 3) of philox((i >> 2,
+    0xfffffffe, row, stream_id), seed); tokens above n become 0 (A10)."""
     key = spec.seed_key(seed)
-    t = list(range(1, n + 1))
+    L = n + n_sep
+    t = list(range(1, L + 1))
     w = None
-    for i in range(n - 1, 0, -1):
-        if (i & 3) == 3 or i == n - 1:
+    for i in range(L - 1, 0, -1):
+        if (i & 3) == 3 or i == L - 1:
             w = spec.philox4x32_10((i >> 2, 0xFFFFFFFE, row, stream_id), key)
         j = w[i & 3] % (i + 1)
         t[i], t[j] = t[j], t[i]
-    return t
+    return [0 if v > n else v for v in t]
 
 
 def elites_order(keys, E: int):

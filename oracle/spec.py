@@ -137,12 +137,20 @@ def eval_cvrp(D, perm, demand, capacities, start_times, objective: int = OBJ_SUM
     after all K vehicles are closed are unvisited.  Route duration = arrival
     back at depot - start_times[k] (A7).
 
+    A10 (route separators): the token 0 (the depot) may appear in the tour
+    any number of times; it closes vehicle k's route (an empty route has
+    duration 0) and opens vehicle k+1, exactly like a customer that does
+    not fit, but is not itself a customer: once all K vehicles are closed
+    later separators change nothing and are never counted as unvisited.
+
     Anchors: ``api/parameters.py:11-12`` (capacities, startTimes),
     ``src/solver.py:27`` (``unvisited``), result keys at
     ``api/vrp/ga/index.py:49-53``, vehicles payload at
-    ``api/database.py:73-76``.
+    ``api/database.py:73-76``; A10: ``src/solver.py:24`` (the depot 0 inside
+    the returned ``tour`` list marks route boundaries).
     Returns dict(sum, max, unvisited, key, routes, durations, vehicle_of)
-    where ``vehicle_of[i]`` is the vehicle of perm position i or -1.
+    where ``vehicle_of[i]`` is the vehicle of tour position i, -1 when the
+    customer is unvisited, -2 for a separator.
     """
     D = as_3d(D)
     H = D.shape[0]
@@ -164,6 +172,14 @@ def eval_cvrp(D, perm, demand, capacities, start_times, objective: int = OBJ_SUM
 
     for c in perm:
         c = int(c)
+        if c == 0:                      # A10: separator
+            vehicle_of.append(-2)
+            if k < K:
+                close(k, t, prev)
+                k += 1
+                if k < K:
+                    load, t, prev = 0, st[k], 0
+            continue
         while k < K and load + dem[c] > cap[k]:
             close(k, t, prev)
             k += 1
@@ -191,7 +207,8 @@ def eval_cvrp(D, perm, demand, capacities, start_times, objective: int = OBJ_SUM
 
 
 def eval_cvrp_batch(D, perms, demand, capacities, start_times, objective: int = OBJ_SUM):
-    """Vectorised A6/A7 over candidates; returns (keys u64, sums, maxs, unv)."""
+    """Vectorised A6/A7 (+ A10 separators) over candidates; returns (keys
+    u64, sums, maxs, unv)."""
     D = as_3d(D)
     H = D.shape[0]
     perms = np.asarray(perms, dtype=np.int64)
@@ -217,20 +234,28 @@ def eval_cvrp_batch(D, perms, demand, capacities, start_times, objective: int = 
         dsum = dsum + rd
         dmax = np.maximum(dmax, rd)
 
+    def advance(act):
+        nonlocal k, load, t, prev
+        k = np.where(act, k + 1, k)
+        kk = np.minimum(k, K - 1)
+        load = np.where(act, 0, load)
+        t = np.where(act, st[kk], t)
+        prev = np.where(act, 0, prev)
+
     for i in range(n):
         c = perms[:, i]
+        sep = c == 0
+        act = sep & (k < K)                     # A10: separators close the route
+        close(act)
+        advance(act)
         while True:
-            act = (k < K) & (load + dem[c] > cap[np.minimum(k, K - 1)])
+            act = ~sep & (k < K) & (load + dem[c] > cap[np.minimum(k, K - 1)])
             if not act.any():
                 break
             close(act)
-            k = np.where(act, k + 1, k)
-            kk = np.minimum(k, K - 1)
-            load = np.where(act, 0, load)
-            t = np.where(act, st[kk], t)
-            prev = np.where(act, 0, prev)
-        ok = k < K
-        unv = unv + (~ok)
+            advance(act)
+        ok = ~sep & (k < K)
+        unv = unv + (~sep & ~ok)
         step = D[(t // 60) % H, prev, c]
         t = np.where(ok, t + step, t)
         load = np.where(ok, load + dem[c], load)

@@ -38,10 +38,11 @@ class StandInContext:
                                    inst.problem, objective)
 
     # -- runners --------------------------------------------------------------
-    def random_tours(self, count, n, seed, stream_id=0, ld=None, dtype=None):
+    def random_tours(self, count, n, seed, stream_id=0, ld=None, dtype=None, n_sep=0):
         import torch
-        rows = [pool.philox_tour(n, seed, r, stream_id) for r in range(count)]
-        return torch.tensor(np.array(rows, dtype=np.int64).reshape(count, n), dtype=torch.int16)
+        rows = [pool.philox_tour(n, seed, r, stream_id, n_sep) for r in range(count)]
+        return torch.tensor(np.array(rows, dtype=np.int64).reshape(count, n + n_sep),
+                            dtype=torch.int16)
 
     def eval(self, perms, n=None, with_parts=False, out=None):
         P = perms.numpy().astype(np.uint16)

@@ -72,6 +72,47 @@ def test_cvrp_hand_example_split_and_unvisited():
     assert r["key"] == spec.pack_key(1, d0 + d1, max(d0, d1))
 
 
+def test_cvrp_separators_close_routes():
+    """A10: token 0 closes the current route and opens the next vehicle; an
+    empty route has duration 0; after the K-th vehicle separators are ignored
+    and never counted unvisited."""
+    N = 5
+    D = np.arange(N * N).reshape(N, N) % 7 + 1
+    np.fill_diagonal(D, 0)
+    dem = [0, 1, 1, 1, 1]
+    r = spec.eval_cvrp(D, [1, 0, 2, 3, 0, 4], dem, [10, 10, 10], [0, 0, 0])
+    assert r["routes"] == [[1], [2, 3], [4]]
+    assert r["vehicle_of"] == [0, -2, 1, 1, -2, 2] and r["unvisited"] == 0
+    assert r["durations"] == [D[0, 1] + D[1, 0], D[0, 2] + D[2, 3] + D[3, 0], D[0, 4] + D[4, 0]]
+    # leading / doubled separators burn empty vehicles; later customers unvisited
+    r = spec.eval_cvrp(D, [0, 1, 0, 0, 2, 3, 4], dem, [10, 10, 10], [0, 0, 0])
+    assert r["routes"] == [[], [1], []] and r["unvisited"] == 3
+    assert r["vehicle_of"] == [-2, 1, -2, -2, -1, -1, -1] and r["durations"][0] == 0
+    # a separator after the fleet is exhausted changes nothing
+    a = spec.eval_cvrp(D, [1, 2, 3, 0, 4], dem, [1, 1], [0, 0])
+    b = spec.eval_cvrp(D, [1, 2, 3, 4], dem, [1, 1], [0, 0])
+    assert (a["key"], a["unvisited"]) == (b["key"], b["unvisited"]) == (a["key"], 2)
+
+
+def test_c_restatement_matches_python_spec_with_separators(coracle):
+    for slack, S in [(0.9, 4), (1.2, 3), (1.5, 2)]:
+        inst = synth.cvrp(15, 4, seed=2, slack=slack)
+        rng = np.random.default_rng(S)
+        P = np.array([rng.permutation(np.concatenate([np.arange(1, 16), np.zeros(S, dtype=int)]))
+                      for _ in range(400)]).astype(np.uint8)
+        for obj in (0, 1):
+            ref = spec.eval_cvrp_batch(inst.durations, P, inst.demand, inst.capacities,
+                                       inst.start_times, obj)
+            got = coracle.eval_batch(inst.durations, P, inst.demand, inst.capacities,
+                                     inst.start_times, 1, obj)
+            for x, y in zip(ref, got):
+                assert (np.asarray(x).astype(np.int64) == np.asarray(y).astype(np.int64)).all()
+        for i in range(0, 400, 37):
+            r = spec.eval_cvrp(inst.durations, P[i], inst.demand, inst.capacities,
+                               inst.start_times, 1)   # ref: the last (objective 1) pass
+            assert r["key"] == int(ref[0][i])
+
+
 def test_cvrp_oversized_customer_skips_empty_vehicles():
     D = np.ones((4, 4), dtype=np.int64)
     np.fill_diagonal(D, 0)

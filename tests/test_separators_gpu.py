@@ -1,0 +1,154 @@
+"""A10 route separators (token 0 inside a CVRP giant tour) on every scoring
+path, the decode and the SA kernels, against the C / Python oracle."""
+import numpy as np
+import pytest
+
+from oracle import search, spec
+from oracle import pool as opool
+from vrpms_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def torch_():
+    import torch
+    return torch
+
+
+def u64(t):
+    return [int(x) & (2**64 - 1) for x in t.reshape(-1).cpu().tolist()]
+
+
+def sep_tours(C, n, S, seed, ld=None, dtype=np.uint8):
+    """C random orders of customers 1..n plus S separators (zeros)."""
+    rng = np.random.default_rng(seed)
+    L = n + S
+    ld = L if ld is None else ld
+    out = np.zeros((C, ld), dtype=dtype)
+    base = np.concatenate([np.arange(1, n + 1), np.zeros(S, dtype=np.int64)])
+    out[:, :L] = rng.permuted(np.tile(base, (C, 1)), axis=1).astype(dtype)
+    return out
+
+
+def load(ctx, inst, objective=0):
+    from vrpms_amd.core import CVRP
+    ctx.set_instance(CVRP, inst.durations, inst.demand, inst.capacities, inst.start_times,
+                     objective=objective)
+
+
+def check(ctx, coracle, inst, P, L, objective=0):
+    torch = torch_()
+    dP = torch.from_numpy(P).to(ctx.dev)
+    keys, sums, maxs, unv = ctx.eval(dP, n=L, with_parts=True)
+    ref = coracle.eval_batch(inst.durations, P, inst.demand, inst.capacities, inst.start_times,
+                             1, objective, n=L)
+    got = keys.cpu().numpy().view(np.uint64)
+    np.testing.assert_array_equal(got, ref[0])
+    np.testing.assert_array_equal(sums.cpu().numpy(), ref[1])
+    np.testing.assert_array_equal(maxs.cpu().numpy(), ref[2])
+    np.testing.assert_array_equal(unv.cpu().numpy(), ref[3])
+    for i in range(0, P.shape[0], max(1, P.shape[0] // 5)):
+        r = spec.eval_cvrp(inst.durations, P[i, :L], inst.demand, inst.capacities,
+                           inst.start_times, objective)
+        assert int(got[i]) == r["key"]
+    return got
+
+
+@pytest.mark.parametrize("slack,S", [(1.1, 7), (0.9, 3), (1.3, 12)])
+def test_fast_split_kernels_with_separators(ctx, coracle, slack, S):
+    """rows2 (every configuration), words2 and eval_cvrp_packed MODE 1/2 on
+    CVRP-100 tours with S separators; tight fleets exhaust (exact re-walk)."""
+    from vrpms_amd.core import VrpmsError  # noqa: F401
+    inst = synth.cvrp(100, 8, seed=S, slack=slack)
+    load(ctx, inst)
+    L = inst.n + S
+    ld = (L + 3) // 4 * 4
+    P = sep_tours(6007, inst.n, S, seed=S, ld=ld)
+    try:
+        ref = check(ctx, coracle, inst, P, L)
+        for cfg in range(1, 6):
+            ctx.set_rows_config(cfg)
+            np.testing.assert_array_equal(check(ctx, coracle, inst, P, L), ref)
+        ctx.set_rows_config(0)
+        ctx.set_words_kernel(1)          # eval_cvrp_packed, prefix-ret (MODE 1)
+        np.testing.assert_array_equal(check(ctx, coracle, inst, P, L), ref)
+        ctx.set_split_mode(2)            # eval_cvrp_packed, branchy (MODE 2)
+        np.testing.assert_array_equal(check(ctx, coracle, inst, P, L), ref)
+    finally:
+        ctx.set_rows_config(0)
+        ctx.set_words_kernel(0)
+        ctx.set_split_mode(0)
+    torch = torch_()
+    words = ctx.to_words(torch.from_numpy(P).to(ctx.dev), L)
+    k = ctx.eval_words(words, L)
+    np.testing.assert_array_equal(k.cpu().numpy().view(np.uint64), ref)
+
+
+def test_heterogeneous_fleet_and_generic_paths(ctx, coracle):
+    """MODE 0 (heterogeneous capacities, packed) and the L2 / generic paths
+    (uint16 tours, N = 150; hour-indexed TD-60) with separators."""
+    inst = synth.cvrp(40, 5, seed=3, slack=1.0)
+    inst.capacities = np.array([30, 60, 45, 80, 50])
+    load(ctx, inst)
+    P = sep_tours(3001, inst.n, 4, seed=1, ld=44)
+    check(ctx, coracle, inst, P, inst.n + 4)
+    big = synth.cvrp(150, 12, seed=4)
+    load(ctx, big)
+    P = sep_tours(2003, big.n, 11, seed=2, dtype=np.uint16).astype(np.int16)
+    check(ctx, coracle, big, P, big.n + 11)
+    td = synth.td_cvrp(60, 5, seed=5)
+    load(ctx, td)
+    P = sep_tours(2001, td.n, 4, seed=3, ld=64)
+    check(ctx, coracle, td, P, td.n + 4)
+
+
+def test_decode_marks_separators(ctx):
+    torch = torch_()
+    inst = synth.cvrp(20, 4, seed=6, slack=1.2)
+    load(ctx, inst)
+    P = sep_tours(5, inst.n, 3, seed=9)
+    for row in P:
+        veh, dur = ctx.decode(torch.from_numpy(row.astype(np.int16)).to(ctx.dev), len(row))
+        r = spec.eval_cvrp(inst.durations, row, inst.demand, inst.capacities, inst.start_times)
+        assert veh == r["vehicle_of"] and dur == r["durations"]
+
+
+@pytest.mark.parametrize("kind", ["packed", "generic_td"])
+def test_sa_with_separators_matches_oracle(ctx, coracle, kind):
+    """SA trajectories over separator tours: sa_packed_kernel (cfg-2 style)
+    against the C restatement, sa_kernel on an hour-indexed instance against
+    the Python replay."""
+    torch = torch_()
+    if kind == "packed":
+        inst, S, chains, steps = synth.cvrp(60, 6, seed=7, slack=1.05), 5, 16, 60
+    else:
+        inst, S, chains, steps = synth.td_cvrp(12, 3, seed=8), 2, 3, 10
+    load(ctx, inst)
+    L = inst.n + S
+    P = sep_tours(chains, inst.n, S, seed=4, dtype=np.uint16).astype(np.int16)
+    cur = torch.from_numpy(P).to(ctx.dev)
+    best = cur.clone()
+    ck = torch.empty(chains, dtype=torch.int64, device=ctx.dev)
+    bk = torch.full((chains,), -1, dtype=torch.int64, device=ctx.dev)
+    ctx.sa_run(cur, ck, best, bk, steps=steps, inv_t0=1 / 60.0, inv_alpha=1 / 0.99, seed=3,
+               step0=11)
+    if kind == "packed":
+        ccur, cbest = P.view(np.uint16).copy(), P.view(np.uint16).copy()
+        cbk = np.full(chains, 2**64 - 1, dtype=np.uint64)
+        cck = coracle.sa_run(inst.durations, ccur, cbest, cbk, steps, 1 / 60.0, 1 / 0.99, 3, 11,
+                             inst.demand, inst.capacities, inst.start_times)
+        assert (cur.cpu().numpy().view(np.uint16) == ccur).all()
+        assert u64(ck) == [int(x) for x in cck] and u64(bk) == [int(x) for x in cbk]
+    else:
+        sc = search.Scorer(inst.durations, inst.demand, inst.capacities, inst.start_times)
+        ref = search.sa_run(sc, P.tolist(), P.tolist(), [2**64 - 1] * chains, 3, 11, steps,
+                            1 / 60.0, 1 / 0.99)
+        assert cur.cpu().numpy().tolist() == ref[0] and u64(bk) == ref[3]
+    assert all(sorted(r) == [0] * S + list(range(1, inst.n + 1)) for r in cur.cpu().tolist())
+
+
+def test_random_tours_with_separators(ctx):
+    T = ctx.random_tours(50, 30, seed=4, stream_id=1, n_sep=5).cpu().tolist()
+    for r in (0, 17, 49):
+        assert T[r] == opool.philox_tour(30, 4, r, 1, 5)
+    assert all(sorted(t) == [0] * 5 + list(range(1, 31)) for t in T)

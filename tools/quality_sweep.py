@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--T", type=float, nargs="+", default=[1.0, 10.0, 60.0])
     ap.add_argument("--seeds", type=int, nargs="+", default=[0, 1, 2, 3, 4])
     ap.add_argument("--chains", type=int, default=4096)
+    ap.add_argument("--sep", type=int, default=None,
+                    help="A10 route separators per tour (default K - 1; 0 = plain giant tours)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "quality_sweep.json"))
     args = ap.parse_args()
 
@@ -45,7 +47,7 @@ def main():
         ctx.set_instance(CVRP, inst.durations, inst.demand, inst.capacities, inst.start_times)
         for T in args.T:
             q = bench.quality(ctx, inst, T, 1, 0, None, with_cpu=True, chains=args.chains,
-                              label=f"cvrp100_k8 seed {seed}")
+                              label=f"cvrp100_k8 seed {seed}", n_sep=args.sep)
             q["seed"] = seed
             cells.append(q)
             print(json.dumps({"seed": seed, "T_s": T, "gpu": q["gpu"]["duration_sum"],
@@ -64,6 +66,7 @@ def main():
                 json.dump({"metric": "best-cost gap at equal wall time, (gpu - cpu) / cpu "
                                      "on durationSum, negative = GPU better",
                            "workload": "CVRP-100, K=8 (synth.cvrp), SA on both sides",
+                           "separators": cells[0]["separators"],
                            "cpu_cores": cells[0]["cpu"]["cores"],
                            "summary": summary, "cells": cells}, f, indent=1)
     print(json.dumps({"summary": summary}), flush=True)

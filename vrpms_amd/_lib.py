@@ -88,7 +88,8 @@ SIGNATURES = {
     "vrpms_probe_l2_gather": (_c.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp]),
     "vrpms_tsp_batch_sa": (_c.c_int, [_vp, _vp, _i32, _i32, _c.POINTER(SaParams), _vp, _vp,
                                       _vp]),
-    "vrpms_random_tours": (_c.c_int, [_vp, _i64, _i32, _i64, _i32, _u64, _c.c_uint32, _vp, _vp]),
+    "vrpms_random_tours": (_c.c_int, [_vp, _i64, _i32, _i32, _i64, _i32, _u64, _c.c_uint32, _vp,
+                                      _vp]),
     "vrpms_pool_elites": (_c.c_int, [_vp, _c.POINTER(Pool), _i32, _vp, _vp, _vp]),
     "vrpms_pool_inject": (_c.c_int, [_vp, _c.POINTER(Pool), _i32, _vp, _vp, _i32, _vp]),
     "vrpms_island_msg_bytes": (_i64, [_i32, _i32]),

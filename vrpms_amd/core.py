@@ -289,16 +289,18 @@ class Context:
 
     # -- populations and the island model (pool.hip) ---------------------------
     def random_tours(self, count: int, n: int, seed: int, stream_id: int = 0, ld: int | None = None,
-                     dtype=None):
-        """Philox Fisher-Yates permutations of 1..n (vrpms_random_tours) as
-        int16 (default) or uint8 rows of `ld` elements."""
+                     dtype=None, n_sep: int = 0):
+        """Philox Fisher-Yates permutations of 1..n plus `n_sep` route
+        separators (token 0, A10) -- vrpms_random_tours -- as int16 (default)
+        or uint8 rows of `ld` elements."""
         torch = _torch()
         dtype = torch.int16 if dtype is None else dtype
-        ld = n if ld is None else int(ld)
+        ld = n + n_sep if ld is None else int(ld)
         out = torch.zeros((int(count), ld), dtype=dtype, device=self.dev)
-        check(self.lib.vrpms_random_tours(self._ctx, int(count), int(n), ld, perm_dtype_bytes(out),
-                                          int(seed) & (2**64 - 1), int(stream_id) & 0xFFFFFFFF,
-                                          out.data_ptr(), self.stream()))
+        check(self.lib.vrpms_random_tours(self._ctx, int(count), int(n), int(n_sep), ld,
+                                          perm_dtype_bytes(out), int(seed) & (2**64 - 1),
+                                          int(stream_id) & 0xFFFFFFFF, out.data_ptr(),
+                                          self.stream()))
         return out
 
     @staticmethod

@@ -120,7 +120,8 @@ __global__ void pack_prefix_kernel(const int32_t* __restrict__ D, const int32_t*
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int a = (int)(i / N), b = (int)(i % N);
-    uint32_t lo = 0, hi = 0;
+    // column 0 (A10 separator): never fits, opens an empty route (hi = 0)
+    uint32_t lo = 0x7fffffffu, hi = 0;
     if (b > 0) {
       const int64_t retb = D[(int64_t)b * N], reta = a > 0 ? D[(int64_t)a * N] : 0;
       const int64_t d = (int64_t)D[(int64_t)a * N + b] + retb - reta;

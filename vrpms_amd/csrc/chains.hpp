@@ -118,24 +118,14 @@ struct WordChains {
 #pragma unroll
       for (int i = 0; i < ILP; ++i) split_step_fast(sa[i], g[i][q], vsmask, kinc);
   }
-  // The exact split of one tour, word by word (word(w) returns tour word w):
-  // the slow path for a chain whose fast walk met the fleet limit.
+  // The exact split of one tour (fleet limit, A10 separators), word by word
+  // (word(w) returns tour word w): the slow path for a chain whose fast walk
+  // met the fleet limit.
   template <class WordAt>
-  VRPMS_DEV SplitAcc redo_exact(const FastSplit& f, int n, WordAt word) const {
-    SplitAcc s;
-    s.init(f);
-    uint32_t prev = 0;  // byte 3 = the depot before the first customer
-    const int nw = (n + 3) >> 2;
-    for (int w = 0; w < nw; ++w) {
-      const uint32_t x = word(w);
-      const int rem = min(4, n - 4 * w);
-      if (rem > 0) split_step(s, gat(__builtin_amdgcn_perm(x, prev, kSel30)), vsmask, kinc, deadacc);
-      if (rem > 1) split_step(s, gat(__builtin_amdgcn_perm(x, x, kSel01)), vsmask, kinc, deadacc);
-      if (rem > 2) split_step(s, gat(__builtin_amdgcn_perm(x, x, kSel12)), vsmask, kinc, deadacc);
-      if (rem > 3) split_step(s, gat(__builtin_amdgcn_perm(x, x, kSel23)), vsmask, kinc, deadacc);
-      prev = x;
-    }
-    return s;
+  VRPMS_DEV TourCost redo_exact(const FastSplit& f, int n, WordAt word) const {
+    return exact_split(
+        f, n, [&](int q) { return (word(q >> 2) >> (8 * (q & 3))) & 0xffu; },
+        [&](uint32_t a, uint32_t b) { return gat(a | (b << 16)); });
   }
   // next word's address math (perm + dot2) interleaved into this word's
   // split chain, each ds_read well after its dot2
@@ -163,9 +153,8 @@ struct WordChains {
   }
 };
 
-VRPMS_DEV void store_cost(const FastSplit& f, const SplitAcc& s, int n, int64_t c,
-                          uint64_t* keys, int32_t* sums, int32_t* maxs, int32_t* unv) {
-  const TourCost tc = s.finish(f, n);
+VRPMS_DEV void store_cost(const TourCost& tc, int64_t c, uint64_t* keys, int32_t* sums,
+                          int32_t* maxs, int32_t* unv) {
   keys[c] = tc.key;
   if (sums) sums[c] = tc.sum;
   if (maxs) maxs[c] = tc.max;

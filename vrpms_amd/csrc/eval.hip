@@ -227,36 +227,64 @@ __global__ __launch_bounds__(BLOCK) void eval_cvrp_packed(PackedArgs a) {
     int k = 0;
     // MODE 1 state (prefix-ret): acc = load << S | (cur + ret(prev))
     uint32_t acc = 0;
-    bool dead = false;
+    bool dead = false;  // all K vehicles closed: customers unvisited, separators ignored
     // MODE 0/2 state
     int rcap = MODE == 0 ? capL[0] : cap0;
     uint32_t cur = 0, hprev = 0;
-    // one split step at tour position `pos`
-    auto step = [&](uint64_t e, int pos) {
+    bool open = false;  // the current route holds a customer
+    // one split step for token c (A10: c == 0 is a route separator)
+    auto step = [&](uint64_t e, uint32_t c) {
       const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
       if constexpr (MODE == 1) {
-        // Branch-free: one add + one unsigned compare is the capacity test
-        // (the load sits above bit S); closing a route reads its duration
-        // straight out of the low field because ret(prev) is pre-added.
+        // one add + one unsigned compare is the capacity test (the load sits
+        // above bit S); closing a route reads its duration straight out of
+        // the low field because ret(prev) is pre-added
+        if (dead) {
+          unv += c != 0u;
+          return;
+        }
         const uint32_t t = acc + lo;
-        const bool f = t < lim || dead;
-        const uint32_t rd = f ? 0u : (acc & smask);
+        if (c != 0u && t < lim) {
+          acc = t;
+          return;
+        }
+        const uint32_t rd = acc & smask;  // close route k (0 when empty)
         dsum += rd;
         dmax = max(dmax, rd);
-        k += f ? 0 : 1;
-        const bool die = !f && (k >= K || hi >= lim);  // no vehicle left / fits none
-        unv = die ? (uint32_t)(n - pos) : unv;
-        dead = dead || die;
-        acc = f ? t : hi;  // hi = open'(c): a fresh route holding c
+        ++k;
+        if (c == 0u) {
+          dead = k >= K;
+          acc = 0;
+        } else if (k >= K || hi >= lim) {  // no vehicle left / c fits no empty vehicle
+          dead = true;
+          ++unv;
+        } else {
+          acc = hi;  // hi = open'(c): a fresh route holding c
+        }
       } else {
+        if (c == 0u) {  // separator: close route k (if any), open vehicle k + 1
+          if (k < K) {
+            if (open) {
+              const uint32_t rd = cur + (hprev & wmask);
+              dsum += rd;
+              dmax = max(dmax, rd);
+            }
+            ++k;
+            open = false;
+            cur = 0;
+            rcap = k < K ? (MODE == 2 ? cap0 : capL[k]) : INT_MIN;
+          }
+          return;
+        }
         const int dem = (int)(hi >> dshift);
         if (dem <= rcap) {
           cur += lo;
           rcap -= dem;
+          open = true;
         } else if (k >= K) {
           ++unv;
         } else {
-          if (pos != 0) {  // close the open route: prev -> depot
+          if (open) {  // close the open route: prev -> depot
             const uint32_t rd = cur + (hprev & wmask);
             dsum += rd;
             dmax = max(dmax, rd);
@@ -270,9 +298,11 @@ __global__ __launch_bounds__(BLOCK) void eval_cvrp_packed(PackedArgs a) {
           if (k < K) {
             cur = (hi >> w) & wmask;  // depot -> c
             rcap = (MODE == 2 ? cap0 : capL[k]) - dem;
+            open = true;
           } else {
             ++unv;
             rcap = INT_MIN;
+            open = false;
           }
         }
         hprev = hi;
@@ -294,16 +324,13 @@ __global__ __launch_bounds__(BLOCK) void eval_cvrp_packed(PackedArgs a) {
                      n3 = wn >> 24;
       const uint64_t f0 = gat(c3, n0), f1 = gat(n0, n1), f2 = gat(n1, n2), f3 = gat(n2, n3);
       const int pos = 4 * j;
-      if (pos + 4 <= n) {
-        step(e0, pos);
-        step(e1, pos + 1);
-        step(e2, pos + 2);
-        step(e3, pos + 3);
-      } else {
-        step(e0, pos);
-        if (pos + 1 < n) step(e1, pos + 1);
-        if (pos + 2 < n) step(e2, pos + 2);
-      }
+      step(e0, c0);
+      if (pos + 1 < n) step(e1, c1);
+      if (pos + 2 < n) step(e2, c2);
+      if (pos + 3 < n) step(e3, c3);
+      c0 = n0;
+      c1 = n1;
+      c2 = n2;
       c3 = n3;
       e0 = f0;
       e1 = f1;
@@ -317,7 +344,7 @@ __global__ __launch_bounds__(BLOCK) void eval_cvrp_packed(PackedArgs a) {
         dmax = max(dmax, rd);
       }
     } else {
-      if (k < K && n > 0) {
+      if (k < K && open) {
         const uint32_t rd = cur + (hprev & wmask);
         dsum += rd;
         dmax = max(dmax, rd);
@@ -441,6 +468,22 @@ __global__ void decode_kernel(const int32_t* __restrict__ M, int N, int H, int p
   uint32_t prev = 0;
   for (int i = 0; i < n; ++i) {
     const uint32_t cc = min((uint32_t)perm[i], (uint32_t)N - 1);
+    if (cc == 0) {  // A10 separator
+      vehicle_of[i] = -2;
+      if (k < K) {
+        if (prev) {
+          t += M[hr(t) + prev * N];
+          route_dur[k] = t - start[k];
+        }
+        ++k;
+        if (k < K) {
+          load = 0;
+          t = start[k];
+          prev = 0;
+        }
+      }
+      continue;
+    }
     const int dc = dem[cc];
     while (k < K && load + dc > cap[k]) {
       if (prev) {

@@ -178,6 +178,10 @@ __global__ __launch_bounds__(kStBlock) void eval_staged(StagedArgs a) {
   // before the step (used unless the step closes a route).
   auto step = [&](StState& s, uint32_t cc, int g) {
     if constexpr (CVRP) {
+      if (cc == 0) {  // A10 separator: close route k (if any), open vehicle k + 1
+        if (s.k < K) close_route(s);
+        return;
+      }
       const int dc = demT[cc];
       bool closed = false;
       if (s.k < K && s.load + dc > s.capk) {

@@ -152,11 +152,14 @@ __global__ __launch_bounds__(1024) void eval_cvrp_words2(WordsArgs a) {
 #pragma unroll
     for (int i = 0; i < ILP; ++i) {
       const int64_t c = c0 + threadIdx.x + 1024 * i;
-      if (live[i] && (int32_t)ch.sa[i].dsum < 0)  // met the fleet limit: exact re-walk
-        ch.sa[i] = ch.redo_exact(a.f, n, [&](int w) {
-          return a.words[(int64_t)w * wstride + c * (int64_t)a.cstride];
-        });
-      if (live[i]) store_cost(a.f, ch.sa[i], n, c, a.keys, a.sums, a.maxs, a.unv);
+      if (!live[i]) continue;
+      // a walk that met the fleet limit is re-walked exactly
+      const TourCost tc = (int32_t)ch.sa[i].dsum < 0
+          ? ch.redo_exact(a.f, n, [&](int w) {
+              return a.words[(int64_t)w * wstride + c * (int64_t)a.cstride];
+            })
+          : ch.sa[i].finish(a.f, n);
+      store_cost(tc, c, a.keys, a.sums, a.maxs, a.unv);
     }
   }
 }
@@ -286,11 +289,14 @@ __global__ __launch_bounds__(1024) void eval_cvrp_rows2(RowsArgs a) {
 #pragma unroll
     for (int i = 0; i < ILP; ++i) {
       const int64_t c = t0 + wave * WR + l + 64 * i;
-      if (c < C && (int32_t)ch.sa[i].dsum < 0)  // met the fleet limit: exact re-walk
-        ch.sa[i] = ch.redo_exact(a.f, n, [&](int w) {
-          return *reinterpret_cast<const uint32_t*>(a.perms + c * (int64_t)a.ld + 4 * w);
-        });
-      if (c < C) store_cost(a.f, ch.sa[i], n, c, a.keys, a.sums, a.maxs, a.unv);
+      if (c >= C) continue;
+      // a walk that met the fleet limit is re-walked exactly
+      const TourCost tc = (int32_t)ch.sa[i].dsum < 0
+          ? ch.redo_exact(a.f, n, [&](int w) {
+              return *reinterpret_cast<const uint32_t*>(a.perms + c * (int64_t)a.ld + 4 * w);
+            })
+          : ch.sa[i].finish(a.f, n);
+      store_cost(tc, c, a.keys, a.sums, a.maxs, a.unv);
     }
   }
 }

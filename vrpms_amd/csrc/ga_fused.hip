@@ -258,9 +258,9 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
         const uint32_t x[1] = {rw[nfull]};
         ch.partial(x, n & 3);
       }
-      if ((int32_t)ch.sa[0].dsum < 0)  // met the fleet limit: exact re-walk
-        ch.sa[0] = ch.redo_exact(a.f, n, [&](int w) { return rw[w]; });
-      ck[t] = ch.sa[0].finish(a.f, n).key;
+      ck[t] = (int32_t)ch.sa[0].dsum < 0  // met the fleet limit: exact re-walk
+                  ? ch.redo_exact(a.f, n, [&](int w) { return rw[w]; }).key
+                  : ch.sa[0].finish(a.f, n).key;
     }
     __syncthreads();
     GA_T(1);

@@ -29,12 +29,13 @@ namespace vrpms {
 
 // ---------------------------------------------------------------------------
 // Philox Fisher-Yates start tours: row r of `count` is the permutation of
-// 1..n made by, for i = n-1 .. 1, swapping t[i] with t[w % (i + 1)] where w
-// is word (i & 3) of philox((i >> 2, 0xfffffffe, r, stream), seed).
+// 1..n+S made by, for i = n+S-1 .. 1, swapping t[i] with t[w % (i + 1)]
+// where w is word (i & 3) of philox((i >> 2, 0xfffffffe, r, stream), seed);
+// tokens n+1..n+S are then written as 0 (A10 route separators).
 // ---------------------------------------------------------------------------
 struct RandArgs {
   int64_t count;
-  int n, ld, out_bytes, in_lds;
+  int n, nsep, ld, out_bytes, in_lds;  // tokens = n + nsep; values > n leave as 0 (A10)
   uint32_t seed_lo, seed_hi, stream_id;
   void* out;
 };
@@ -43,7 +44,7 @@ __global__ __launch_bounds__(64) void random_tours_kernel(RandArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int64_t row = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (row >= a.count) return;
-  const int n = a.n;
+  const int n = a.n + a.nsep, nc = a.n;
   // the lane's working row: its LDS slice, or the output row itself
   uint16_t* T = a.in_lds ? reinterpret_cast<uint16_t*>(smem) + threadIdx.x * (uint32_t)n : nullptr;
   uint8_t* o8 = static_cast<uint8_t*>(a.out) + row * a.ld;
@@ -68,11 +69,11 @@ __global__ __launch_bounds__(64) void random_tours_kernel(RandArgs a) {
     wr(i, tj);
     wr(j, ti);
   }
-  if (T) {
-    for (int q = 0; q < n; ++q) {
-      if (a.out_bytes == 1) o8[q] = (uint8_t)T[q];
-      else o16[q] = T[q];
-    }
+  for (int q = 0; q < n; ++q) {
+    uint32_t v = rd(q);
+    v = v > (uint32_t)nc ? 0u : v;  // the nsep largest tokens are separators
+    if (a.out_bytes == 1) o8[q] = (uint8_t)v;
+    else o16[q] = (uint16_t)v;
   }
 }
 
@@ -342,20 +343,24 @@ using namespace vrpms;
 
 extern "C" {
 
-int vrpms_random_tours(vrpms_ctx* ctx, int64_t count, int32_t n, int64_t ld, int32_t tour_bytes,
-                       uint64_t seed, uint32_t stream_id, void* d_tours, void* stream) {
+int vrpms_random_tours(vrpms_ctx* ctx, int64_t count, int32_t n, int32_t n_sep, int64_t ld,
+                       int32_t tour_bytes, uint64_t seed, uint32_t stream_id, void* d_tours,
+                       void* stream) {
   if (!ctx) return fail(VRPMS_EINVAL, "vrpms_random_tours: ctx is NULL");
-  if (count < 0 || n < 0 || ld < n || (tour_bytes != 1 && tour_bytes != 2))
-    return fail(VRPMS_EINVAL, "vrpms_random_tours: need count >= 0, 0 <= n <= ld, tour_bytes 1 or 2");
-  if ((tour_bytes == 1 && n > 255) || n > 65535)
-    return fail(VRPMS_EINVAL, "vrpms_random_tours: customer ids do not fit the tour element");
-  if (count == 0 || n == 0) return VRPMS_OK;
+  if (count < 0 || n < 0 || n_sep < 0 || ld < (int64_t)n + n_sep ||
+      (tour_bytes != 1 && tour_bytes != 2))
+    return fail(VRPMS_EINVAL,
+                "vrpms_random_tours: need count >= 0, n, n_sep >= 0, n + n_sep <= ld, tour_bytes 1 or 2");
+  if ((tour_bytes == 1 && n + n_sep > 255) || n + n_sep > 65535)
+    return fail(VRPMS_EINVAL, "vrpms_random_tours: token ids do not fit the tour element");
+  const int tokens = n + n_sep;
+  if (count == 0 || tokens == 0) return VRPMS_OK;
   if (!d_tours) return fail(VRPMS_EINVAL, "vrpms_random_tours: d_tours is NULL");
   VRPMS_HIP(hipSetDevice(ctx->device));
   // each lane shuffles its row in LDS when 64 rows fit, else in place in HBM
-  const size_t lds = (size_t)64 * n * 2;
+  const size_t lds = (size_t)64 * tokens * 2;
   const bool in_lds = lds <= ctx->max_lds;
-  RandArgs a{count, n, (int)ld, tour_bytes, in_lds ? 1 : 0, (uint32_t)seed,
+  RandArgs a{count, n, n_sep, (int)ld, tour_bytes, in_lds ? 1 : 0, (uint32_t)seed,
              (uint32_t)(seed >> 32), stream_id, d_tours};
   if (in_lds && lds > 65536)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(random_tours_kernel),

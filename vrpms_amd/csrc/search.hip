@@ -253,7 +253,7 @@ VRPMS_DEV uint64_t eval_mapped(const FastSplit& f, const unsigned char* E, uint3
     return *reinterpret_cast<const uint64_t*>(E + (__umul24(x, N8) + (y << 3)));
   };
   auto rd = [&](int q) { return (uint32_t)T[map_src(mm, q)]; };
-  const uint32_t smask = f.smask, kinc = 1u << f.ks, deadacc = f.dead;
+  const uint32_t smask = f.smask, kinc = 1u << f.ks;
   SplitAcc sa;
   sa.init(f);
   const int nfull = n >> 2;
@@ -290,15 +290,8 @@ VRPMS_DEV uint64_t eval_mapped(const FastSplit& f, const unsigned char* E, uint3
   if (rem > 0) sa.step_fast(e0, smask, kinc);
   if (rem > 1) sa.step_fast(e1, smask, kinc);
   if (rem > 2) sa.step_fast(e2, smask, kinc);
-  if (sa.hit_fleet_limit()) {  // rare: exact re-walk with the exhaustion test
-    sa.init(f);
-    uint32_t prev = 0;
-    for (int q = 0; q < n; ++q) {
-      const uint32_t c = rd(q);
-      sa.step(gat(prev, c), smask, kinc, deadacc);
-      prev = c;
-    }
-  }
+  if (sa.hit_fleet_limit())  // rare: exact re-walk (fleet limit, separators)
+    return exact_split(f, n, rd, gat).key;
   return sa.finish(f, n).key;
 }
 
@@ -1086,8 +1079,11 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
                             int32_t n, void* stream) {
   if (!ctx || !p) return fail(VRPMS_EINVAL, "vrpms_sa_run: NULL ctx/params");
   if (!ctx->has_instance) return fail(VRPMS_ESTATE, "vrpms_sa_run: no instance loaded");
-  if (p->chains <= 0 || p->steps < 0 || n < 0 || n > ctx->inst.N - 1)
-    return fail(VRPMS_EINVAL, "vrpms_sa_run: need chains > 0, steps >= 0, 0 <= n <= N-1");
+  // tours: customers, plus (CVRP) A10 separator tokens, fewer than K of
+  // them useful; at most N - 1 + K tokens
+  const int max_tokens = ctx->inst.N - 1 + (ctx->inst.problem == VRPMS_CVRP ? ctx->inst.K : 0);
+  if (p->chains <= 0 || p->steps < 0 || n < 0 || n > max_tokens)
+    return fail(VRPMS_EINVAL, "vrpms_sa_run: need chains > 0, steps >= 0, 0 <= n <= N-1 (+K for CVRP)");
   if (!d_cur || !d_cur_key || !d_best || !d_best_key)
     return fail(VRPMS_EINVAL, "vrpms_sa_run: NULL state buffer");
   VRPMS_HIP(hipSetDevice(ctx->device));

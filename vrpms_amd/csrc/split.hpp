@@ -1,4 +1,4 @@
-// Branch-free greedy split (SURVEY.md Appendix A5-A8) over the prefix-ret
+// Branch-free greedy split (SURVEY.md Appendix A5-A8, A10) over the prefix-ret
 // packed matrix, shared by the headline scoring kernel (eval_cvrp_words) and
 // the CVRP SA chain kernel (sa_packed_kernel) so both produce the same key
 // for the same tour, bit for bit, as oracle/spec.py eval_cvrp.
@@ -12,6 +12,9 @@
 //   rd'  = (acc & smask) | 1 << KS      finished route, vehicle count above KS
 //   dsum += f ? 0 : rd';  dmax = max(dmax, f ? 0 : rd')
 //   acc  = f ? t : (dsum >= K << KS ? DEAD : hi)
+// A10 separator tokens (0) need no special case: column 0 of E holds
+// lo = 0x7fffffff (never fits: the route closes) and hi = -lim (an empty
+// route), so a separator closes the route and opens the next vehicle.
 // The vehicle counter lives in dsum's high bits, starting at 2^B - K so that
 // exhausting the fleet sets bit 31; the accumulator is then parked at DEAD,
 // which never fits again and adds no duration, so every later customer adds
@@ -96,5 +99,53 @@ struct SplitAcc {
     return {cvrp_key(unv, s, m, f.objective), (int32_t)s, (int32_t)m, (int32_t)unv};
   }
 };
+
+// The exact split of one tour with the fleet limit and A10 separators
+// (token 0: close the route, open the next vehicle), walked token by token:
+// the slow path for a lane whose fast walk met the fleet limit.  `tok(q)`
+// is tour token q, `gat(a, b)` the biased packed entry E[a][b].  Once the
+// K-th route has closed, customers are counted unvisited and separators are
+// ignored.  Same result as step() + finish() on separator-free tours.
+template <class Tok, class Gat>
+VRPMS_DEV TourCost exact_split(const FastSplit& f, int n, Tok tok, Gat gat) {
+  const uint32_t kinc = 1u << f.ks, fresh = 0u - f.lim;
+  uint32_t acc = fresh, dsum = f.klim, dmax = 0, unv = 0, prev = 0;
+  bool dead = false;
+  for (int q = 0; q < n; ++q) {
+    const uint32_t c = tok(q);
+    if (dead) {
+      unv += c != 0u;
+      continue;
+    }
+    uint32_t next = fresh;  // a separator opens an empty route
+    if (c != 0u) {
+      const uint64_t e = gat(prev, c);
+      const uint32_t t = acc + (uint32_t)e;
+      if ((int32_t)t < 0) {  // fits
+        acc = t;
+        prev = c;
+        continue;
+      }
+      next = (uint32_t)(e >> 32);  // opens a route holding c
+    }
+    const uint32_t rdm = (acc & f.smask) | kinc;  // close route k
+    dsum += rdm;
+    dmax = max(dmax, rdm);
+    if ((int32_t)dsum < 0) {  // that was the K-th vehicle
+      dead = true;
+      unv += c != 0u;
+      continue;
+    }
+    acc = next;
+    prev = c;
+  }
+  uint32_t s = dsum & (kinc - 1u), m = dmax >= kinc ? dmax - kinc : 0u;
+  if (!dead) {
+    const uint32_t rd = acc & f.smask;  // close the last route (0 when empty)
+    s += rd;
+    m = max(m, rd);
+  }
+  return {cvrp_key(unv, s, m, f.objective), (int32_t)s, (int32_t)m, (int32_t)unv};
+}
 
 }  // namespace vrpms

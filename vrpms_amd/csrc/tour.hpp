@@ -44,8 +44,9 @@ struct TourCost {
   int32_t sum, max, unv;
 };
 
-// A4 (TSP) / A5-A7 (CVRP greedy split); `tour(i)` returns customer i
-// (values >= N are clamped to N-1 so a corrupt tour can never fault).
+// A4 (TSP) / A5-A7 (CVRP greedy split, A10 separator tokens 0); `tour(i)`
+// returns customer i (values >= N are clamped to N-1 so a corrupt tour can
+// never fault).
 template <bool CVRP, typename Mat, typename Tour>
 VRPMS_DEV TourCost eval_tour(const Mat& D, const SplitParams& sp, const Tour& tour, int n) {
   const uint32_t Nm1 = D.N - 1;
@@ -67,6 +68,24 @@ VRPMS_DEV TourCost eval_tour(const Mat& D, const SplitParams& sp, const Tour& to
     uint32_t prev = 0, unv = 0, dsum = 0, dmax = 0;
     for (int i = 0; i < n; ++i) {
       const uint32_t cc = min((uint32_t)tour(i), Nm1);
+      if (cc == 0) {  // A10 separator: close route k (if any), open vehicle k + 1
+        if (k < K) {
+          if (prev) {
+            t += D(t, prev, 0);
+            const uint32_t rd = (uint32_t)(t - sp.start[k]);
+            dsum += rd;
+            dmax = max(dmax, rd);
+          }
+          ++k;
+          if (k < K) {
+            load = 0;
+            t = sp.start[k];
+            prev = 0;
+            capk = sp.cap[k];
+          }
+        }
+        continue;
+      }
       const int dc = sp.dem[cc];
       if (k < K && load + dc > capk) {
         do {

@@ -67,13 +67,16 @@ class _Base:
 
 class SARunner(_Base):
     """Independent SA chains (one wavefront each), geometric cooling from
-    t0 to t_end over `total_steps` steps."""
+    t0 to t_end over `total_steps` steps.  `n_sep` A10 route separators
+    (CVRP) ride in every tour, so the moves also place route boundaries;
+    tours then hold n + n_sep tokens (self.n)."""
 
     def __init__(self, ctx: Context, n: int, chains: int = 1024, seed: int = 0,
                  total_steps: int = 2000, steps_per_epoch: int = 250, t0: float | None = None,
-                 t_end: float | None = None, durations=None):
+                 t_end: float | None = None, durations=None, n_sep: int = 0):
         torch = _torch()
-        self.ctx, self.n, self.seed = ctx, n, seed
+        self.ctx, self.n, self.seed = ctx, n + n_sep, seed
+        self.n_sep = n_sep
         self.chains = chains
         edge = typical_edge(durations) if durations is not None else 100.0
         t0 = t0 if t0 is not None else 0.5 * edge
@@ -82,7 +85,7 @@ class SARunner(_Base):
         self.inv_t = np.float32(1.0 / t0)
         self.steps_per_epoch = steps_per_epoch
         self.step = 0
-        self.cur = random_tours(ctx, chains, n, seed)
+        self.cur = ctx.random_tours(chains, n, seed, n_sep=n_sep)
         self.best_t = self.cur.clone()
         self.cur_key = torch.empty(chains, dtype=torch.int64, device=ctx.dev)
         self.best_key = torch.full((chains,), -1, dtype=torch.int64, device=ctx.dev)

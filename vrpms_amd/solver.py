@@ -165,8 +165,11 @@ def search(ctx: Context, ci: CompactInstance, algorithm: str, seed: int = 0,
     iters = knobs.get("iteration_count")
     if algorithm == "sa":
         steps = int(iters or knobs.get("steps", 4000))
+        # VRP: K - 1 route separators (A10) let the moves place route
+        # boundaries instead of leaving them to the greedy split alone
+        n_sep = int(knobs.get("separators", len(ci.capacities) - 1 if ci.problem == CVRP else 0))
         r = runners.SARunner(ctx, n, chains=int(knobs.get("chains", 1024)), seed=seed,
-                             total_steps=steps, durations=ci.durations)
+                             total_steps=steps, durations=ci.durations, n_sep=n_sep)
         epochs = max(1, steps // r.steps_per_epoch)
     elif algorithm == "ga":
         pop = int(knobs.get("random_permutation_count") or knobs.get("pop", 256))
@@ -229,6 +232,8 @@ def solve_vrp(algorithm: str, durations, locations, capacities, start_times,
     if tour:
         veh, durs = _decode(ctx, tour)
         for c, v in zip(tour, veh):
+            if v == -2:                # A10 separator: a route boundary, not a customer
+                continue
             (routes[v] if v >= 0 else unvisited).append(ci.nodes[c])
     else:
         durs = [0] * K
