@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--T", type=float, nargs="+", default=[1.0, 10.0, 60.0])
     ap.add_argument("--seeds", type=int, nargs="+", default=[0, 1, 2, 3, 4])
     ap.add_argument("--chains", type=int, default=4096)
+    ap.add_argument("--instance", default="cvrp100", choices=["cvrp100", "cvrp200", "x1000"],
+                    help="cfg 2 CVRP-100 K=8, CVRP-200 K=16, or cfg 4 X-style CVRP-1000")
     ap.add_argument("--sep", type=int, default=None,
                     help="A10 route separators per tour (default K - 1; 0 = plain giant tours)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "quality_sweep.json"))
@@ -42,12 +44,15 @@ def main():
     cells = []
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     t_start = time.time()
+    make = {"cvrp100": lambda s: synth.cvrp(100, 8, seed=s),
+            "cvrp200": lambda s: synth.cvrp(200, 16, seed=s),
+            "x1000": lambda s: synth.x_style(1000, seed=s)}[args.instance]
     for seed in args.seeds:
-        inst = synth.cvrp(100, 8, seed=seed)
+        inst = make(seed)
         ctx.set_instance(CVRP, inst.durations, inst.demand, inst.capacities, inst.start_times)
         for T in args.T:
             q = bench.quality(ctx, inst, T, 1, 0, None, with_cpu=True, chains=args.chains,
-                              label=f"cvrp100_k8 seed {seed}", n_sep=args.sep)
+                              label=f"{args.instance} seed {seed}", n_sep=args.sep)
             q["seed"] = seed
             cells.append(q)
             print(json.dumps({"seed": seed, "T_s": T, "gpu": q["gpu"]["duration_sum"],
@@ -65,7 +70,7 @@ def main():
             with open(args.out, "w") as f:
                 json.dump({"metric": "best-cost gap at equal wall time, (gpu - cpu) / cpu "
                                      "on durationSum, negative = GPU better",
-                           "workload": "CVRP-100, K=8 (synth.cvrp), SA on both sides",
+                           "workload": f"{args.instance} (vrpms_amd.synth), SA on both sides",
                            "separators": cells[0]["separators"],
                            "cpu_cores": cells[0]["cpu"]["cores"],
                            "summary": summary, "cells": cells}, f, indent=1)
