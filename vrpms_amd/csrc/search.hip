@@ -249,8 +249,16 @@ struct SaPackedArgs {
 // Key of tour T (u8, LDS, zero padded to n + 12) read through map mm.
 VRPMS_DEV uint64_t eval_mapped(const FastSplit& f, const unsigned char* E, uint32_t N8,
                                const uint8_t* T, int n, const MoveMap& mm) {
+  // E[x][y] at x * 8N + 8y: the pair laid out as u16 halves (one v_lshl_or)
+  // and v_dot2_u32_u16 against (8N, 8) with the LDS base as accumulator
+  typedef unsigned short us2v __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(3))) const uint64_t lds_u64v;
+  const uint32_t ebase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const unsigned char*)E;
+  const us2v w8 = {(unsigned short)N8, (unsigned short)8};
   auto gat = [&](uint32_t x, uint32_t y) {
-    return *reinterpret_cast<const uint64_t*>(E + (__umul24(x, N8) + (y << 3)));
+    const uint32_t addr =
+        __builtin_amdgcn_udot2(__builtin_bit_cast(us2v, x | (y << 16)), w8, ebase, false);
+    return *(lds_u64v*)(uintptr_t)addr;
   };
   auto rd = [&](int q) { return (uint32_t)T[map_src(mm, q)]; };
   const uint32_t smask = f.smask, kinc = 1u << f.ks;
