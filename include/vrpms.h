@@ -134,6 +134,10 @@ int vrpms_eval_path(vrpms_ctx* ctx, int32_t perm_bytes, int64_t ld, const void* 
  *   kernel whenever the island fits the LDS), 2 = force the three-kernel
  *   path (breed / score / select launches per generation); A/B. */
 #define VRPMS_OPT_GA_FUSED 7
+/*   VRPMS_OPT_SA_ROUTE: 0 = auto (windowed SA on an exchangeable fleet prices
+ *   moves route-locally, sa_route_kernel), 2 = force full re-evaluation of
+ *   every move (sa_kernel); A/B. */
+#define VRPMS_OPT_SA_ROUTE 8
 int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value);
 
 /* Decode ONE giant tour into the result dict of api/vrp/ga/index.py:49-53
@@ -168,6 +172,8 @@ typedef struct {
   float inv_alpha;  /* per-step factor on 1/T (1/alpha for T *= alpha) */
   uint64_t seed;
   uint64_t step0;   /* global index of the first step (Philox counter) */
+  int32_t window;   /* A11: 0 = moves over the whole tour; W > 0 = the second
+                       position within W of the first (large tours) */
 } vrpms_sa_params;
 
 /* d_cur [chains][n] in/out (cur_key out); d_best/d_best_key in/out (set
@@ -279,6 +285,15 @@ typedef struct {
 int vrpms_random_tours(vrpms_ctx* ctx, int64_t count, int32_t n, int32_t n_sep, int64_t ld,
                        int32_t tour_bytes, uint64_t seed, uint32_t stream_id, void* d_tours,
                        void* stream);
+
+/* Feasible separator tours for the SA start: row r of d_out [count][n+n_sep]
+ * is row r of d_in [count][n] (customers only) with a separator (0) where
+ * the loaded instance's greedy split would open the next route (at most
+ * n_sep, never before the first customer; route i's capacity is
+ * capacities[min(i, K-1)]) and the unused separators appended -- same cost
+ * as the input while the fleet lasts (oracle/spec.py insert_separators). */
+int vrpms_insert_separators(vrpms_ctx* ctx, const uint16_t* d_in, int64_t count, int32_t n,
+                            int32_t n_sep, uint16_t* d_out, void* stream);
 
 /* The E best rows of a pool by (key, index), ascending: d_tours [E][n],
  * d_keys [E] (0 < E <= min(count, 1024)). */

@@ -183,6 +183,24 @@ static move_t decode_move(uint32_t r0, uint32_t r1, uint32_t r2, int n) {
   return m;
 }
 
+/* A11 (oracle/spec.py decode_move_window): j within `window` of i */
+static move_t decode_move_window(uint32_t r0, uint32_t r1, uint32_t r2, int n, int window) {
+  if (window <= 0 || 2 * window + 1 >= n) return decode_move(r0, r1, r2, n);
+  move_t m;
+  m.typ = (int)(r0 % 3u);
+  m.i = (int)(r1 % (uint32_t)n);
+  const int o = (int)(r2 % (uint32_t)(2 * window));
+  const int d = o < window ? o - window : o - window + 1;
+  m.j = m.i + d;
+  if (m.j < 0 || m.j >= n) m.j = m.i - d;
+  if (m.typ != 2 && m.i > m.j) {
+    int t = m.i;
+    m.i = m.j;
+    m.j = t;
+  }
+  return m;
+}
+
 static inline int moved_index(int q, const move_t* m) {
   int i = m->i, j = m->j;
   if (m->typ == 0) return q == i ? j : (q == j ? i : q);
@@ -292,7 +310,7 @@ int oracle_sa_run(int problem, const int32_t* D, int H, int N, const int32_t* de
                   const int32_t* cap, const int32_t* st, int K, int objective, uint16_t* cur,
                   uint64_t* cur_key, uint16_t* best, uint64_t* best_key, int chains, int n,
                   int steps, float inv_t0, float inv_alpha, uint64_t seed, uint64_t step0,
-                  int threads) {
+                  int window, int threads) {
   inst_t I = {problem, H, N, K, objective, D, dem, cap, st};
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 #ifdef _OPENMP
@@ -318,7 +336,7 @@ int oracle_sa_run(int problem, const int32_t* D, int H, int N, const int32_t* de
       for (int lane = 0; lane < 64; ++lane) {
         u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)c, (uint32_t)lane, k0,
                          k1);
-        move_t m = decode_move(r.x, r.y, r.z, n);
+        move_t m = decode_move_window(r.x, r.y, r.z, n, window);
         uint64_t kk = tour_key(&I, A, n, &m);
         if (kk < kbest) {
           kbest = kk;

@@ -330,6 +330,47 @@ def decode_move(r0: int, r1: int, r2: int, n: int):
     return typ, i, j
 
 
+def decode_move_window(r0: int, r1: int, r2: int, n: int, window: int):
+    """A11: a move whose second position lies within `window` of the first
+    (the neighbourhood SA samples on large tours).  window <= 0 or
+    2 * window + 1 >= n: decode_move.  Else i = r1 % n, o = r2 % (2 window),
+    d = o - window (o < window) or o - window + 1, j = i + d, reflected to
+    i - d when outside [0, n); swap / 2-opt canonicalised i < j."""
+    if window <= 0 or 2 * window + 1 >= n:
+        return decode_move(r0, r1, r2, n)
+    typ = r0 % 3
+    i = r1 % n
+    o = r2 % (2 * window)
+    d = o - window if o < window else o - window + 1
+    j = i + d
+    if j < 0 or j >= n:
+        j = i - d
+    if typ != MOVE_RELOCATE and i > j:
+        i, j = j, i
+    return typ, i, j
+
+
+def insert_separators(perm, n_sep: int, demand, capacities):
+    """The giant tour `perm` (customers only) with A10 separators at the
+    route boundaries the greedy split (A6) places: a 0 goes where a customer
+    does not fit and opens the next route (at most n_sep of them); the
+    separators left over are appended.  Same cost as `perm` when the
+    greedy split never runs out of vehicles; used for feasible SA starts."""
+    dem = [int(x) for x in demand]
+    cap = [int(x) for x in capacities]
+    K = len(cap)
+    out, load, used = [], 0, 0
+    for c in perm:
+        c = int(c)
+        if used < n_sep and load > 0 and load + dem[c] > cap[min(used, K - 1)]:
+            out.append(0)
+            used += 1
+            load = 0
+        load += dem[c]
+        out.append(c)
+    return out + [0] * (n_sep - used)
+
+
 def apply_move(perm, typ: int, i: int, j: int):
     """Return a new list with the move applied.
 

@@ -50,13 +50,14 @@ class StandInContext:
                                self.inst.start_times, self.problem, self.objective)[0]
         return _i64([int(x) for x in k])
 
-    def sa_run(self, cur, cur_key, best, best_key, steps, inv_t0, inv_alpha, seed, step0):
+    def sa_run(self, cur, cur_key, best, best_key, steps, inv_t0, inv_alpha, seed, step0,
+               window=0):
         c = cur.numpy().view(np.uint16).copy()
         b = best.numpy().view(np.uint16).copy()
         bk = np.array(_u64(best_key), dtype=np.uint64)
         ck = coracle.sa_run(self.inst.durations, c, b, bk, steps, inv_t0, inv_alpha, seed, step0,
                             self.inst.demand, self.inst.capacities, self.inst.start_times,
-                            self.problem, self.objective)
+                            self.problem, self.objective, window=window)
         cur.copy_(_as_i16(c))
         best.copy_(_as_i16(b))
         cur_key.copy_(_i64([int(x) for x in ck]))
@@ -72,6 +73,12 @@ class StandInContext:
         import torch
         pop.copy_(torch.tensor(rp, dtype=torch.int16))
         keys.copy_(_i64([k for ks in rk for k in ks]).view(islands, P))
+
+    def insert_separators(self, tours, n_sep):
+        import torch
+        rows = [spec.insert_separators(t, n_sep, self.inst.demand, self.inst.capacities)
+                for t in tours.tolist()]
+        return torch.tensor(rows, dtype=torch.int16)
 
     def argmin(self, keys):
         vals = _u64(keys)

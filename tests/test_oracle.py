@@ -187,6 +187,46 @@ def test_c_sa_matches_python_replay(coracle, kind):
     assert best.tolist() == ref[2] and [int(x) for x in bk] == ref[3]
 
 
+def test_c_sa_windowed_with_separators_matches_python_replay(coracle):
+    """A11 windowed moves on A10 separator tours: C == Python replay."""
+    from oracle import search
+    inst = synth.cvrp(30, 4, seed=6, slack=1.1)
+    rng = np.random.default_rng(2)
+    P = np.array([rng.permutation(np.concatenate([np.arange(1, 31), np.zeros(3, dtype=int)]))
+                  for _ in range(2)]).astype(np.uint16)
+    cur, best = P.copy(), P.copy()
+    bk = np.full(2, 2**64 - 1, dtype=np.uint64)
+    ck = coracle.sa_run(inst.durations, cur, best, bk, 12, 1 / 90.0, 1 / 0.97, 5, 2,
+                        inst.demand, inst.capacities, inst.start_times, window=4)
+    sc = search.Scorer(inst.durations, inst.demand, inst.capacities, inst.start_times)
+    ref = search.sa_run(sc, P.tolist(), P.tolist(), [2**64 - 1] * 2, 5, 2, 12, 1 / 90.0,
+                        1 / 0.97, window=4)
+    assert cur.tolist() == ref[0] and [int(x) for x in ck] == ref[1]
+    assert best.tolist() == ref[2] and [int(x) for x in bk] == ref[3]
+
+
+def test_windowed_moves_stay_in_window():
+    rng = np.random.default_rng(1)
+    for _ in range(2000):
+        n, W = int(rng.integers(12, 60)), int(rng.integers(1, 5))
+        r = [int(x) for x in rng.integers(0, 2**32, size=3, dtype=np.uint64)]
+        t, i, j = spec.decode_move_window(*r, n, W)
+        assert i != j and 0 <= i < n and 0 <= j < n and abs(i - j) <= W
+    assert spec.decode_move_window(5, 6, 7, 9, 4) == spec.decode_move(5, 6, 7, 9)
+
+
+def test_insert_separators_keeps_the_greedy_cost():
+    inst = synth.cvrp(40, 6, seed=3, slack=1.2)
+    P = synth.random_perms(30, 40, seed=5)
+    for p in P:
+        t = spec.insert_separators(p, 5, inst.demand, inst.capacities)
+        assert sorted(t) == [0] * 5 + list(range(1, 41))
+        a = spec.eval_cvrp(inst.durations, p, inst.demand, inst.capacities, inst.start_times)
+        b = spec.eval_cvrp(inst.durations, t, inst.demand, inst.capacities, inst.start_times)
+        if a["unvisited"] == 0:
+            assert (a["sum"], a["max"]) == (b["sum"], b["max"])
+
+
 @pytest.mark.parametrize("kind", ["symmetric", "asymmetric"])
 def test_c_tsp_batch_matches_python_replay(coracle, kind):
     """The C restatement of vrpms_tsp_batch_sa (used for the TSP-50 GPU

@@ -152,3 +152,71 @@ def test_random_tours_with_separators(ctx):
     for r in (0, 17, 49):
         assert T[r] == opool.philox_tour(30, 4, r, 1, 5)
     assert all(sorted(t) == [0] * 5 + list(range(1, 31)) for t in T)
+
+
+def _run_sa(ctx, P, steps, inv_t0, inv_alpha, seed, step0, window):
+    torch = torch_()
+    cur = torch.from_numpy(P).to(ctx.dev)
+    best = cur.clone()
+    ck = torch.empty(P.shape[0], dtype=torch.int64, device=ctx.dev)
+    bk = torch.full((P.shape[0],), -1, dtype=torch.int64, device=ctx.dev)
+    ctx.sa_run(cur, ck, best, bk, steps=steps, inv_t0=inv_t0, inv_alpha=inv_alpha, seed=seed,
+               step0=step0, window=window)
+    return cur.cpu().numpy(), u64(ck), best.cpu().numpy(), u64(bk)
+
+
+ROUTE_CASES = [
+    # cfg 4: X-1000, K - 1 separators where the greedy split closes routes (feasible start)
+    ("x1000_greedy", lambda: synth.x_style(1000, seed=1), "greedy", 16, 40, 1 / 300.0, 32),
+    # cfg 3: hour-indexed TD-200 (one start time), random separators: an infeasible start,
+    # so moves that leave customers unserved are re-evaluated in full
+    ("td200_random", lambda: synth.td_cvrp(200, 16, seed=2), "random", 8, 30, 1 / 200.0, 16),
+    # hot chain: the unserved-move shortcut is off (invT < 2^-20)
+    ("cvrp150_hot", lambda: synth.cvrp(150, 12, seed=3), "greedy", 8, 30, 1e-7, 8),
+]
+
+
+@pytest.mark.parametrize("name,maker,start,chains,steps,inv_t0,window", ROUTE_CASES,
+                         ids=[c[0] for c in ROUTE_CASES])
+def test_route_local_sa_matches_c_restatement(ctx, coracle, name, maker, start, chains, steps,
+                                              inv_t0, window):
+    """sa_route_kernel (windowed moves priced route-locally) against the C
+    restatement's full re-evaluation, and against sa_kernel on the device."""
+    inst = maker()
+    load(ctx, inst)
+    S = inst.K - 1
+    if start == "greedy":
+        P0 = synth.random_perms(chains, inst.n, seed=9, dtype=np.uint16)
+        P = np.array([spec.insert_separators(p, S, inst.demand, inst.capacities) for p in P0])
+        torch = torch_()
+        dev = ctx.insert_separators(torch.from_numpy(P0.astype(np.int16)).to(ctx.dev), S)
+        assert dev.cpu().numpy().tolist() == P.tolist()
+    else:
+        P = sep_tours(chains, inst.n, S, seed=9, dtype=np.uint16)
+    P = P.astype(np.int16)
+    got = _run_sa(ctx, P, steps, inv_t0, 1 / 0.99, 21, 7, window)
+    ccur, cbest = P.view(np.uint16).copy(), P.view(np.uint16).copy()
+    cbk = np.full(chains, 2**64 - 1, dtype=np.uint64)
+    cck = coracle.sa_run(inst.durations, ccur, cbest, cbk, steps, inv_t0, 1 / 0.99, 21, 7,
+                         inst.demand, inst.capacities, inst.start_times, window=window)
+    assert (got[0].view(np.uint16) == ccur).all()
+    assert got[1] == [int(x) for x in cck] and got[3] == [int(x) for x in cbk]
+    assert (got[2].view(np.uint16) == cbest).all()
+    ctx.set_sa_route(2)
+    try:
+        full = _run_sa(ctx, P, steps, inv_t0, 1 / 0.99, 21, 7, window)
+    finally:
+        ctx.set_sa_route(0)
+    assert (full[0] == got[0]).all() and full[1] == got[1] and full[3] == got[3]
+
+
+def test_route_local_sa_small_matches_python_oracle(ctx):
+    inst = synth.cvrp(24, 4, seed=11, slack=1.15)
+    load(ctx, inst)
+    P = sep_tours(3, inst.n, 3, seed=2, dtype=np.uint16).astype(np.int16)
+    got = _run_sa(ctx, P, 15, 1 / 80.0, 1 / 0.98, 4, 0, 3)
+    sc = search.Scorer(inst.durations, inst.demand, inst.capacities, inst.start_times)
+    ref = search.sa_run(sc, P.tolist(), P.tolist(), [2**64 - 1] * 3, 4, 0, 15, 1 / 80.0,
+                        1 / 0.98, window=3)
+    assert got[0].tolist() == ref[0] and got[1] == ref[1]
+    assert got[2].tolist() == ref[2] and got[3] == ref[3]

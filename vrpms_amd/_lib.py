@@ -31,6 +31,7 @@ OPT_WORDS_ILP = 4
 OPT_WORDS_LOOKAHEAD = 5
 OPT_ROWS_CONFIG = 6
 OPT_GA_FUSED = 7
+OPT_SA_ROUTE = 8
 OBJ_SUM = 0
 OBJ_MAX = 1
 INJECT_WORST = 0
@@ -45,7 +46,8 @@ _u64 = _c.c_uint64
 
 class SaParams(ctypes.Structure):
     _fields_ = [("chains", _i32), ("steps", _i32), ("inv_t0", ctypes.c_float),
-                ("inv_alpha", ctypes.c_float), ("seed", _u64), ("step0", _u64)]
+                ("inv_alpha", ctypes.c_float), ("seed", _u64), ("step0", _u64),
+                ("window", _i32)]
 
 
 class GaParams(ctypes.Structure):
@@ -90,6 +92,7 @@ SIGNATURES = {
                                       _vp]),
     "vrpms_random_tours": (_c.c_int, [_vp, _i64, _i32, _i32, _i64, _i32, _u64, _c.c_uint32, _vp,
                                       _vp]),
+    "vrpms_insert_separators": (_c.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp]),
     "vrpms_pool_elites": (_c.c_int, [_vp, _c.POINTER(Pool), _i32, _vp, _vp, _vp]),
     "vrpms_pool_inject": (_c.c_int, [_vp, _c.POINTER(Pool), _i32, _vp, _vp, _i32, _vp]),
     "vrpms_island_msg_bytes": (_i64, [_i32, _i32]),

@@ -170,6 +170,10 @@ class Context:
         """Path 0 of vrpms_eval: 0 = auto (eval_cvrp_rows2), 1 = eval_cvrp_packed."""
         check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_WORDS_KERNEL, int(gen)))
 
+    def set_sa_route(self, mode: int):
+        """0 = auto (route-local move pricing for windowed SA), 2 = full re-evaluation."""
+        check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_SA_ROUTE, int(mode)))
+
     def set_ga_fused(self, mode: int):
         """0 = auto (fused one-workgroup-per-island GA when it fits), 2 = three kernels."""
         check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_GA_FUSED, int(mode)))
@@ -218,11 +222,12 @@ class Context:
 
     # -- search kernels (state lives in caller-owned device tensors) ----------
     def sa_run(self, cur, cur_key, best, best_key, steps: int, inv_t0: float, inv_alpha: float,
-               seed: int, step0: int):
-        """Advance every chain (rows of the int16 [chains][n] tensor ``cur``)."""
+               seed: int, step0: int, window: int = 0):
+        """Advance every chain (rows of the int16 [chains][n] tensor ``cur``);
+        window > 0 samples A11 windowed moves."""
         chains, n = cur.shape
         p = _lib.SaParams(chains, int(steps), float(inv_t0), float(inv_alpha),
-                          int(seed) & (2**64 - 1), int(step0))
+                          int(seed) & (2**64 - 1), int(step0), int(window))
         check(self.lib.vrpms_sa_run(self._ctx, ctypes.byref(p), cur.data_ptr(),
                                     cur_key.data_ptr(), best.data_ptr(), best_key.data_ptr(), n,
                                     self.stream()))
@@ -282,7 +287,7 @@ class Context:
         tours = torch.empty((R, max(N - 1, 1)), dtype=torch.int16, device=self.dev)
         keys = torch.empty(R, dtype=torch.int64, device=self.dev)
         p = _lib.SaParams(4 * R, int(steps), float(inv_t0), float(inv_alpha),
-                          int(seed) & (2**64 - 1), 0)
+                          int(seed) & (2**64 - 1), 0, 0)
         check(self.lib.vrpms_tsp_batch_sa(self._ctx, mats.data_ptr(), R, N, ctypes.byref(p),
                                           tours.data_ptr(), keys.data_ptr(), self.stream()))
         return tours, keys
@@ -301,6 +306,16 @@ class Context:
                                           perm_dtype_bytes(out), int(seed) & (2**64 - 1),
                                           int(stream_id) & 0xFFFFFFFF, out.data_ptr(),
                                           self.stream()))
+        return out
+
+    def insert_separators(self, tours, n_sep: int):
+        """int16 [count][n] customer tours -> [count][n + n_sep] with A10
+        separators at the greedy split's route boundaries (vrpms_insert_separators)."""
+        torch = _torch()
+        count, n = tours.shape
+        out = torch.empty((count, n + int(n_sep)), dtype=torch.int16, device=self.dev)
+        check(self.lib.vrpms_insert_separators(self._ctx, tours.contiguous().data_ptr(), count, n,
+                                               int(n_sep), out.data_ptr(), self.stream()))
         return out
 
     @staticmethod

@@ -228,6 +228,12 @@ int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value) {
     ctx->opt_words_kernel = value;
     return VRPMS_OK;
   }
+  if (option == VRPMS_OPT_SA_ROUTE) {
+    if (value != 0 && value != 2)
+      return fail(VRPMS_EINVAL, "vrpms_set_option: SA route must be 0 (auto) or 2 (full walks)");
+    ctx->opt_sa_route = value;
+    return VRPMS_OK;
+  }
   if (option == VRPMS_OPT_GA_FUSED) {
     if (value != 0 && value != 2)
       return fail(VRPMS_EINVAL, "vrpms_set_option: GA fused must be 0 (auto) or 2 (three kernels)");
@@ -323,6 +329,7 @@ int vrpms_set_instance(vrpms_ctx* ctx, int32_t problem, const int32_t* d_dur, in
   in.min_cap = problem == VRPMS_CVRP ? st[4] : INT_MAX;
   in.max_cap = problem == VRPMS_CVRP ? st[5] : INT_MAX;
   in.max_start = st[7];
+  in.min_start = st[6];
   in.symmetric = st[8] == 0;
   in.cap0 = caps[0];
   in.uniform_cap = std::all_of(caps.begin(), caps.end(), [&](int32_t c) { return c == caps[0]; });

@@ -18,7 +18,7 @@ enum MatTier : int {
 struct Instance {
   int problem = VRPMS_TSP;
   int H = 1, N = 0, K = 1, objective = VRPMS_OBJ_SUM;
-  int max_dur = 0, max_dem = 0, max_start = 0, min_cap = 0, max_cap = 0;
+  int max_dur = 0, max_dem = 0, max_start = 0, min_start = 0, min_cap = 0, max_cap = 0;
   bool uniform_cap = true;
   bool symmetric = false;      // hour slice 0 is symmetric (O(1) 2-opt delta for static TSP)
   int cap0 = 0;
@@ -53,7 +53,8 @@ struct vrpms_ctx {
   int opt_words_ilp = 0;        // candidates per lane in eval_cvrp_words2 (0 auto, 1, 2 or 3)
   int opt_words_lookahead = 0;  // VRPMS_OPT_WORDS_LOOKAHEAD (words2 gather lookahead, A/B)
   int opt_words_kernel = 0;     // VRPMS_OPT_WORDS_KERNEL (0 auto = words2/rows2, 1 = first generation)
-  int opt_ga_fused = 0;         // VRPMS_OPT_GA_FUSED (0 auto, 2 = force the three-kernel GA)
+  int opt_ga_fused = 0;
+  int opt_sa_route = 0;         // VRPMS_OPT_SA_ROUTE (0 auto, 2 = force full re-evaluation)         // VRPMS_OPT_GA_FUSED (0 auto, 2 = force the three-kernel GA)
   int opt_rows_config = 0;      // VRPMS_OPT_ROWS_CONFIG (0 auto, 1..5 force eval_cvrp_rows2's (CW, ILP))
   int32_t* d_stats = nullptr;   // scratch for set_instance validation
   uint64_t* d_scratch = nullptr;  // small reduction scratch

@@ -77,6 +77,33 @@ __global__ __launch_bounds__(64) void random_tours_kernel(RandArgs a) {
   }
 }
 
+// Separator insertion (oracle/spec.py insert_separators): row r of `out`
+// is row r of `in` (customers only, n of them) with a 0 wherever the greedy
+// split would open the next route (at most n_sep, never before the first
+// customer), the unused separators appended.  One lane per row.
+__global__ void insert_separators_kernel(const uint16_t* __restrict__ in, int64_t count, int n,
+                                         int nsep, const int32_t* __restrict__ dem,
+                                         const int32_t* __restrict__ cap, int K,
+                                         uint16_t* __restrict__ out) {
+  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (r >= count) return;
+  const uint16_t* t = in + r * n;
+  uint16_t* o = out + r * (int64_t)(n + nsep);
+  int load = 0, used = 0, w = 0;
+  for (int q = 0; q < n; ++q) {
+    const uint32_t c = t[q];
+    const int d = dem[c];
+    if (used < nsep && load > 0 && load + d > cap[min(used, K - 1)]) {
+      o[w++] = 0;
+      ++used;
+      load = 0;
+    }
+    load += d;
+    o[w++] = (uint16_t)c;
+  }
+  while (w < n + nsep) o[w++] = 0;
+}
+
 constexpr int kTopChunk = 2048;
 
 // Per chunk of kTopChunk entries: the E smallest (key', index) pairs, where
@@ -367,6 +394,23 @@ int vrpms_random_tours(vrpms_ctx* ctx, int64_t count, int32_t n, int32_t n_sep, 
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   random_tours_kernel<<<(unsigned)((count + 63) / 64), 64, in_lds ? lds : 0,
                         (hipStream_t)stream>>>(a);
+  VRPMS_HIP(hipGetLastError());
+  return VRPMS_OK;
+}
+
+int vrpms_insert_separators(vrpms_ctx* ctx, const uint16_t* d_in, int64_t count, int32_t n,
+                            int32_t n_sep, uint16_t* d_out, void* stream) {
+  if (!ctx) return fail(VRPMS_EINVAL, "vrpms_insert_separators: ctx is NULL");
+  if (!ctx->has_instance || ctx->inst.problem != VRPMS_CVRP)
+    return fail(VRPMS_ESTATE, "vrpms_insert_separators: needs a CVRP instance");
+  if (count < 0 || n < 0 || n > ctx->inst.N - 1 || n_sep < 0)
+    return fail(VRPMS_EINVAL, "vrpms_insert_separators: need count >= 0, 0 <= n <= N-1, n_sep >= 0");
+  if (count == 0 || n + n_sep == 0) return VRPMS_OK;
+  if (!d_in || !d_out) return fail(VRPMS_EINVAL, "vrpms_insert_separators: NULL buffer");
+  VRPMS_HIP(hipSetDevice(ctx->device));
+  const Instance& in = ctx->inst;
+  insert_separators_kernel<<<(unsigned)((count + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+      d_in, count, n, n_sep, in.dem, in.cap, in.K, d_out);
   VRPMS_HIP(hipGetLastError());
   return VRPMS_OK;
 }

@@ -114,7 +114,7 @@ VRPMS_DEV StagedInst<MatT, HM> stage_inst(const SearchInst& si, unsigned char* s
 // ===========================================================================
 struct SaArgs {
   SearchInst si;
-  int chains, n, steps;
+  int chains, n, steps, window;
   float inv_t0, inv_alpha;
   uint32_t seed_lo, seed_hi;
   uint64_t step0;
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(256) void sa_kernel(SaArgs a) {
     const uint64_t step = a.step0 + (uint64_t)s;
     const u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)chain,
                            (uint32_t)lane, a.seed_lo, a.seed_hi);
-    const Move m = decode_move(r.x, r.y, r.z, n);
+    const Move m = decode_move_window(r.x, r.y, r.z, n, a.window);
     uint64_t k;
     int nd = 0;
     if constexpr (kDelta) {
@@ -221,6 +221,299 @@ __global__ __launch_bounds__(256) void sa_kernel(SaArgs a) {
 }
 
 // ===========================================================================
+// Route-local SA (CVRP tours with A10 separators, exchangeable vehicles:
+// one capacity and one start time for the whole fleet, every demand fits an
+// empty vehicle).  Same chain, moves and acceptance as sa_kernel; what
+// changes is how a move is priced.  The separators cut the tour into
+// segments whose greedy split is independent of everything outside them,
+// so a move touching positions lo..hi changes only the segments holding lo
+// .. hi: a lane walks those (from the separator before lo to the one after
+// hi -- with A11 windowed moves a few routes instead of the whole tour) and
+// composes the key with per-segment totals of the current tour kept in LDS
+// (route count, duration sum and max, prefix / suffix scans of them).
+// Exact: a composed tour that keeps every customer served gets its exact
+// key; one that cannot (more closures before its last customer than
+// vehicles) is either re-evaluated in full or, when the current tour serves
+// everyone and the temperature makes accepting an unserved customer
+// impossible, given the largest key -- it can then neither win a feasible
+// argmin nor be accepted, so the trajectory equals full re-evaluation.
+// ===========================================================================
+struct RouteStats {
+  uint16_t* segid;  // [npad] separators before position q
+  uint16_t* send;   // [segs] position of segment s's terminator (n for the last)
+  uint32_t *rc, *ds, *dm, *ne;   // per segment: routes, duration sum / max, has a customer
+  uint32_t *rcp, *dsp, *pmx, *smx, *lnea;  // prefix sums, prefix / suffix max, any customer >= s
+  int32_t* xb;      // closures before the last customer in segments < s (-1: none)
+};
+
+// Wave-wide inclusive scan (add or max) of v over lanes (shuffle steps).
+template <bool MAX>
+VRPMS_DEV uint32_t wave_scan_incl(uint32_t v) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t o = (uint32_t)__shfl_up((int)v, off, 64);
+    if (lane >= off) v = MAX ? (o > v ? o : v) : v + o;
+  }
+  return v;
+}
+
+template <typename MatT, int HM>
+__global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const StagedInst<MatT, HM> I = stage_inst<MatT, HM>(a.si, smem);
+  const int n = a.n;
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  const int chain = blockIdx.x * 4 + wave;
+  const int K = a.si.K;
+  const int SEGS = K + 2;
+  const uint32_t npad = ((uint32_t)n + 7u) & ~7u;
+  const uint32_t wbytes = 4u * npad * 2u + (((uint32_t)SEGS * 2u + 3u) & ~3u) + 11u * SEGS * 4u;
+  unsigned char* wb = smem + inst_lds_bytes(a.si) + wave * ((wbytes + 15u) & ~15u);
+  if (chain >= a.chains) return;  // no block-wide barrier after this point
+  uint16_t* A = reinterpret_cast<uint16_t*>(wb);
+  uint16_t* B = A + npad;
+  uint16_t* Best = B + npad;
+  RouteStats R;
+  R.segid = Best + npad;
+  R.send = R.segid + npad;
+  uint32_t* u = reinterpret_cast<uint32_t*>(wb + 4u * npad * 2u + (((uint32_t)SEGS * 2u + 3u) & ~3u));
+  R.rc = u;
+  R.ds = u + SEGS;
+  R.dm = u + 2 * SEGS;
+  R.ne = u + 3 * SEGS;
+  R.rcp = u + 4 * SEGS;
+  R.dsp = u + 5 * SEGS;
+  R.pmx = u + 6 * SEGS;
+  R.smx = u + 7 * SEGS;
+  R.lnea = u + 8 * SEGS;
+  R.xb = reinterpret_cast<int32_t*>(u + 9 * SEGS);
+  const uint16_t* gcur = a.cur + (int64_t)chain * n;
+  for (int q = lane; q < n; q += 64) A[q] = gcur[q];
+  wave_sync();
+  const uint32_t Nm1 = (uint32_t)a.si.N - 1;
+  const int cap0 = I.sp.cap[0], st0 = I.sp.start[0];
+  const int32_t* dem = I.sp.dem;
+  // greedy split of tokens tok(q), q in [from, to), starting a fresh route:
+  // routes used (closures incl. the final one), duration sum / max, and the
+  // closures before the last customer (-1: no customer)
+  struct SegCost {
+    uint32_t rc, ds, dm;
+    int xs;
+  };
+  auto seg_walk = [&](int from, int to, auto tok) {
+    int load = 0, t = st0;
+    uint32_t prev = 0, cnt = 0, ds = 0, dm = 0;
+    int xs = -1;
+    auto close = [&]() {
+      if (prev) {
+        t += I.D(t, prev, 0);
+        const uint32_t rd = (uint32_t)(t - st0);
+        ds += rd;
+        dm = max(dm, rd);
+      }
+      ++cnt;
+      load = 0;
+      t = st0;
+      prev = 0;
+    };
+    for (int q = from; q < to; ++q) {
+      const uint32_t c = min((uint32_t)tok(q), Nm1);
+      if (c == 0) {
+        close();
+        continue;
+      }
+      const int d = dem[c];
+      if (load + d > cap0) close();
+      t += I.D(t, prev, c);
+      load += d;
+      prev = c;
+      xs = (int)cnt;
+    }
+    const int xs_last = xs;
+    close();
+    return SegCost{cnt, ds, dm, xs_last};
+  };
+  // segment index of every position and each segment's terminator; the
+  // number of separators
+  auto build_segments = [&]() -> int {
+    int carry = 0;
+    for (int base = 0; base < n; base += 64) {
+      const int q = base + lane;
+      const bool z = q < n && A[q] == 0;
+      const uint64_t ball = __ballot(z);
+      const int pre = carry + __popcll(ball & ((1ull << lane) - 1ull));
+      if (q < n) R.segid[q] = (uint16_t)pre;
+      if (z && pre < SEGS - 1) R.send[pre] = (uint16_t)q;
+      carry += __popcll(ball);
+    }
+    if (lane == 0 && carry < SEGS - 1) R.send[carry] = (uint16_t)n;
+    wave_sync();
+    return carry;
+  };
+  auto walk_segments = [&](int s0, int s1) {  // segments s0..s1 of A
+    for (int s = s0 + lane; s <= s1; s += 64) {
+      const int from = s ? R.send[s - 1] + 1 : 0, to = R.send[s];
+      const SegCost sc = seg_walk(from, to, [&](int q) { return (uint32_t)A[q]; });
+      R.rc[s] = sc.rc;
+      R.ds[s] = sc.ds;
+      R.dm[s] = sc.dm;
+      R.ne[s] = sc.xs >= 0 ? 1u : 0u;
+    }
+    wave_sync();
+  };
+  // prefix sums / maxima over segments 0..S (entries 0..S+1)
+  auto scan_segments = [&](int S) {
+    uint32_t crc = 0, cds = 0, cmx = 0;
+    int clnb = -1;
+    for (int base = 0; base <= S + 1; base += 64) {
+      const int s = base + lane;
+      const bool in = s <= S;
+      const uint32_t rc = in ? R.rc[s] : 0u, ds = in ? R.ds[s] : 0u, dm = in ? R.dm[s] : 0u;
+      const uint32_t irc = wave_scan_incl<false>(rc), ids = wave_scan_incl<false>(ds);
+      const uint32_t imx = wave_scan_incl<true>(dm);
+      const int nb = in && R.ne[s] ? s : -1;
+      const int ilnb = (int)wave_scan_incl<true>((uint32_t)(nb + 1)) - 1;  // last nonempty <= s
+      if (s <= S + 1) {  // exclusive: entries for segments < s
+        R.rcp[s] = crc + irc - rc;
+        R.dsp[s] = cds + ids - ds;
+      }
+      const uint32_t ex_mx = (uint32_t)__shfl_up((int)imx, 1, 64);
+      const int ex_lnb = __shfl_up(ilnb, 1, 64);
+      if (s <= S + 1) {
+        R.pmx[s] = max(cmx, lane ? ex_mx : 0u);
+        const int lnb = max(clnb, lane ? ex_lnb : -1);
+        R.xb[s] = lnb;  // segment index for now; turned into closures below
+      }
+      crc += (uint32_t)__shfl((int)irc, 63, 64);
+      cds += (uint32_t)__shfl((int)ids, 63, 64);
+      cmx = max(cmx, (uint32_t)__shfl((int)imx, 63, 64));
+      clnb = max(clnb, __shfl(ilnb, 63, 64));
+    }
+    wave_sync();
+    // suffix max of dm and "any customer at or after s", from the top
+    uint32_t smx = 0, sne = 0;
+    for (int top = S + 1; top >= 0; top -= 64) {
+      const int s = top - lane;
+      const bool in = s >= 0 && s <= S;
+      const uint32_t dm = in ? R.dm[s] : 0u, ne = in ? R.ne[s] : 0u;
+      const uint32_t imx = wave_scan_incl<true>(dm), ine = wave_scan_incl<true>(ne);
+      if (s >= 0) {
+        R.smx[s] = max(smx, imx);
+        R.lnea[s] = max(sne, ine);
+      }
+      smx = max(smx, (uint32_t)__shfl((int)imx, 63, 64));
+      sne = max(sne, (uint32_t)__shfl((int)ine, 63, 64));
+    }
+    wave_sync();
+    for (int s = lane; s <= S + 1; s += 64) {
+      const int lnb = R.xb[s];
+      R.xb[s] = lnb >= 0 ? (int32_t)(R.rcp[lnb + 1] - 1u) : -1;
+    }
+    wave_sync();
+  };
+
+  // the current tour
+  uint64_t ck;
+  {
+    auto tour = [&](int i) { return (uint32_t)A[i]; };
+    ck = eval_tour<true>(I.D, I.sp, tour, n).key;
+  }
+  int S = build_segments();
+  const bool route_ok = S + 1 <= K;  // wave-uniform: else every move is re-evaluated in full
+  if (route_ok) {
+    walk_segments(0, S);
+    scan_segments(S);
+  }
+  uint64_t bk = a.best_key[chain];
+  bool best_in_lds = false;
+  if (ck < bk) {
+    bk = ck;
+    for (int q = lane; q < n; q += 64) Best[q] = A[q];
+    best_in_lds = true;
+  }
+  float invT = a.inv_t0;
+  for (int st = 0; st < a.steps && n >= 2; ++st) {
+    const uint64_t step = a.step0 + (uint64_t)st;
+    const u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)chain,
+                           (uint32_t)lane, a.seed_lo, a.seed_hi);
+    const Move m = decode_move_window(r.x, r.y, r.z, n, a.window);
+    auto moved = [&](int q) { return (uint32_t)A[moved_index(q, m)]; };
+    uint64_t k;
+    // an unserved customer cannot be accepted from a tour serving everyone
+    // when 2^28 * invT puts the acceptance threshold at 0 (tour.hpp)
+    const bool shortcut = (ck >> 56) == 0 && invT >= 0x1p-20f;
+    int s_lo = 0, s_hi = 0;
+    bool full = !route_ok;
+    if (route_ok) {
+      const int lo = min(m.i, m.j), hi = max(m.i, m.j);
+      s_lo = R.segid[lo];
+      s_hi = R.segid[hi];
+      const int from = s_lo ? R.send[s_lo - 1] + 1 : 0, to = R.send[s_hi];
+      const SegCost sc = seg_walk(from, to, moved);
+      const uint32_t span_old = R.rcp[s_hi + 1] - R.rcp[s_lo];
+      int X;  // closures before the moved tour's last customer
+      if (R.lnea[s_hi + 1]) X = R.xb[S + 1] + (int)sc.rc - (int)span_old;
+      else if (sc.xs >= 0) X = (int)R.rcp[s_lo] + sc.xs;
+      else X = R.xb[s_lo];
+      if (X < K) {
+        const uint32_t dsum = R.dsp[S + 1] - (R.dsp[s_hi + 1] - R.dsp[s_lo]) + sc.ds;
+        const uint32_t dmax = max(max(R.pmx[s_lo], R.smx[s_hi + 1]), sc.dm);
+        k = cvrp_key(0, dsum, dmax, I.sp.objective);
+      } else if (shortcut) {
+        k = ~0ull;
+      } else {
+        full = true;
+      }
+    }
+    if (full) k = eval_tour<true>(I.D, I.sp, moved, n).key;
+    int bl;
+    k = wave_argmin_lane(k, bl);  // wave-uniform (key, lane) minimum
+    bool accept = k <= ck;
+    if (!accept) {
+      const uint64_t d = (k >> 28) - (ck >> 28);
+      const uint32_t dp = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
+      accept = ((uint32_t)wave_bcast((int)r.w, bl) >> 8) < accept_threshold(dp, invT);
+    }
+    if (accept) {
+      Move mb;
+      mb.typ = (uint32_t)wave_bcast((int)m.typ, bl);
+      mb.i = wave_bcast(m.i, bl);
+      mb.j = wave_bcast(m.j, bl);
+      const int bs_lo = wave_bcast(s_lo, bl), bs_hi = wave_bcast(s_hi, bl);
+      for (int q = lane; q < n; q += 64) B[q] = A[moved_index(q, mb)];
+      wave_sync();
+      uint16_t* t = A;
+      A = B;
+      B = t;
+      ck = k;
+      if (ck < bk) {
+        bk = ck;
+        for (int q = lane; q < n; q += 64) Best[q] = A[q];
+        best_in_lds = true;
+      }
+      wave_sync();
+      if (route_ok) {  // the move kept the separators of segments < s_lo and > s_hi in place
+        build_segments();
+        walk_segments(bs_lo, bs_hi);
+        scan_segments(S);
+      }
+    }
+    invT = invT * a.inv_alpha;
+  }
+  uint16_t* gout = a.cur + (int64_t)chain * n;
+  for (int q = lane; q < n; q += 64) gout[q] = A[q];
+  if (best_in_lds) {
+    uint16_t* gb = a.best + (int64_t)chain * n;
+    for (int q = lane; q < n; q += 64) gb[q] = Best[q];
+  }
+  if (lane == 0) {
+    a.cur_key[chain] = ck;
+    a.best_key[chain] = bk;
+  }
+}
+
+// ===========================================================================
 // SA fast path (static CVRP, uniform fleet, every demand fits an empty
 // vehicle): the same chain, moves and acceptance as sa_kernel, but each
 // candidate is priced with the branch-free split of split.hpp over the
@@ -235,7 +528,7 @@ constexpr int kSaPackedWaves = 16;
 
 struct SaPackedArgs {
   FastSplit f;
-  int chains, n, steps;
+  int chains, n, steps, window;
   float inv_t0, inv_alpha;
   uint32_t seed_lo, seed_hi;
   uint64_t step0;
@@ -342,7 +635,7 @@ __global__ __launch_bounds__(1024) void sa_packed_kernel(SaPackedArgs a) {
     const uint64_t step = a.step0 + (uint64_t)s;
     const u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)chain,
                            (uint32_t)lane, a.seed_lo, a.seed_hi);
-    const Move m = decode_move(r.x, r.y, r.z, n);
+    const Move m = decode_move_window(r.x, r.y, r.z, n, a.window);
     uint64_t k = eval_mapped(a.f, smem, N8, A, n, move_map(m));
     int bl;
     k = wave_argmin_lane(k, bl);  // wave-uniform (key, lane) minimum
@@ -1059,6 +1352,10 @@ struct SaK {
   static auto kernel() { return sa_kernel<MatT, HM, CVRP>; }
 };
 template <typename MatT, int HM, bool CVRP>
+struct RouteK {
+  static auto kernel() { return sa_route_kernel<MatT, HM>; }
+};
+template <typename MatT, int HM, bool CVRP>
 struct BfK {
   static auto kernel() { return bf_kernel<MatT, HM, CVRP>; }
 };
@@ -1101,7 +1398,7 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
     const size_t lds = (((size_t)f.N * f.N * 8 + 15) & ~(size_t)15) +
                        (size_t)kSaPackedWaves * 3 * tb;
     if (lds <= ctx->max_lds) {
-      SaPackedArgs pa{f, p->chains, n, p->steps, p->inv_t0, p->inv_alpha, (uint32_t)p->seed,
+      SaPackedArgs pa{f, p->chains, n, p->steps, p->window, p->inv_t0, p->inv_alpha, (uint32_t)p->seed,
                       (uint32_t)(p->seed >> 32), p->step0, tb, d_cur, d_cur_key, d_best,
                       d_best_key};
       if (lds > 65536)
@@ -1113,9 +1410,27 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
       return VRPMS_OK;
     }
   }
-  SaArgs a{search_inst(ctx), p->chains, n, p->steps, p->inv_t0, p->inv_alpha,
+  SaArgs a{search_inst(ctx), p->chains, n, p->steps, p->window, p->inv_t0, p->inv_alpha,
            (uint32_t)p->seed, (uint32_t)(p->seed >> 32), p->step0, d_cur, d_cur_key, d_best,
            d_best_key};
+  // route-local pricing (sa_route_kernel) for windowed SA on a fleet of
+  // exchangeable vehicles: one capacity, one start time, every demand fits
+  const Instance& in = ctx->inst;
+  if (p->window > 0 && in.problem == VRPMS_CVRP && in.uniform_cap &&
+      in.min_start == in.max_start && in.max_dem <= in.cap0 && ctx->opt_sa_route != 2) {
+    const size_t npad = ((size_t)n + 7) & ~(size_t)7;
+    const size_t segs = (size_t)in.K + 2;
+    const size_t wbytes = (4 * npad * 2 + ((segs * 2 + 3) & ~(size_t)3) + 11 * segs * 4 + 15) &
+                          ~(size_t)15;
+    size_t lds = inst_lds_bytes_host(a.si) + 4 * wbytes;
+    if (lds > ctx->max_lds) {
+      a.si.mat_lds = 0;
+      lds = inst_lds_bytes_host(a.si) + 4 * wbytes;
+    }
+    if (lds <= ctx->max_lds)
+      return launch_inst<RouteK>(ctx, dim3((p->chains + 3) / 4), dim3(256), lds,
+                                 (hipStream_t)stream, a);
+  }
   const size_t npad = ((size_t)n + 7) & ~(size_t)7;
   size_t lds = inst_lds_bytes_host(a.si) + 4 * 3 * npad * 2;
   if (lds > ctx->max_lds) {

@@ -147,6 +147,26 @@ VRPMS_DEV Move decode_move(uint32_t r0, uint32_t r1, uint32_t r2, int n) {
   return m;
 }
 
+// A11 (oracle/spec.py decode_move_window): the second position within
+// `window` of the first; window <= 0 or 2 window + 1 >= n: decode_move.
+VRPMS_DEV Move decode_move_window(uint32_t r0, uint32_t r1, uint32_t r2, int n, int window) {
+  if (window <= 0 || 2 * window + 1 >= n) return decode_move(r0, r1, r2, n);
+  Move m;
+  m.typ = r0 % 3u;
+  m.i = (int)(r1 % (uint32_t)n);
+  const int o = (int)(r2 % (uint32_t)(2 * window));
+  const int d = o < window ? o - window : o - window + 1;
+  int j = m.i + d;
+  if (j < 0 || j >= n) j = m.i - d;
+  m.j = j;
+  if (m.typ != kMoveRelocate && m.i > m.j) {
+    const int x = m.i;
+    m.i = m.j;
+    m.j = x;
+  }
+  return m;
+}
+
 // Position in the ORIGINAL tour read at position q of the moved tour.
 VRPMS_DEV int moved_index(int q, const Move& m) {
   const int i = m.i, j = m.j;

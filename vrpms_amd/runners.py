@@ -69,14 +69,18 @@ class SARunner(_Base):
     """Independent SA chains (one wavefront each), geometric cooling from
     t0 to t_end over `total_steps` steps.  `n_sep` A10 route separators
     (CVRP) ride in every tour, so the moves also place route boundaries;
-    tours then hold n + n_sep tokens (self.n)."""
+    tours then hold n + n_sep tokens (self.n).  `window` > 0 samples A11
+    windowed moves (priced route-locally on an exchangeable fleet);
+    `greedy_start` puts the separators where the greedy split closes routes
+    (a feasible start) instead of at random."""
 
     def __init__(self, ctx: Context, n: int, chains: int = 1024, seed: int = 0,
                  total_steps: int = 2000, steps_per_epoch: int = 250, t0: float | None = None,
-                 t_end: float | None = None, durations=None, n_sep: int = 0):
+                 t_end: float | None = None, durations=None, n_sep: int = 0, window: int = 0,
+                 greedy_start: bool = False):
         torch = _torch()
         self.ctx, self.n, self.seed = ctx, n + n_sep, seed
-        self.n_sep = n_sep
+        self.n_sep, self.window = n_sep, window
         self.chains = chains
         edge = typical_edge(durations) if durations is not None else 100.0
         t0 = t0 if t0 is not None else 0.5 * edge
@@ -85,7 +89,10 @@ class SARunner(_Base):
         self.inv_t = np.float32(1.0 / t0)
         self.steps_per_epoch = steps_per_epoch
         self.step = 0
-        self.cur = ctx.random_tours(chains, n, seed, n_sep=n_sep)
+        if n_sep and greedy_start:   # separators where the greedy split closes routes
+            self.cur = ctx.insert_separators(ctx.random_tours(chains, n, seed), n_sep)
+        else:
+            self.cur = ctx.random_tours(chains, n, seed, n_sep=n_sep)
         self.best_t = self.cur.clone()
         self.cur_key = torch.empty(chains, dtype=torch.int64, device=ctx.dev)
         self.best_key = torch.full((chains,), -1, dtype=torch.int64, device=ctx.dev)
@@ -93,7 +100,7 @@ class SARunner(_Base):
     def epoch(self, steps: int | None = None):
         s = self.steps_per_epoch if steps is None else steps
         self.ctx.sa_run(self.cur, self.cur_key, self.best_t, self.best_key, s, float(self.inv_t),
-                        float(self.inv_alpha), self.seed, self.step)
+                        float(self.inv_alpha), self.seed, self.step, window=self.window)
         for _ in range(s):      # same float32 recurrence as the kernel
             self.inv_t = np.float32(self.inv_t * self.inv_alpha)
         self.step += s
