@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--T", type=float, nargs="+", default=[1.0, 10.0, 60.0])
     ap.add_argument("--seeds", type=int, nargs="+", default=[0, 1, 2, 3, 4])
     ap.add_argument("--chains", type=int, default=4096)
+    ap.add_argument("--window", type=int, default=None,
+                    help="A11 move window (default: 0 for cvrp100, 32 otherwise)")
     ap.add_argument("--instance", default="cvrp100", choices=["cvrp100", "cvrp200", "x1000"],
                     help="cfg 2 CVRP-100 K=8, CVRP-200 K=16, or cfg 4 X-style CVRP-1000")
     ap.add_argument("--sep", type=int, default=None,
@@ -51,8 +53,11 @@ def main():
         inst = make(seed)
         ctx.set_instance(CVRP, inst.durations, inst.demand, inst.capacities, inst.start_times)
         for T in args.T:
+            window = args.window if args.window is not None else (
+                0 if args.instance == "cvrp100" else 32)
             q = bench.quality(ctx, inst, T, 1, 0, None, with_cpu=True, chains=args.chains,
-                              label=f"{args.instance} seed {seed}", n_sep=args.sep)
+                              label=f"{args.instance} seed {seed}", n_sep=args.sep,
+                              window=window, greedy_start=window > 0)
             q["seed"] = seed
             cells.append(q)
             print(json.dumps({"seed": seed, "T_s": T, "gpu": q["gpu"]["duration_sum"],
@@ -72,6 +77,7 @@ def main():
                                      "on durationSum, negative = GPU better",
                            "workload": f"{args.instance} (vrpms_amd.synth), SA on both sides",
                            "separators": cells[0]["separators"],
+                           "window": cells[0]["window"],
                            "cpu_cores": cells[0]["cpu"]["cores"],
                            "summary": summary, "cells": cells}, f, indent=1)
     print(json.dumps({"summary": summary}), flush=True)

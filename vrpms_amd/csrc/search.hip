@@ -447,8 +447,11 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
     bool full = !route_ok;
     if (route_ok) {
       const int lo = min(m.i, m.j), hi = max(m.i, m.j);
+      // the span runs from the separator before lo to the one after hi: a
+      // separator AT hi ends segment segid[hi] but moves with the move, so
+      // the span then reaches through the next segment
       s_lo = R.segid[lo];
-      s_hi = R.segid[hi];
+      s_hi = R.segid[hi] + (A[hi] == 0 ? 1 : 0);
       const int from = s_lo ? R.send[s_lo - 1] + 1 : 0, to = R.send[s_hi];
       const SegCost sc = seg_walk(from, to, moved);
       const uint32_t span_old = R.rcp[s_hi + 1] - R.rcp[s_lo];
