@@ -296,12 +296,14 @@ def other_configs(ctx, torch, dev, seed=0):
 
 
 def island_leg(ctx, torch, dev, world, rank, dist, epochs=20, steps=25, chains=1024, E=8,
-               every=5, seed=0):
+               every=5, seed=0, window=32):
     """BASELINE.json cfg 4 as a search, not a scoring pass: X-style CVRP-1000
     (u16 matrix L2-resident), `chains` SA chains per GPU, a fixed number of
     epochs with an elite exchange every `every` epochs -- an RCCL all-gather
     of every rank's E best (tour + key) over xGMI when N > 1, local
-    re-injection at N = 1.  Every rank runs the same control flow
+    re-injection at N = 1.  Tours carry K - 1 A10 separators and the moves
+    are A11-windowed, priced route-locally (sa_route_kernel): every sampled
+    move still gets its exact full-tour key.  Every rank runs the same control flow
     (islands.run_fixed), and a pre-flight all-reduce makes all ranks skip
     together if any rank failed to set up.  Reports whole-job full-tour
     evals/s inside the search (every sampled move is a full re-evaluation of
@@ -313,9 +315,12 @@ def island_leg(ctx, torch, dev, world, rank, dist, epochs=20, steps=25, chains=1
     try:
         x = synth.x_style(1000, seed=seed)
         ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
+        # the front-end's large-instance SA: K - 1 separators at the greedy
+        # split's route boundaries, A11 windowed moves priced route-locally
         r = runners.SARunner(ctx, x.n, chains=chains, seed=500 + rank,
                              total_steps=epochs * steps, steps_per_epoch=steps,
-                             durations=x.durations)
+                             durations=x.durations, n_sep=x.K - 1, window=window,
+                             greedy_start=True)
         r.epoch(2)                          # code object load, instance staging
         torch.cuda.synchronize(dev)
     except Exception:
@@ -344,6 +349,8 @@ def island_leg(ctx, torch, dev, world, rank, dist, epochs=20, steps=25, chains=1
         key, _ = islands.global_best(r)
     evals = world * chains * epochs * steps * 64
     return {"workload": "cfg4 X-style CVRP-1000, island SA", "vehicles": x.K,
+            "separators": x.K - 1, "window": window,
+            "kernel": "sa_route_kernel (route-local pricing of windowed moves)",
             "chains_per_gpu": chains, "epochs": epochs, "steps_per_epoch": steps,
             "moves_per_step": 64, "exchange_every": every, "elites": E,
             "exchange": "RCCL all_gather over xGMI" if world > 1 else "local re-injection",

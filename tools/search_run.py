@@ -1,8 +1,11 @@
 #!/usr/bin/env python3
 """Run only the search kernels on their bench workloads, a few launches each
--- a short target for rocprofv3 --pmc passes:
+-- a short target for rocprofv3 --pmc / --stats passes:
   cfg 5: tsp_batch_sa_kernel, 10,000 TSP-50 requests x 1000 SA steps
   cfg 2: sa_packed_kernel, 4096 SA chains on CVRP-100 K = 8, 400-step epochs
+  cfg 2: ga_fused_kernel, 256 islands x 256, 20 generations per call
+  cfg 4: sa_route_kernel, 1024 windowed SA chains on X-1000 with K - 1
+         separators (greedy start), 100-step epochs
 usage: search_run.py [reps]"""
 import os
 import sys
@@ -24,11 +27,20 @@ for _ in range(reps):
     ctx.tsp_batch_sa(mats, 1000, 1 / 80.0, 1 / 0.995, 1)
 torch.cuda.synchronize()
 del mats
-
 inst = synth.cvrp(100, 8, seed=0)
 ctx.set_instance(CVRP, inst.durations, inst.demand, inst.capacities, inst.start_times)
 r = runners.SARunner(ctx, inst.n, chains=4096, total_steps=400 * reps, durations=inst.durations)
 for _ in range(reps):
     r.epoch(400)
+ga = runners.GARunner(ctx, inst.n, islands=256, pop=256, seed=1, gens_per_epoch=20)
+for _ in range(reps):
+    ga.epoch()
 torch.cuda.synchronize()
-print("done", r.best()[0])
+x = synth.x_style(1000, seed=0)
+ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
+rx = runners.SARunner(ctx, x.n, chains=1024, total_steps=100 * reps, durations=x.durations,
+                      n_sep=x.K - 1, window=32, greedy_start=True)
+for _ in range(reps):
+    rx.epoch(100)
+torch.cuda.synchronize()
+print("done", r.best()[0], ga.best()[0], rx.best()[0])

@@ -35,6 +35,9 @@ ALGORITHMS = ("bf", "ga", "sa", "aco")
 # measured ~64 G evals/s of bf_kernel on one MI355X (bench "search.bf");
 # vrpms_bf_run itself accepts n <= 15 (nibble-packed tours)
 BF_MAX_CUSTOMERS = 13
+# SA on tours of more than SA_WINDOW_MIN_N customers samples A11 windowed
+# moves (second position within SA_WINDOW of the first)
+SA_WINDOW, SA_WINDOW_MIN_N = 32, 150
 
 
 @dataclass
@@ -168,8 +171,12 @@ def search(ctx: Context, ci: CompactInstance, algorithm: str, seed: int = 0,
         # VRP: K - 1 route separators (A10) let the moves place route
         # boundaries instead of leaving them to the greedy split alone
         n_sep = int(knobs.get("separators", len(ci.capacities) - 1 if ci.problem == CVRP else 0))
+        # large tours: A11 windowed moves (priced route-locally on an
+        # exchangeable fleet) from separators at the greedy route boundaries
+        window = int(knobs.get("window", SA_WINDOW if n > SA_WINDOW_MIN_N else 0))
         r = runners.SARunner(ctx, n, chains=int(knobs.get("chains", 1024)), seed=seed,
-                             total_steps=steps, durations=ci.durations, n_sep=n_sep)
+                             total_steps=steps, durations=ci.durations, n_sep=n_sep,
+                             window=window, greedy_start=window > 0 and n_sep > 0)
         epochs = max(1, steps // r.steps_per_epoch)
     elif algorithm == "ga":
         pop = int(knobs.get("random_permutation_count") or knobs.get("pop", 256))
