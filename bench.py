@@ -146,7 +146,7 @@ class _TimedCooling:
 
 
 def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label="cvrp100_k8 seed 0",
-            gpu_seed=None, n_sep=None, window=0, greedy_start=False):
+            gpu_seed=None, n_sep=None, window=0, window_types=0, start="random"):
     """Best-cost gap at fixed wall time (the metric's second half): the same SA
     (Philox streams, 64 sampled moves per step, geometric cooling from
     0.5 to 0.002 x the mean edge spread over the wall-time budget by
@@ -156,8 +156,9 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
     `seconds` of wall time are spent.  Both legs search giant tours with
     n_sep A10 route separators (default K - 1, the front-end's VRP SA), so
     the moves place route boundaries too; `window` > 0 samples A11 windowed
-    moves and `greedy_start` starts from separators at the greedy split's
-    route boundaries (large instances).  gap = (gpu - cpu) / cpu on the
+    moves of the A12 types `window_types`, and `start` places the separators
+    of the start tours ("random", "greedy": the greedy split's route
+    boundaries, "pack": first-fit routes -- large instances).  gap = (gpu - cpu) / cpu on the
     objective key's primary term (durationSum) with unvisited == 0."""
     import torch
     from vrpms_amd import islands, runners
@@ -167,14 +168,14 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
     edge = runners.typical_edge(inst.durations)
     t0, t_end = 0.5 * edge, 0.002 * edge
     warm = runners.SARunner(ctx, n, chains=chains, total_steps=1000, durations=inst.durations,
-                            n_sep=n_sep, window=window, greedy_start=greedy_start)
+                            n_sep=n_sep, window=window, window_types=window_types, start=start)
     warm.epoch(20)                       # first launch: code object load, LDS setup
     torch.cuda.synchronize(dev)
     del warm
     seed = (1000 + rank) if gpu_seed is None else gpu_seed
     r = runners.SARunner(ctx, n, chains=chains, seed=seed, total_steps=1000,
                          durations=inst.durations, t0=t0, t_end=t_end, n_sep=n_sep,
-                         window=window, greedy_start=greedy_start)
+                         window=window, window_types=window_types, start=start)
     if world > 1:
         dist.barrier()
     cool = _TimedCooling(seconds, t0, t_end)
@@ -198,18 +199,21 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
     if world > 1:
         key, _ = islands.global_best(r)
     out = {"T_s": seconds, "algorithm": "sa", "instance": label, "cooling": "wall-time geometric",
-           "separators": n_sep, "window": window, "greedy_start": greedy_start,
+           "separators": n_sep, "window": window, "window_types": window_types,
+           "start": start,
            "gpu": {"chains_per_gpu": chains, "steps_per_chain": r.step, "epochs": e,
                    "wall_s": gpu_wall, "unvisited": key >> 56,
                    "duration_sum": (key >> 28) & (2**28 - 1)}}
     if with_cpu:
         from oracle import coracle
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or coracle.max_threads()
-        if n_sep and greedy_start:
-            start = ctx.insert_separators(ctx.random_tours(threads, n, 7), n_sep)
+        if n_sep and start == "greedy":
+            t0_ = ctx.insert_separators(ctx.random_tours(threads, n, 7), n_sep)
+        elif n_sep and start == "pack":
+            t0_ = ctx.pack_separators(ctx.random_tours(threads, n, 7), n_sep)
         else:
-            start = ctx.random_tours(threads, n, 7, n_sep=n_sep)
-        cur = np.asarray(start.cpu().numpy()).view(np.uint16)
+            t0_ = ctx.random_tours(threads, n, 7, n_sep=n_sep)
+        cur = np.asarray(t0_.cpu().numpy()).view(np.uint16)
         cur = cur.copy()
         best = cur.copy()
         bk = np.full(threads, 2**64 - 1, dtype=np.uint64)
@@ -221,7 +225,7 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
                 break
             coracle.sa_run(inst.durations, cur, best, bk, steps, float(cool.inv_t), float(inv_a),
                            1, step, inst.demand, inst.capacities, inst.start_times,
-                           threads=threads, window=window)
+                           threads=threads, window=window, window_types=window_types)
             cool.advance(steps, inv_a)
             step += steps
         cpu_wall = cool.elapsed()
@@ -320,7 +324,7 @@ def island_leg(ctx, torch, dev, world, rank, dist, epochs=20, steps=25, chains=1
         r = runners.SARunner(ctx, x.n, chains=chains, seed=500 + rank,
                              total_steps=epochs * steps, steps_per_epoch=steps,
                              durations=x.durations, n_sep=x.K - 1, window=window,
-                             greedy_start=True)
+                             window_types=2, start="pack")
         r.epoch(2)                          # code object load, instance staging
         torch.cuda.synchronize(dev)
     except Exception:

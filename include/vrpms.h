@@ -174,6 +174,8 @@ typedef struct {
   uint64_t step0;   /* global index of the first step (Philox counter) */
   int32_t window;   /* A11: 0 = moves over the whole tour; W > 0 = the second
                        position within W of the first (large tours) */
+  uint32_t window_types; /* A12: move types the window applies to, bit t for
+                            type t (1 swap, 2 2-opt, 4 relocate); 0 = all */
 } vrpms_sa_params;
 
 /* d_cur [chains][n] in/out (cur_key out); d_best/d_best_key in/out (set
@@ -294,6 +296,15 @@ int vrpms_random_tours(vrpms_ctx* ctx, int64_t count, int32_t n, int32_t n_sep, 
  * as the input while the fleet lasts (oracle/spec.py insert_separators). */
 int vrpms_insert_separators(vrpms_ctx* ctx, const uint16_t* d_in, int64_t count, int32_t n,
                             int32_t n_sep, uint16_t* d_out, void* stream);
+
+/* First-fit start tours (oracle/spec.py pack_separators): each customer of
+ * row r of d_in [count][n], in order, joins the first of n_sep + 1 routes
+ * with room for it (the last route when none has); d_out [count][n + n_sep]
+ * lists the routes in order with one separator between consecutive routes.
+ * Packs a fleet with little spare capacity into K routes, where
+ * vrpms_insert_separators (next fit) runs out of vehicles on a random order. */
+int vrpms_pack_separators(vrpms_ctx* ctx, const uint16_t* d_in, int64_t count, int32_t n,
+                          int32_t n_sep, uint16_t* d_out, void* stream);
 
 /* The E best rows of a pool by (key, index), ascending: d_tours [E][n],
  * d_keys [E] (0 < E <= min(count, 1024)). */

@@ -183,9 +183,13 @@ static move_t decode_move(uint32_t r0, uint32_t r1, uint32_t r2, int n) {
   return m;
 }
 
-/* A11 (oracle/spec.py decode_move_window): j within `window` of i */
-static move_t decode_move_window(uint32_t r0, uint32_t r1, uint32_t r2, int n, int window) {
-  if (window <= 0 || 2 * window + 1 >= n) return decode_move(r0, r1, r2, n);
+/* A11 (oracle/spec.py decode_move_window): j within `window` of i, for the
+ * move types in `types` (A12; 0 = all) */
+static move_t decode_move_window(uint32_t r0, uint32_t r1, uint32_t r2, int n, int window,
+                                 uint32_t types) {
+  if (!types) types = 7u;
+  if (window <= 0 || 2 * window + 1 >= n || !((types >> (r0 % 3u)) & 1u))
+    return decode_move(r0, r1, r2, n);
   move_t m;
   m.typ = (int)(r0 % 3u);
   m.i = (int)(r1 % (uint32_t)n);
@@ -310,7 +314,7 @@ int oracle_sa_run(int problem, const int32_t* D, int H, int N, const int32_t* de
                   const int32_t* cap, const int32_t* st, int K, int objective, uint16_t* cur,
                   uint64_t* cur_key, uint16_t* best, uint64_t* best_key, int chains, int n,
                   int steps, float inv_t0, float inv_alpha, uint64_t seed, uint64_t step0,
-                  int window, int threads) {
+                  int window, uint32_t window_types, int threads) {
   inst_t I = {problem, H, N, K, objective, D, dem, cap, st};
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 #ifdef _OPENMP
@@ -336,7 +340,7 @@ int oracle_sa_run(int problem, const int32_t* D, int H, int N, const int32_t* de
       for (int lane = 0; lane < 64; ++lane) {
         u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)c, (uint32_t)lane, k0,
                          k1);
-        move_t m = decode_move_window(r.x, r.y, r.z, n, window);
+        move_t m = decode_move_window(r.x, r.y, r.z, n, window, window_types);
         uint64_t kk = tour_key(&I, A, n, &m);
         if (kk < kbest) {
           kbest = kk;

@@ -80,9 +80,10 @@ def accept_threshold(dp: int, invT) -> int:
 
 
 def sa_run(score: Scorer, cur_tours, best_tours, best_keys, seed: int, step0: int, steps: int,
-           inv_t0: float, inv_alpha: float, window: int = 0):
+           inv_t0: float, inv_alpha: float, window: int = 0, window_types: int = 0):
     """vrpms_sa_run: one chain per tour; returns (cur, cur_keys, best, best_keys).
-    `window` > 0 samples A11 windowed moves (spec.decode_move_window)."""
+    `window` > 0 samples A11 windowed moves (spec.decode_move_window) of the
+    A12 types `window_types` (0 = all)."""
     key = spec.seed_key(seed)
     cur_out, ck_out, best_out, bk_out = [], [], [], []
     for c, cur in enumerate(cur_tours):
@@ -99,7 +100,7 @@ def sa_run(score: Scorer, cur_tours, best_tours, best_keys, seed: int, step0: in
                 cands = []
                 for lane in range(64):
                     r = spec.philox4x32_10((step & M32, step >> 32, c, lane), key)
-                    m = spec.decode_move_window(r[0], r[1], r[2], n, window)
+                    m = spec.decode_move_window(r[0], r[1], r[2], n, window, window_types)
                     cands.append((score(spec.apply_move(cur, *m)), lane, m, r[3]))
                 kk, lane, m, r3 = min(cands, key=lambda t: (t[0], t[1]))
                 acc = kk <= ck

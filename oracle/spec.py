@@ -330,13 +330,20 @@ def decode_move(r0: int, r1: int, r2: int, n: int):
     return typ, i, j
 
 
-def decode_move_window(r0: int, r1: int, r2: int, n: int, window: int):
+def decode_move_window(r0: int, r1: int, r2: int, n: int, window: int, types: int = 0):
     """A11: a move whose second position lies within `window` of the first
     (the neighbourhood SA samples on large tours).  window <= 0 or
     2 * window + 1 >= n: decode_move.  Else i = r1 % n, o = r2 % (2 window),
     d = o - window (o < window) or o - window + 1, j = i + d, reflected to
-    i - d when outside [0, n); swap / 2-opt canonicalised i < j."""
-    if window <= 0 or 2 * window + 1 >= n:
+    i - d when outside [0, n); swap / 2-opt canonicalised i < j.
+
+    A12: `types` (bit t for move type t; 0 = all) limits the window to some
+    move types; a move of another type is drawn by decode_move.  Windowed
+    2-opt with unrestricted swap / relocate keeps reversals short (they are
+    priced by walking the reversed span) while customers still move
+    anywhere in the tour."""
+    types = types or 7
+    if window <= 0 or 2 * window + 1 >= n or not (types >> (r0 % 3)) & 1:
         return decode_move(r0, r1, r2, n)
     typ = r0 % 3
     i = r1 % n
@@ -369,6 +376,35 @@ def insert_separators(perm, n_sep: int, demand, capacities):
         load += dem[c]
         out.append(c)
     return out + [0] * (n_sep - used)
+
+
+def pack_separators(perm, n_sep: int, demand, capacities):
+    """First-fit start: the customers of `perm`, in that order, each go to
+    the first of n_sep + 1 routes with room for them (route b holds up to
+    cap[min(b, K - 1)]; a customer that fits nowhere joins the last route),
+    and the tour lists route 0, a separator, route 1, ... route n_sep, every
+    route in `perm` order.  Exactly n_sep separators.  Unlike
+    insert_separators (next fit) it packs a fleet with little spare capacity
+    into K routes, so SA starts feasible where the greedy split of a random
+    order runs out of vehicles."""
+    dem = [int(x) for x in demand]
+    cap = [int(x) for x in capacities]
+    K = len(cap)
+    B = n_sep + 1
+    load = [0] * B
+    bins = [[] for _ in range(B)]
+    for c in perm:
+        c = int(c)
+        d = dem[c]
+        b = next((b for b in range(B) if load[b] + d <= cap[min(b, K - 1)]), B - 1)
+        load[b] += d
+        bins[b].append(c)
+    out = []
+    for b in range(B):
+        if b:
+            out.append(0)
+        out += bins[b]
+    return out
 
 
 def apply_move(perm, typ: int, i: int, j: int):

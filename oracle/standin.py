@@ -51,13 +51,14 @@ class StandInContext:
         return _i64([int(x) for x in k])
 
     def sa_run(self, cur, cur_key, best, best_key, steps, inv_t0, inv_alpha, seed, step0,
-               window=0):
+               window=0, window_types=0):
         c = cur.numpy().view(np.uint16).copy()
         b = best.numpy().view(np.uint16).copy()
         bk = np.array(_u64(best_key), dtype=np.uint64)
         ck = coracle.sa_run(self.inst.durations, c, b, bk, steps, inv_t0, inv_alpha, seed, step0,
                             self.inst.demand, self.inst.capacities, self.inst.start_times,
-                            self.problem, self.objective, window=window)
+                            self.problem, self.objective, window=window,
+                            window_types=window_types)
         cur.copy_(_as_i16(c))
         best.copy_(_as_i16(b))
         cur_key.copy_(_i64([int(x) for x in ck]))
@@ -77,6 +78,12 @@ class StandInContext:
     def insert_separators(self, tours, n_sep):
         import torch
         rows = [spec.insert_separators(t, n_sep, self.inst.demand, self.inst.capacities)
+                for t in tours.tolist()]
+        return torch.tensor(rows, dtype=torch.int16)
+
+    def pack_separators(self, tours, n_sep):
+        import torch
+        rows = [spec.pack_separators(t, n_sep, self.inst.demand, self.inst.capacities)
                 for t in tours.tolist()]
         return torch.tensor(rows, dtype=torch.int16)
 

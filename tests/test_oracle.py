@@ -227,6 +227,72 @@ def test_insert_separators_keeps_the_greedy_cost():
             assert (a["sum"], a["max"]) == (b["sum"], b["max"])
 
 
+def test_pack_separators_first_fit():
+    """First-fit start: every customer once, exactly n_sep separators, each
+    route within its capacity whenever first fit finds room, routes in
+    input order; X-1000's fleet (K = LB + 2) packs where next fit fails."""
+    inst = synth.cvrp(40, 6, seed=3, slack=1.05)
+    for p in synth.random_perms(20, 40, seed=6):
+        t = spec.pack_separators(p, 5, inst.demand, inst.capacities)
+        assert sorted(t) == [0] * 5 + list(range(1, 41))
+        routes, cur = [], []
+        for c in t + [0]:
+            if c == 0:
+                routes.append(cur)
+                cur = []
+            else:
+                cur.append(c)
+        assert len(routes) == 6
+        pos = {int(c): i for i, c in enumerate(p)}
+        for r in routes:
+            assert [pos[c] for c in r] == sorted(pos[c] for c in r)
+        loads = [sum(int(inst.demand[c]) for c in r) for r in routes]
+        assert all(x <= int(inst.capacities[0]) for x in loads[:-1])
+    x = synth.x_style(1000, seed=0)
+    p = synth.random_perms(1, 1000, seed=1, dtype=np.uint16)[0]
+    packed = spec.eval_cvrp(x.durations, spec.pack_separators(p, x.K - 1, x.demand, x.capacities),
+                            x.demand, x.capacities, x.start_times)
+    greedy = spec.eval_cvrp(x.durations, spec.insert_separators(p, x.K - 1, x.demand,
+                                                                x.capacities),
+                            x.demand, x.capacities, x.start_times)
+    assert packed["unvisited"] == 0 and greedy["unvisited"] > 0
+
+
+def test_window_types_limit_the_window():
+    """A12: only the move types in the mask are windowed."""
+    rng = np.random.default_rng(4)
+    n, W = 200, 5
+    seen = set()
+    for _ in range(3000):
+        r = [int(v) for v in rng.integers(0, 2**32, size=3)]
+        t, i, j = spec.decode_move_window(*r, n, W, 2)
+        seen.add(t)
+        if t == 1:
+            assert 1 <= abs(i - j) <= W
+        else:
+            assert (t, i, j) == spec.decode_move(*r, n)
+        assert spec.decode_move_window(*r, n, W, 0) == spec.decode_move_window(*r, n, W, 7)
+    assert seen == {0, 1, 2}
+
+
+def test_c_sa_window_types_matches_python_replay(coracle):
+    """A12 (windowed 2-opt only) on separator tours: C == Python replay."""
+    from oracle import search
+    inst = synth.cvrp(36, 5, seed=8, slack=1.1)
+    rng = np.random.default_rng(3)
+    P = np.array([rng.permutation(np.concatenate([np.arange(1, 37), np.zeros(4, dtype=int)]))
+                  for _ in range(2)]).astype(np.uint16)
+    cur, best = P.copy(), P.copy()
+    bk = np.full(2, 2**64 - 1, dtype=np.uint64)
+    ck = coracle.sa_run(inst.durations, cur, best, bk, 15, 1 / 90.0, 1 / 0.97, 9, 4,
+                        inst.demand, inst.capacities, inst.start_times, window=3, window_types=2)
+    sc = search.Scorer(inst.durations, inst.demand, inst.capacities, inst.start_times)
+    ref = search.sa_run(sc, P.tolist(), P.tolist(), [2**64 - 1] * 2, 9, 4, 15, 1 / 90.0,
+                        1 / 0.97, window=3, window_types=2)
+    assert cur.tolist() == ref[0] and [int(x) for x in ck] == ref[1]
+    assert best.tolist() == ref[2] and [int(x) for x in bk] == ref[3]
+
+
 @pytest.mark.parametrize("kind", ["symmetric", "asymmetric"])
 def test_c_tsp_batch_matches_python_replay(coracle, kind):
     """The C restatement of vrpms_tsp_batch_sa (used for the TSP-50 GPU

@@ -154,57 +154,69 @@ def test_random_tours_with_separators(ctx):
     assert all(sorted(t) == [0] * 5 + list(range(1, 31)) for t in T)
 
 
-def _run_sa(ctx, P, steps, inv_t0, inv_alpha, seed, step0, window):
+def _run_sa(ctx, P, steps, inv_t0, inv_alpha, seed, step0, window, types=0):
     torch = torch_()
     cur = torch.from_numpy(P).to(ctx.dev)
     best = cur.clone()
     ck = torch.empty(P.shape[0], dtype=torch.int64, device=ctx.dev)
     bk = torch.full((P.shape[0],), -1, dtype=torch.int64, device=ctx.dev)
     ctx.sa_run(cur, ck, best, bk, steps=steps, inv_t0=inv_t0, inv_alpha=inv_alpha, seed=seed,
-               step0=step0, window=window)
+               step0=step0, window=window, window_types=types)
     return cur.cpu().numpy(), u64(ck), best.cpu().numpy(), u64(bk)
 
 
 ROUTE_CASES = [
-    # cfg 4: X-1000, K - 1 separators where the greedy split closes routes (feasible start)
-    ("x1000_greedy", lambda: synth.x_style(1000, seed=1), "greedy", 16, 40, 1 / 300.0, 32),
+    # cfg 4: X-1000, K - 1 separators where the greedy split closes routes
+    ("x1000_greedy", lambda: synth.x_style(1000, seed=1), "greedy", 16, 40, 1 / 300.0, 32, 0),
+    # cfg 4 as the front-end runs it: first-fit routes (a feasible start), windowed 2-opt,
+    # swap / relocate anywhere (two-zone pricing)
+    ("x1000_pack_2opt", lambda: synth.x_style(1000, seed=2), "pack", 16, 60, 1 / 300.0, 32, 2),
     # cfg 3: hour-indexed TD-200 (one start time), random separators: an infeasible start,
     # so moves that leave customers unserved are re-evaluated in full
-    ("td200_random", lambda: synth.td_cvrp(200, 16, seed=2), "random", 8, 30, 1 / 200.0, 16),
-    # hot chain: the unserved-move shortcut is off (invT < 2^-20)
-    ("cvrp150_hot", lambda: synth.cvrp(150, 12, seed=3), "greedy", 8, 30, 1e-7, 8),
+    ("td200_random", lambda: synth.td_cvrp(200, 16, seed=2), "random", 8, 30, 1 / 200.0, 16, 0),
+    ("td200_random_2opt", lambda: synth.td_cvrp(200, 16, seed=4), "random", 8, 30, 1 / 200.0, 16,
+     2),
+    # hot chains: the unserved-move shortcut is off (invT < 2^-20)
+    ("cvrp150_hot", lambda: synth.cvrp(150, 12, seed=3), "greedy", 8, 30, 1e-7, 8, 0),
+    ("cvrp150_pack_hot", lambda: synth.cvrp(150, 12, seed=5, slack=1.02), "pack", 8, 40, 1e-7, 6,
+     2),
+    # many separators per route (S > K - 1 is never route-local; S < K - 1 is)
+    ("cvrp120_few_seps", lambda: synth.cvrp(120, 10, seed=6), "pack_few", 8, 40, 1 / 100.0, 5, 2),
 ]
 
 
-@pytest.mark.parametrize("name,maker,start,chains,steps,inv_t0,window", ROUTE_CASES,
+@pytest.mark.parametrize("name,maker,start,chains,steps,inv_t0,window,types", ROUTE_CASES,
                          ids=[c[0] for c in ROUTE_CASES])
 def test_route_local_sa_matches_c_restatement(ctx, coracle, name, maker, start, chains, steps,
-                                              inv_t0, window):
+                                              inv_t0, window, types):
     """sa_route_kernel (windowed moves priced route-locally) against the C
     restatement's full re-evaluation, and against sa_kernel on the device."""
     inst = maker()
     load(ctx, inst)
-    S = inst.K - 1
-    if start == "greedy":
+    S = inst.K - 1 if start != "pack_few" else inst.K - 4
+    if start != "random":
         P0 = synth.random_perms(chains, inst.n, seed=9, dtype=np.uint16)
-        P = np.array([spec.insert_separators(p, S, inst.demand, inst.capacities) for p in P0])
+        f = spec.insert_separators if start == "greedy" else spec.pack_separators
+        P = np.array([f(p, S, inst.demand, inst.capacities) for p in P0])
         torch = torch_()
-        dev = ctx.insert_separators(torch.from_numpy(P0.astype(np.int16)).to(ctx.dev), S)
+        g = ctx.insert_separators if start == "greedy" else ctx.pack_separators
+        dev = g(torch.from_numpy(P0.astype(np.int16)).to(ctx.dev), S)
         assert dev.cpu().numpy().tolist() == P.tolist()
     else:
         P = sep_tours(chains, inst.n, S, seed=9, dtype=np.uint16)
     P = P.astype(np.int16)
-    got = _run_sa(ctx, P, steps, inv_t0, 1 / 0.99, 21, 7, window)
+    got = _run_sa(ctx, P, steps, inv_t0, 1 / 0.99, 21, 7, window, types)
     ccur, cbest = P.view(np.uint16).copy(), P.view(np.uint16).copy()
     cbk = np.full(chains, 2**64 - 1, dtype=np.uint64)
     cck = coracle.sa_run(inst.durations, ccur, cbest, cbk, steps, inv_t0, 1 / 0.99, 21, 7,
-                         inst.demand, inst.capacities, inst.start_times, window=window)
+                         inst.demand, inst.capacities, inst.start_times, window=window,
+                         window_types=types)
     assert (got[0].view(np.uint16) == ccur).all()
     assert got[1] == [int(x) for x in cck] and got[3] == [int(x) for x in cbk]
     assert (got[2].view(np.uint16) == cbest).all()
     ctx.set_sa_route(2)
     try:
-        full = _run_sa(ctx, P, steps, inv_t0, 1 / 0.99, 21, 7, window)
+        full = _run_sa(ctx, P, steps, inv_t0, 1 / 0.99, 21, 7, window, types)
     finally:
         ctx.set_sa_route(0)
     assert (full[0] == got[0]).all() and full[1] == got[1] and full[3] == got[3]
@@ -220,3 +232,40 @@ def test_route_local_sa_small_matches_python_oracle(ctx):
                         1 / 0.98, window=3)
     assert got[0].tolist() == ref[0] and got[1] == ref[1]
     assert got[2].tolist() == ref[2] and got[3] == ref[3]
+
+
+def test_route_local_sa_two_zone_small_matches_python_oracle(ctx):
+    """Windowed 2-opt with swap / relocate anywhere (A12), separators moved
+    across routes, against the Python replay."""
+    inst = synth.cvrp(40, 6, seed=12, slack=1.1)
+    load(ctx, inst)
+    P = sep_tours(3, inst.n, 5, seed=3, dtype=np.uint16).astype(np.int16)
+    got = _run_sa(ctx, P, 25, 1 / 60.0, 1 / 0.98, 5, 3, 4, 2)
+    sc = search.Scorer(inst.durations, inst.demand, inst.capacities, inst.start_times)
+    ref = search.sa_run(sc, P.tolist(), P.tolist(), [2**64 - 1] * 3, 5, 3, 25, 1 / 60.0,
+                        1 / 0.98, window=4, window_types=2)
+    assert got[0].tolist() == ref[0] and got[1] == ref[1]
+    assert got[2].tolist() == ref[2] and got[3] == ref[3]
+
+
+def test_pack_separators_matches_spec(ctx):
+    """First-fit start tours (vrpms_pack_separators) == oracle/spec.py, and
+    they serve every customer on the cfg-4 fleet."""
+    torch = torch_()
+    x = synth.x_style(1000, seed=3)
+    load(ctx, x)
+    P0 = synth.random_perms(64, x.n, seed=5, dtype=np.uint16)
+    dev = ctx.pack_separators(torch.from_numpy(P0.astype(np.int16)).to(ctx.dev), x.K - 1)
+    got = dev.cpu().numpy().view(np.uint16)
+    for r in (0, 31, 63):
+        assert got[r].tolist() == spec.pack_separators(P0[r], x.K - 1, x.demand, x.capacities)
+    keys, sums, maxs, unv = ctx.eval(dev, n=x.n + x.K - 1, with_parts=True)
+    assert int(unv.max()) == 0
+    het = synth.cvrp(50, 6, seed=2, slack=1.05)
+    het.capacities = np.array([40, 90, 60, 70, 55, 80])
+    load(ctx, het)
+    P0 = synth.random_perms(17, het.n, seed=1, dtype=np.uint16)
+    for S in (2, 5, 9):
+        dev = ctx.pack_separators(torch.from_numpy(P0.astype(np.int16)).to(ctx.dev), S)
+        want = [spec.pack_separators(p, S, het.demand, het.capacities) for p in P0]
+        assert dev.cpu().numpy().tolist() == want

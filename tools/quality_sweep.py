@@ -27,6 +27,12 @@ def main():
     ap.add_argument("--T", type=float, nargs="+", default=[1.0, 10.0, 60.0])
     ap.add_argument("--seeds", type=int, nargs="+", default=[0, 1, 2, 3, 4])
     ap.add_argument("--chains", type=int, default=4096)
+    ap.add_argument("--types", type=int, default=None,
+                    help="A12 window move types (bit 0 swap, 1 2-opt, 2 relocate; "
+                         "default 2 = windowed 2-opt only when windowed)")
+    ap.add_argument("--start", default=None, choices=["random", "greedy", "pack"],
+                    help="separator placement of the start tours (default: random for "
+                         "cvrp100, pack otherwise)")
     ap.add_argument("--window", type=int, default=None,
                     help="A11 move window (default: 0 for cvrp100, 32 otherwise)")
     ap.add_argument("--instance", default="cvrp100", choices=["cvrp100", "cvrp200", "x1000"],
@@ -57,7 +63,10 @@ def main():
                 0 if args.instance == "cvrp100" else 32)
             q = bench.quality(ctx, inst, T, 1, 0, None, with_cpu=True, chains=args.chains,
                               label=f"{args.instance} seed {seed}", n_sep=args.sep,
-                              window=window, greedy_start=window > 0)
+                              window=window,
+                              window_types=args.types if args.types is not None else 2,
+                              start=args.start or ("random" if args.instance == "cvrp100"
+                                                   else "pack"))
             q["seed"] = seed
             cells.append(q)
             print(json.dumps({"seed": seed, "T_s": T, "gpu": q["gpu"]["duration_sum"],
@@ -77,7 +86,8 @@ def main():
                                      "on durationSum, negative = GPU better",
                            "workload": f"{args.instance} (vrpms_amd.synth), SA on both sides",
                            "separators": cells[0]["separators"],
-                           "window": cells[0]["window"],
+                           "window": cells[0]["window"], "window_types": cells[0]["window_types"],
+                           "start": cells[0]["start"],
                            "cpu_cores": cells[0]["cpu"]["cores"],
                            "summary": summary, "cells": cells}, f, indent=1)
     print(json.dumps({"summary": summary}), flush=True)

@@ -4,8 +4,8 @@
   cfg 5: tsp_batch_sa_kernel, 10,000 TSP-50 requests x 1000 SA steps
   cfg 2: sa_packed_kernel, 4096 SA chains on CVRP-100 K = 8, 400-step epochs
   cfg 2: ga_fused_kernel, 256 islands x 256, 20 generations per call
-  cfg 4: sa_route_kernel, 1024 windowed SA chains on X-1000 with K - 1
-         separators (greedy start), 100-step epochs
+  cfg 4: sa_route_kernel, 1024 SA chains on X-1000 with K - 1 separators
+         (first-fit start, windowed 2-opt), 100-step epochs
 usage: search_run.py [reps]"""
 import os
 import sys
@@ -39,7 +39,7 @@ torch.cuda.synchronize()
 x = synth.x_style(1000, seed=0)
 ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
 rx = runners.SARunner(ctx, x.n, chains=1024, total_steps=100 * reps, durations=x.durations,
-                      n_sep=x.K - 1, window=32, greedy_start=True)
+                      n_sep=x.K - 1, window=32, window_types=2, start="pack")
 for _ in range(reps):
     rx.epoch(100)
 torch.cuda.synchronize()

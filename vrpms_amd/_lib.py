@@ -47,7 +47,7 @@ _u64 = _c.c_uint64
 class SaParams(ctypes.Structure):
     _fields_ = [("chains", _i32), ("steps", _i32), ("inv_t0", ctypes.c_float),
                 ("inv_alpha", ctypes.c_float), ("seed", _u64), ("step0", _u64),
-                ("window", _i32)]
+                ("window", _i32), ("window_types", _c.c_uint32)]
 
 
 class GaParams(ctypes.Structure):
@@ -93,6 +93,7 @@ SIGNATURES = {
     "vrpms_random_tours": (_c.c_int, [_vp, _i64, _i32, _i32, _i64, _i32, _u64, _c.c_uint32, _vp,
                                       _vp]),
     "vrpms_insert_separators": (_c.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp]),
+    "vrpms_pack_separators": (_c.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp]),
     "vrpms_pool_elites": (_c.c_int, [_vp, _c.POINTER(Pool), _i32, _vp, _vp, _vp]),
     "vrpms_pool_inject": (_c.c_int, [_vp, _c.POINTER(Pool), _i32, _vp, _vp, _i32, _vp]),
     "vrpms_island_msg_bytes": (_i64, [_i32, _i32]),

@@ -222,12 +222,13 @@ class Context:
 
     # -- search kernels (state lives in caller-owned device tensors) ----------
     def sa_run(self, cur, cur_key, best, best_key, steps: int, inv_t0: float, inv_alpha: float,
-               seed: int, step0: int, window: int = 0):
+               seed: int, step0: int, window: int = 0, window_types: int = 0):
         """Advance every chain (rows of the int16 [chains][n] tensor ``cur``);
-        window > 0 samples A11 windowed moves."""
+        window > 0 samples A11 windowed moves of the A12 types
+        ``window_types`` (bit t for move type t, 0 = all)."""
         chains, n = cur.shape
         p = _lib.SaParams(chains, int(steps), float(inv_t0), float(inv_alpha),
-                          int(seed) & (2**64 - 1), int(step0), int(window))
+                          int(seed) & (2**64 - 1), int(step0), int(window), int(window_types))
         check(self.lib.vrpms_sa_run(self._ctx, ctypes.byref(p), cur.data_ptr(),
                                     cur_key.data_ptr(), best.data_ptr(), best_key.data_ptr(), n,
                                     self.stream()))
@@ -316,6 +317,17 @@ class Context:
         out = torch.empty((count, n + int(n_sep)), dtype=torch.int16, device=self.dev)
         check(self.lib.vrpms_insert_separators(self._ctx, tours.contiguous().data_ptr(), count, n,
                                                int(n_sep), out.data_ptr(), self.stream()))
+        return out
+
+    def pack_separators(self, tours, n_sep: int):
+        """int16 [count][n] customer tours -> [count][n + n_sep]: first-fit
+        routes in input order, one separator between consecutive routes
+        (vrpms_pack_separators)."""
+        torch = _torch()
+        count, n = tours.shape
+        out = torch.empty((count, n + int(n_sep)), dtype=torch.int16, device=self.dev)
+        check(self.lib.vrpms_pack_separators(self._ctx, tours.contiguous().data_ptr(), count, n,
+                                             int(n_sep), out.data_ptr(), self.stream()))
         return out
 
     @staticmethod

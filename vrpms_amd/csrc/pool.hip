@@ -104,6 +104,61 @@ __global__ void insert_separators_kernel(const uint16_t* __restrict__ in, int64_
   while (w < n + nsep) o[w++] = 0;
 }
 
+// First-fit start (oracle/spec.py pack_separators): the customers of row r
+// of `in`, in order, each join the first of B = n_sep + 1 routes with room
+// (route b holds cap[min(b, K-1)]; none: the last route); out = route 0, 0,
+// route 1, 0, ..., each route in input order.  One wavefront per row: the
+// 64 lanes test 64 routes per ballot; lane 0 books the load and, at the end,
+// places the customers.  LDS per wave: load [B] i32, start [B] i32, bin [n] u16.
+__global__ __launch_bounds__(256) void pack_separators_kernel(
+    const uint16_t* __restrict__ in, int64_t count, int n, int nsep,
+    const int32_t* __restrict__ dem, const int32_t* __restrict__ cap, int K,
+    uint32_t wave_bytes, uint16_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int wave = threadIdx.x >> 6, lane = (int)(threadIdx.x & 63u);
+  const int64_t r = (int64_t)blockIdx.x * 4 + wave;
+  if (r >= count) return;  // no block-wide barrier below
+  const int B = nsep + 1;
+  int32_t* load = reinterpret_cast<int32_t*>(smem + wave * wave_bytes);
+  int32_t* start = load + B;
+  uint16_t* bin = reinterpret_cast<uint16_t*>(start + B);
+  const uint16_t* t = in + r * n;
+  uint16_t* o = out + r * (int64_t)(n + nsep);
+  for (int b = lane; b < B; b += 64) load[b] = 0;
+  wave_sync();
+  for (int q = 0; q < n; ++q) {
+    const int d = dem[t[q]];
+    int first = B - 1;
+    for (int base = 0; base < B; base += 64) {
+      const int b = base + lane;
+      const bool fits = b < B && load[b] + d <= cap[min(b, K - 1)];
+      const uint64_t ball = __ballot(fits);
+      if (ball) {
+        first = base + (int)__builtin_ctzll(ball);
+        break;
+      }
+    }
+    if (lane == 0) {
+      load[first] += d;
+      bin[q] = (uint16_t)first;
+    }
+    wave_sync();
+  }
+  if (lane == 0) {
+    // customers per route -> first position of each route (separators between)
+    for (int b = 0; b < B; ++b) start[b] = 0;
+    for (int q = 0; q < n; ++q) ++start[bin[q]];
+    int pos = 0;
+    for (int b = 0; b < B; ++b) {
+      const int c = start[b];
+      start[b] = pos;
+      pos += c;
+      if (b + 1 < B) o[pos++] = 0;
+    }
+    for (int q = 0; q < n; ++q) o[start[bin[q]]++] = t[q];
+  }
+}
+
 constexpr int kTopChunk = 2048;
 
 // Per chunk of kTopChunk entries: the E smallest (key', index) pairs, where
@@ -411,6 +466,29 @@ int vrpms_insert_separators(vrpms_ctx* ctx, const uint16_t* d_in, int64_t count,
   const Instance& in = ctx->inst;
   insert_separators_kernel<<<(unsigned)((count + 255) / 256), 256, 0, (hipStream_t)stream>>>(
       d_in, count, n, n_sep, in.dem, in.cap, in.K, d_out);
+  VRPMS_HIP(hipGetLastError());
+  return VRPMS_OK;
+}
+
+int vrpms_pack_separators(vrpms_ctx* ctx, const uint16_t* d_in, int64_t count, int32_t n,
+                          int32_t n_sep, uint16_t* d_out, void* stream) {
+  if (!ctx) return fail(VRPMS_EINVAL, "vrpms_pack_separators: ctx is NULL");
+  if (!ctx->has_instance || ctx->inst.problem != VRPMS_CVRP)
+    return fail(VRPMS_ESTATE, "vrpms_pack_separators: needs a CVRP instance");
+  if (count < 0 || n < 0 || n > ctx->inst.N - 1 || n_sep < 0 || n_sep > 4095)
+    return fail(VRPMS_EINVAL, "vrpms_pack_separators: need count >= 0, 0 <= n <= N-1, 0 <= n_sep < 4096");
+  if (count == 0 || n + n_sep == 0) return VRPMS_OK;
+  if (!d_in || !d_out) return fail(VRPMS_EINVAL, "vrpms_pack_separators: NULL buffer");
+  VRPMS_HIP(hipSetDevice(ctx->device));
+  const Instance& in = ctx->inst;
+  const uint32_t wave_bytes = ((uint32_t)(n_sep + 1) * 8u + (uint32_t)n * 2u + 15u) & ~15u;
+  const size_t lds = (size_t)4 * wave_bytes;
+  if (lds > ctx->max_lds) return fail(VRPMS_EINVAL, "vrpms_pack_separators: tours too long for LDS");
+  if (lds > 65536)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pack_separators_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  pack_separators_kernel<<<(unsigned)((count + 3) / 4), 256, lds, (hipStream_t)stream>>>(
+      d_in, count, n, n_sep, in.dem, in.cap, in.K, wave_bytes, d_out);
   VRPMS_HIP(hipGetLastError());
   return VRPMS_OK;
 }

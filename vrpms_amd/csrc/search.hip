@@ -115,6 +115,7 @@ VRPMS_DEV StagedInst<MatT, HM> stage_inst(const SearchInst& si, unsigned char* s
 struct SaArgs {
   SearchInst si;
   int chains, n, steps, window;
+  uint32_t window_types;
   float inv_t0, inv_alpha;
   uint32_t seed_lo, seed_hi;
   uint64_t step0;
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(256) void sa_kernel(SaArgs a) {
     const uint64_t step = a.step0 + (uint64_t)s;
     const u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)chain,
                            (uint32_t)lane, a.seed_lo, a.seed_hi);
-    const Move m = decode_move_window(r.x, r.y, r.z, n, a.window);
+    const Move m = decode_move_window(r.x, r.y, r.z, n, a.window, a.window_types);
     uint64_t k;
     int nd = 0;
     if constexpr (kDelta) {
@@ -244,7 +245,21 @@ struct RouteStats {
   uint32_t *rc, *ds, *dm, *ne;   // per segment: routes, duration sum / max, has a customer
   uint32_t *rcp, *dsp, *pmx, *smx, *lnea;  // prefix sums, prefix / suffix max, any customer >= s
   int32_t* xb;      // closures before the last customer in segments < s (-1: none)
+  int32_t* lnb;     // last segment < s holding a customer (-1: none)
+  uint32_t* sp;     // sparse table of dm: level l >= 1 at sp + (l - 1) * segs (level 0 = dm)
 };
+
+// route stats per chain: u32 arrays (10 named + the sparse-table levels
+// above 0), levels l with 2^l <= segs
+__host__ __device__ inline int route_levels(int segs) {
+  int lv = 1;
+  while ((2 << (lv - 1)) <= segs) ++lv;
+  return lv;
+}
+__host__ __device__ inline uint32_t route_wave_bytes(int npad, int segs) {
+  return 4u * (uint32_t)npad * 2u + (((uint32_t)segs * 2u + 3u) & ~3u) +
+         (uint32_t)(10 + route_levels(segs)) * (uint32_t)segs * 4u;
+}
 
 // Wave-wide inclusive scan (add or max) of v over lanes (shuffle steps).
 template <bool MAX>
@@ -267,8 +282,9 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
   const int chain = blockIdx.x * 4 + wave;
   const int K = a.si.K;
   const int SEGS = K + 2;
+  const int LV = route_levels(SEGS);
   const uint32_t npad = ((uint32_t)n + 7u) & ~7u;
-  const uint32_t wbytes = 4u * npad * 2u + (((uint32_t)SEGS * 2u + 3u) & ~3u) + 11u * SEGS * 4u;
+  const uint32_t wbytes = route_wave_bytes((int)npad, SEGS);
   unsigned char* wb = smem + inst_lds_bytes(a.si) + wave * ((wbytes + 15u) & ~15u);
   if (chain >= a.chains) return;  // no block-wide barrier after this point
   uint16_t* A = reinterpret_cast<uint16_t*>(wb);
@@ -288,6 +304,9 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
   R.smx = u + 7 * SEGS;
   R.lnea = u + 8 * SEGS;
   R.xb = reinterpret_cast<int32_t*>(u + 9 * SEGS);
+  R.lnb = reinterpret_cast<int32_t*>(u + 10 * SEGS);
+  R.sp = u + 11 * SEGS;
+  auto SP = [&](int l) { return l ? R.sp + (l - 1) * SEGS : R.dm; };
   const uint16_t* gcur = a.cur + (int64_t)chain * n;
   for (int q = lane; q < n; q += 64) A[q] = gcur[q];
   wave_sync();
@@ -408,9 +427,24 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
     wave_sync();
     for (int s = lane; s <= S + 1; s += 64) {
       const int lnb = R.xb[s];
+      R.lnb[s] = lnb;
       R.xb[s] = lnb >= 0 ? (int32_t)(R.rcp[lnb + 1] - 1u) : -1;
     }
+    // sparse table of dm for range maxima between two zones
+    for (int l = 1; l < LV; ++l) {
+      const int w = 1 << (l - 1);
+      const uint32_t* src = SP(l - 1);
+      uint32_t* dst = SP(l);
+      for (int s = lane; s + 2 * w <= S + 1; s += 64) dst[s] = max(src[s], src[s + w]);
+      wave_sync();
+    }
     wave_sync();
+  };
+  auto range_max = [&](int lo_s, int hi_s) -> uint32_t {  // max dm over segments lo_s..hi_s
+    if (lo_s > hi_s) return 0u;
+    const int l = 31 - __builtin_clz((uint32_t)(hi_s - lo_s + 1));
+    const uint32_t* t = SP(l);
+    return max(t[lo_s], t[hi_s - (1 << l) + 1]);
   };
 
   // the current tour
@@ -437,7 +471,7 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
     const uint64_t step = a.step0 + (uint64_t)st;
     const u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)chain,
                            (uint32_t)lane, a.seed_lo, a.seed_hi);
-    const Move m = decode_move_window(r.x, r.y, r.z, n, a.window);
+    const Move m = decode_move_window(r.x, r.y, r.z, n, a.window, a.window_types);
     auto moved = [&](int q) { return (uint32_t)A[moved_index(q, m)]; };
     uint64_t k;
     // an unserved customer cannot be accepted from a tour serving everyone
@@ -446,22 +480,48 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
     int s_lo = 0, s_hi = 0;
     bool full = !route_ok;
     if (route_ok) {
+      // the segments a move changes: the one holding each end, plus the next
+      // one when that end is a separator (it merges with or splits off its
+      // neighbour).  Swap / relocate leave the segments between the two ends
+      // intact (a relocate shifts them by one position), so when those groups
+      // do not touch they are priced as two zones; a 2-opt reverses the whole
+      // span, priced as one zone.
       const int lo = min(m.i, m.j), hi = max(m.i, m.j);
-      // the span runs from the separator before lo to the one after hi: a
-      // separator AT hi ends segment segid[hi] but moves with the move, so
-      // the span then reaches through the next segment
-      s_lo = R.segid[lo];
-      s_hi = R.segid[hi] + (A[hi] == 0 ? 1 : 0);
-      const int from = s_lo ? R.send[s_lo - 1] + 1 : 0, to = R.send[s_hi];
-      const SegCost sc = seg_walk(from, to, moved);
-      const uint32_t span_old = R.rcp[s_hi + 1] - R.rcp[s_lo];
+      const int a1 = R.segid[lo], b1 = a1 + (A[lo] == 0 ? 1 : 0);
+      const int a2 = R.segid[hi], b2 = a2 + (A[hi] == 0 ? 1 : 0);
+      const bool two = m.typ != kMove2Opt && b1 < a2;
+      const int from1 = a1 ? R.send[a1 - 1] + 1 : 0;
+      s_lo = a1;
+      s_hi = b2;
+      SegCost z1, z2{0u, 0u, 0u, -1};
+      uint32_t old1, old2 = 0u;  // routes of the old segments each zone replaces
+      int d1, d2 = 0;
+      uint32_t dsum, dmax;
+      if (two) {
+        // tokens between the zones move by dl positions (relocate i < j: -1)
+        const int dl = m.typ == kMoveSwap ? 0 : (m.i < m.j ? -1 : 1);
+        z1 = seg_walk(from1, (int)R.send[b1] + dl, moved);
+        z2 = seg_walk((int)R.send[a2 - 1] + 1 + dl, (int)R.send[b2], moved);
+        old1 = R.rcp[b1 + 1] - R.rcp[a1];
+        old2 = R.rcp[b2 + 1] - R.rcp[a2];
+        dsum = R.dsp[S + 1] - (R.dsp[b1 + 1] - R.dsp[a1]) - (R.dsp[b2 + 1] - R.dsp[a2]) + z1.ds +
+               z2.ds;
+        dmax = max(max(max(R.pmx[a1], R.smx[b2 + 1]), max(z1.dm, z2.dm)), range_max(b1 + 1, a2 - 1));
+        d2 = (int)z2.rc - (int)old2;
+      } else {
+        z1 = seg_walk(from1, (int)R.send[b2], moved);
+        old1 = R.rcp[b2 + 1] - R.rcp[a1];
+        dsum = R.dsp[S + 1] - (R.dsp[b2 + 1] - R.dsp[a1]) + z1.ds;
+        dmax = max(max(R.pmx[a1], R.smx[b2 + 1]), z1.dm);
+      }
+      d1 = (int)z1.rc - (int)old1;
       int X;  // closures before the moved tour's last customer
-      if (R.lnea[s_hi + 1]) X = R.xb[S + 1] + (int)sc.rc - (int)span_old;
-      else if (sc.xs >= 0) X = (int)R.rcp[s_lo] + sc.xs;
-      else X = R.xb[s_lo];
+      if (R.lnea[b2 + 1]) X = R.xb[S + 1] + d1 + d2;
+      else if (z2.xs >= 0) X = (int)R.rcp[a2] + d1 + z2.xs;
+      else if (two && R.lnb[a2] > b1) X = R.xb[a2] + d1;
+      else if (z1.xs >= 0) X = (int)R.rcp[a1] + z1.xs;
+      else X = R.xb[a1];
       if (X < K) {
-        const uint32_t dsum = R.dsp[S + 1] - (R.dsp[s_hi + 1] - R.dsp[s_lo]) + sc.ds;
-        const uint32_t dmax = max(max(R.pmx[s_lo], R.smx[s_hi + 1]), sc.dm);
         k = cvrp_key(0, dsum, dmax, I.sp.objective);
       } else if (shortcut) {
         k = ~0ull;
@@ -532,6 +592,7 @@ constexpr int kSaPackedWaves = 16;
 struct SaPackedArgs {
   FastSplit f;
   int chains, n, steps, window;
+  uint32_t window_types;
   float inv_t0, inv_alpha;
   uint32_t seed_lo, seed_hi;
   uint64_t step0;
@@ -638,7 +699,7 @@ __global__ __launch_bounds__(1024) void sa_packed_kernel(SaPackedArgs a) {
     const uint64_t step = a.step0 + (uint64_t)s;
     const u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)chain,
                            (uint32_t)lane, a.seed_lo, a.seed_hi);
-    const Move m = decode_move_window(r.x, r.y, r.z, n, a.window);
+    const Move m = decode_move_window(r.x, r.y, r.z, n, a.window, a.window_types);
     uint64_t k = eval_mapped(a.f, smem, N8, A, n, move_map(m));
     int bl;
     k = wave_argmin_lane(k, bl);  // wave-uniform (key, lane) minimum
@@ -1394,6 +1455,8 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
     return fail(VRPMS_EINVAL, "vrpms_sa_run: need chains > 0, steps >= 0, 0 <= n <= N-1 (+K for CVRP)");
   if (!d_cur || !d_cur_key || !d_best || !d_best_key)
     return fail(VRPMS_EINVAL, "vrpms_sa_run: NULL state buffer");
+  if (p->window_types > 7u) return fail(VRPMS_EINVAL, "vrpms_sa_run: window_types is a 3-bit mask");
+  const uint32_t wtypes = p->window_types ? p->window_types : 7u;
   VRPMS_HIP(hipSetDevice(ctx->device));
   FastSplit f;
   if (ctx->inst.H == 1 && fast_split_params(ctx, n, &f)) {
@@ -1401,7 +1464,7 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
     const size_t lds = (((size_t)f.N * f.N * 8 + 15) & ~(size_t)15) +
                        (size_t)kSaPackedWaves * 3 * tb;
     if (lds <= ctx->max_lds) {
-      SaPackedArgs pa{f, p->chains, n, p->steps, p->window, p->inv_t0, p->inv_alpha, (uint32_t)p->seed,
+      SaPackedArgs pa{f, p->chains, n, p->steps, p->window, wtypes, p->inv_t0, p->inv_alpha, (uint32_t)p->seed,
                       (uint32_t)(p->seed >> 32), p->step0, tb, d_cur, d_cur_key, d_best,
                       d_best_key};
       if (lds > 65536)
@@ -1413,7 +1476,7 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
       return VRPMS_OK;
     }
   }
-  SaArgs a{search_inst(ctx), p->chains, n, p->steps, p->window, p->inv_t0, p->inv_alpha,
+  SaArgs a{search_inst(ctx), p->chains, n, p->steps, p->window, wtypes, p->inv_t0, p->inv_alpha,
            (uint32_t)p->seed, (uint32_t)(p->seed >> 32), p->step0, d_cur, d_cur_key, d_best,
            d_best_key};
   // route-local pricing (sa_route_kernel) for windowed SA on a fleet of
@@ -1423,8 +1486,7 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
       in.min_start == in.max_start && in.max_dem <= in.cap0 && ctx->opt_sa_route != 2) {
     const size_t npad = ((size_t)n + 7) & ~(size_t)7;
     const size_t segs = (size_t)in.K + 2;
-    const size_t wbytes = (4 * npad * 2 + ((segs * 2 + 3) & ~(size_t)3) + 11 * segs * 4 + 15) &
-                          ~(size_t)15;
+    const size_t wbytes = ((size_t)route_wave_bytes((int)npad, (int)segs) + 15) & ~(size_t)15;
     size_t lds = inst_lds_bytes_host(a.si) + 4 * wbytes;
     if (lds > ctx->max_lds) {
       a.si.mat_lds = 0;

@@ -149,8 +149,11 @@ VRPMS_DEV Move decode_move(uint32_t r0, uint32_t r1, uint32_t r2, int n) {
 
 // A11 (oracle/spec.py decode_move_window): the second position within
 // `window` of the first; window <= 0 or 2 window + 1 >= n: decode_move.
-VRPMS_DEV Move decode_move_window(uint32_t r0, uint32_t r1, uint32_t r2, int n, int window) {
-  if (window <= 0 || 2 * window + 1 >= n) return decode_move(r0, r1, r2, n);
+// A12: only for the move types whose bit is set in `types` (7 = all).
+VRPMS_DEV Move decode_move_window(uint32_t r0, uint32_t r1, uint32_t r2, int n, int window,
+                                  uint32_t types) {
+  if (window <= 0 || 2 * window + 1 >= n || !((types >> (r0 % 3u)) & 1u))
+    return decode_move(r0, r1, r2, n);
   Move m;
   m.typ = r0 % 3u;
   m.i = (int)(r1 % (uint32_t)n);

@@ -70,17 +70,19 @@ class SARunner(_Base):
     t0 to t_end over `total_steps` steps.  `n_sep` A10 route separators
     (CVRP) ride in every tour, so the moves also place route boundaries;
     tours then hold n + n_sep tokens (self.n).  `window` > 0 samples A11
-    windowed moves (priced route-locally on an exchangeable fleet);
-    `greedy_start` puts the separators where the greedy split closes routes
-    (a feasible start) instead of at random."""
+    windowed moves of the A12 types `window_types` (0 = all; priced
+    route-locally on an exchangeable fleet).  `start` places the separators:
+    "random" (Philox tokens), "greedy" (where the greedy split of a random
+    order closes routes) or "pack" (first-fit routes of a random order, a
+    feasible start when the fleet has little spare capacity)."""
 
     def __init__(self, ctx: Context, n: int, chains: int = 1024, seed: int = 0,
                  total_steps: int = 2000, steps_per_epoch: int = 250, t0: float | None = None,
                  t_end: float | None = None, durations=None, n_sep: int = 0, window: int = 0,
-                 greedy_start: bool = False):
+                 window_types: int = 0, start: str = "random"):
         torch = _torch()
         self.ctx, self.n, self.seed = ctx, n + n_sep, seed
-        self.n_sep, self.window = n_sep, window
+        self.n_sep, self.window, self.window_types = n_sep, window, window_types
         self.chains = chains
         edge = typical_edge(durations) if durations is not None else 100.0
         t0 = t0 if t0 is not None else 0.5 * edge
@@ -89,8 +91,10 @@ class SARunner(_Base):
         self.inv_t = np.float32(1.0 / t0)
         self.steps_per_epoch = steps_per_epoch
         self.step = 0
-        if n_sep and greedy_start:   # separators where the greedy split closes routes
+        if n_sep and start == "greedy":   # separators where the greedy split closes routes
             self.cur = ctx.insert_separators(ctx.random_tours(chains, n, seed), n_sep)
+        elif n_sep and start == "pack":   # first-fit routes
+            self.cur = ctx.pack_separators(ctx.random_tours(chains, n, seed), n_sep)
         else:
             self.cur = ctx.random_tours(chains, n, seed, n_sep=n_sep)
         self.best_t = self.cur.clone()
@@ -100,7 +104,8 @@ class SARunner(_Base):
     def epoch(self, steps: int | None = None):
         s = self.steps_per_epoch if steps is None else steps
         self.ctx.sa_run(self.cur, self.cur_key, self.best_t, self.best_key, s, float(self.inv_t),
-                        float(self.inv_alpha), self.seed, self.step, window=self.window)
+                        float(self.inv_alpha), self.seed, self.step, window=self.window,
+                        window_types=self.window_types)
         for _ in range(s):      # same float32 recurrence as the kernel
             self.inv_t = np.float32(self.inv_t * self.inv_alpha)
         self.step += s

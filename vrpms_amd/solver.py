@@ -171,12 +171,13 @@ def search(ctx: Context, ci: CompactInstance, algorithm: str, seed: int = 0,
         # VRP: K - 1 route separators (A10) let the moves place route
         # boundaries instead of leaving them to the greedy split alone
         n_sep = int(knobs.get("separators", len(ci.capacities) - 1 if ci.problem == CVRP else 0))
-        # large tours: A11 windowed moves (priced route-locally on an
-        # exchangeable fleet) from separators at the greedy route boundaries
+        # large tours: A11/A12 windowed 2-opt, swap / relocate anywhere
+        # (priced route-locally on an exchangeable fleet), from first-fit routes
         window = int(knobs.get("window", SA_WINDOW if n > SA_WINDOW_MIN_N else 0))
         r = runners.SARunner(ctx, n, chains=int(knobs.get("chains", 1024)), seed=seed,
                              total_steps=steps, durations=ci.durations, n_sep=n_sep,
-                             window=window, greedy_start=window > 0 and n_sep > 0)
+                             window=window, window_types=int(knobs.get("window_types", 2)),
+                             start="pack" if window > 0 and n_sep > 0 else "random")
         epochs = max(1, steps // r.steps_per_epoch)
     elif algorithm == "ga":
         pop = int(knobs.get("random_permutation_count") or knobs.get("pop", 256))
