@@ -1,0 +1,49 @@
+"""The route-local pricing rules of sa_route_kernel (oracle/route_model.py,
+a step-for-step Python model of the kernel's walk and composition) against
+full evaluation (oracle/spec.py eval_cvrp) on random moves, including
+tours that drifted into long / empty segments and infeasible ones."""
+import numpy as np
+import pytest
+
+from oracle import route_model as rmod
+from oracle import spec
+from vrpms_amd import synth
+
+
+@pytest.mark.parametrize("nn,slack,obj,sep", [(30, 1.02, 0, "K-1"), (60, 1.3, 1, "K-2"),
+                                              (80, 1.25, 0, "0"), (40, 1.5, 1, "K+2")])
+def test_route_pricing_matches_full_evaluation(nn, slack, obj, sep):
+    rng = np.random.default_rng(nn)
+    checked = 0
+    for trial in range(4):
+        inst = synth.cvrp(nn, max(3, nn // 10), seed=trial + nn, slack=slack)
+        K, cap = len(inst.capacities), int(inst.capacities[0])
+        dem = [int(x) for x in inst.demand]
+        D = inst.durations[0]
+        S = max(0, {"K-1": K - 1, "K-2": K - 2, "0": 0, "K+2": K + 2}[sep])
+        A = [int(x) for x in spec.pack_separators(rng.permutation(np.arange(1, nn + 1)), S, dem,
+                                                  inst.capacities)]
+        for _ in range(120):
+            n = len(A)
+            typ, i = int(rng.integers(0, 3)), int(rng.integers(0, n))
+            if rng.random() < 0.5:
+                d = int(rng.integers(1, 5)) * (1 if rng.random() < .5 else -1)
+                j = i + d if 0 <= i + d < n else i - d
+            else:
+                j = int(rng.integers(0, n - 1))
+                j += j >= i
+            if typ != spec.MOVE_RELOCATE and i > j:
+                i, j = j, i
+            T = rmod.Tables(D, A, dem, cap, int(inst.start_times[0]))
+            got = rmod.price(T, (typ, i, j), K, obj)
+            mv = rmod._moved(A, (typ, i, j))
+            ref = spec.eval_cvrp(inst.durations, mv, inst.demand, inst.capacities,
+                                 inst.start_times, obj)
+            if ref["unvisited"] == 0:
+                assert got == ref["key"], (trial, typ, i, j)
+                checked += 1
+            else:
+                assert got is None
+            if ref["unvisited"] == 0 or rng.random() < 0.2:
+                A = mv
+    assert checked > 20

@@ -171,6 +171,11 @@ ROUTE_CASES = [
     # cfg 4 as the front-end runs it: first-fit routes (a feasible start), windowed 2-opt,
     # swap / relocate anywhere (two-zone pricing)
     ("x1000_pack_2opt", lambda: synth.x_style(1000, seed=2), "pack", 16, 60, 1 / 300.0, 32, 2),
+    # many accepted moves (hot): the route tables are updated around every accepted zone
+    ("x1000_pack_long_hot", lambda: synth.x_style(1000, seed=4), "pack", 8, 400, 1 / 2000.0, 32,
+     2),
+    ("x1000_pack_all_windowed", lambda: synth.x_style(1000, seed=5), "pack", 8, 150, 1 / 300.0,
+     24, 0),
     # cfg 3: hour-indexed TD-200 (one start time), random separators: an infeasible start,
     # so moves that leave customers unserved are re-evaluated in full
     ("td200_random", lambda: synth.td_cvrp(200, 16, seed=2), "random", 8, 30, 1 / 200.0, 16, 0),

@@ -26,7 +26,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--T", type=float, nargs="+", default=[1.0, 10.0, 60.0])
     ap.add_argument("--seeds", type=int, nargs="+", default=[0, 1, 2, 3, 4])
-    ap.add_argument("--chains", type=int, default=4096)
+    ap.add_argument("--chains", type=int, default=None,
+                    help="GPU chains (default 4096 for cvrp100; 2048 otherwise, the route-local "
+                         "kernel's resident count: 2 workgroups x 4 chains per CU)")
     ap.add_argument("--types", type=int, default=None,
                     help="A12 window move types (bit 0 swap, 1 2-opt, 2 relocate; "
                          "default 2 = windowed 2-opt only when windowed)")
@@ -61,7 +63,8 @@ def main():
         for T in args.T:
             window = args.window if args.window is not None else (
                 0 if args.instance == "cvrp100" else 32)
-            q = bench.quality(ctx, inst, T, 1, 0, None, with_cpu=True, chains=args.chains,
+            q = bench.quality(ctx, inst, T, 1, 0, None, with_cpu=True,
+                              chains=args.chains or (4096 if args.instance == "cvrp100" else 2048),
                               label=f"{args.instance} seed {seed}", n_sep=args.sep,
                               window=window,
                               window_types=args.types if args.types is not None else 2,

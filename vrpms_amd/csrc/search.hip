@@ -222,44 +222,67 @@ __global__ __launch_bounds__(256) void sa_kernel(SaArgs a) {
 }
 
 // ===========================================================================
-// Route-local SA (CVRP tours with A10 separators, exchangeable vehicles:
-// one capacity and one start time for the whole fleet, every demand fits an
+// Route-local SA (CVRP tours with A10 separators, exchangeable vehicles: one
+// capacity and one start time for the whole fleet, every demand fits an
 // empty vehicle).  Same chain, moves and acceptance as sa_kernel; what
-// changes is how a move is priced.  The separators cut the tour into
-// segments whose greedy split is independent of everything outside them,
-// so a move touching positions lo..hi changes only the segments holding lo
-// .. hi: a lane walks those (from the separator before lo to the one after
-// hi -- with A11 windowed moves a few routes instead of the whole tour) and
-// composes the key with per-segment totals of the current tour kept in LDS
-// (route count, duration sum and max, prefix / suffix scans of them).
-// Exact: a composed tour that keeps every customer served gets its exact
-// key; one that cannot (more closures before its last customer than
-// vehicles) is either re-evaluated in full or, when the current tour serves
-// everyone and the temperature makes accepting an unserved customer
-// impossible, given the largest key -- it can then neither win a feasible
-// argmin nor be accepted, so the trajectory equals full re-evaluation.
+// changes is how a move is priced.
+//
+// Every route of the greedy split starts from the same state (empty
+// vehicle at the depot at the common start time), whether a separator or a
+// customer that did not fit opened it.  So a move touching positions lo..hi
+// leaves the split before the route holding lo untouched; a lane walks the
+// moved tour from that route's start, and stops as soon as its walk is back
+// in step with the current tour: at a position where the current tour
+// starts a route and the walk is also at a route start (fresh, or the
+// token there does not fit).  From there on the two splits coincide.  Swap
+// and relocate leave the tokens between their two ends in order (a
+// relocate shifts them by one), so the walk re-synchronises between the
+// ends too and prices the second end as its own zone; a 2-opt reverses the
+// span and is walked through it.  The key is composed from the walked
+// zones and per-route totals of the current tour kept in LDS (prefix sums
+// of durations, prefix / suffix maxima, a sparse table for the maximum
+// between the zones, the last route holding a customer).
+//
+// Exact: a composed tour that serves every customer (fewer closures before
+// its last customer than vehicles) gets its exact key; one that cannot is
+// re-evaluated in full, or -- when the current tour serves everyone and
+// 2^28 * invT makes accepting an unserved customer impossible -- given the
+// largest key, so the trajectory equals full re-evaluation.  An accepted
+// move re-walks its zones once, recording their routes, and the per-route
+// tables are rebuilt around them.
 // ===========================================================================
-struct RouteStats {
-  uint16_t* segid;  // [npad] separators before position q
-  uint16_t* send;   // [segs] position of segment s's terminator (n for the last)
-  uint32_t *rc, *ds, *dm, *ne;   // per segment: routes, duration sum / max, has a customer
-  uint32_t *rcp, *dsp, *pmx, *smx, *lnea;  // prefix sums, prefix / suffix max, any customer >= s
-  int32_t* xb;      // closures before the last customer in segments < s (-1: none)
-  int32_t* lnb;     // last segment < s holding a customer (-1: none)
-  uint32_t* sp;     // sparse table of dm: level l >= 1 at sp + (l - 1) * segs (level 0 = dm)
-};
+constexpr int kRouteZoneMax = 64;  // routes one accepted zone pair may record
+constexpr int kBlk = 8;            // tokens a pricing walk reads (and fetches legs for) at once
 
-// route stats per chain: u32 arrays (10 named + the sparse-table levels
-// above 0), levels l with 2^l <= segs
-__host__ __device__ inline int route_levels(int segs) {
+__host__ __device__ inline int route_max(int K) { return 2 * K + 2; }  // routes stored
+__host__ __device__ inline int route_rm(int K) { return (route_max(K) + 1 + 7) & ~7; }
+__host__ __device__ inline int route_levels(int rm) {
   int lv = 1;
-  while ((2 << (lv - 1)) <= segs) ++lv;
+  while ((2 << (lv - 1)) <= rm) ++lv;
   return lv;
 }
-__host__ __device__ inline uint32_t route_wave_bytes(int npad, int segs) {
-  return 4u * (uint32_t)npad * 2u + (((uint32_t)segs * 2u + 3u) & ~3u) +
-         (uint32_t)(10 + route_levels(segs)) * (uint32_t)segs * 4u;
+__host__ __device__ inline int route_segs(int K) { return (K + 2 + 7) & ~7; }
+// per-chain LDS: u32 tables, then u16 arrays, then u8 arrays
+__host__ __device__ inline uint32_t route_wave_bytes(int npad, int K) {
+  const uint32_t rm = (uint32_t)route_rm(K), lv = (uint32_t)route_levels(route_rm(K));
+  const uint32_t u32s = (6u + (lv - 1u)) * rm + kRouteZoneMax;
+  const uint32_t u16s = 2u * (uint32_t)npad + rm + (uint32_t)route_segs(K) + kRouteZoneMax;
+  const uint32_t u8s = 2u * (uint32_t)npad + rm + kRouteZoneMax;
+  return 4u * u32s + 2u * u16s + u8s;
 }
+
+struct RouteTabs {
+  uint32_t *dur, *dsp, *pmx, *smx, *lnea;  // per route; prefix sum / max, suffix max, customers >= r
+  int32_t* lnb;      // last route < r holding a customer (-1: none)
+  uint32_t* sp;      // sparse table of dur, level l >= 1 at sp + (l - 1) * rm
+  uint32_t* zd;      // recorded zone routes: duration
+  uint16_t* rs;      // first position of route r (rs[R] = n)
+  uint16_t* send;    // separator positions (init only)
+  uint16_t* zs;      // recorded zone routes: first position
+  uint8_t *rid, *rid2;  // route of each position (current, scratch)
+  uint8_t* cus;      // route holds a customer
+  uint8_t* zc;       // recorded zone routes: holds a customer
+};
 
 // Wave-wide inclusive scan (add or max) of v over lanes (shuffle steps).
 template <bool MAX>
@@ -273,6 +296,13 @@ VRPMS_DEV uint32_t wave_scan_incl(uint32_t v) {
   return v;
 }
 
+#ifdef VRPMS_ROUTE_PROF
+// per-chain counters (A/B builds only: tools/route_prof.py): pricing and
+// accept ticks (wall_clock64, 100 MHz), steps, accepts, walked tokens (wave
+// max, lane sum), lanes re-evaluated in full, tokens re-walked on accepts
+__device__ unsigned long long g_route_prof[12 * 8192];
+#endif
+
 template <typename MatT, int HM>
 __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -281,170 +311,247 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
   const int wave = threadIdx.x >> 6, lane = lane_id();
   const int chain = blockIdx.x * 4 + wave;
   const int K = a.si.K;
-  const int SEGS = K + 2;
-  const int LV = route_levels(SEGS);
+  const int RMAX = route_max(K), RM = route_rm(K), LV = route_levels(RM);
+  const int SEGS = route_segs(K);
   const uint32_t npad = ((uint32_t)n + 7u) & ~7u;
-  const uint32_t wbytes = route_wave_bytes((int)npad, SEGS);
-  unsigned char* wb = smem + inst_lds_bytes(a.si) + wave * ((wbytes + 15u) & ~15u);
+  const uint32_t wbytes = (route_wave_bytes((int)npad, K) + 15u) & ~15u;
+  unsigned char* wb = smem + inst_lds_bytes(a.si) + wave * wbytes;
+  // static matrix: the depot legs out(c) = D(0, c) and ret(c) = D(c, 0) in
+  // LDS, so a pricing walk gathers one matrix entry per token from L2
+  MatT* legs = reinterpret_cast<MatT*>(smem + inst_lds_bytes(a.si) + 4 * wbytes);
+  if constexpr (HM == 1) {
+    const MatT* M = static_cast<const MatT*>(a.si.mat);
+    const uint32_t N = (uint32_t)a.si.N;
+    for (uint32_t c = threadIdx.x; c < N; c += blockDim.x) {
+      legs[c] = M[c];
+      legs[N + c] = M[(size_t)c * N];
+    }
+    __syncthreads();
+  }
   if (chain >= a.chains) return;  // no block-wide barrier after this point
-  uint16_t* A = reinterpret_cast<uint16_t*>(wb);
+  RouteTabs T;
+  {
+    uint32_t* u = reinterpret_cast<uint32_t*>(wb);
+    T.dur = u;
+    T.dsp = u + RM;
+    T.pmx = u + 2 * RM;
+    T.smx = u + 3 * RM;
+    T.lnea = u + 4 * RM;
+    T.lnb = reinterpret_cast<int32_t*>(u + 5 * RM);
+    T.sp = u + 6 * RM;
+    T.zd = u + (6 + LV - 1) * RM;
+    uint16_t* h = reinterpret_cast<uint16_t*>(T.zd + kRouteZoneMax);
+    T.rs = h + 2 * npad;
+    T.send = T.rs + RM;
+    T.zs = T.send + SEGS;
+    uint8_t* b = reinterpret_cast<uint8_t*>(T.zs + kRouteZoneMax);
+    T.rid = b;
+    T.rid2 = b + npad;
+    T.cus = b + 2 * npad;
+    T.zc = T.cus + RM;
+  }
+  uint16_t* A = reinterpret_cast<uint16_t*>(T.zd + kRouteZoneMax);
   uint16_t* B = A + npad;
-  uint16_t* Best = B + npad;
-  RouteStats R;
-  R.segid = Best + npad;
-  R.send = R.segid + npad;
-  uint32_t* u = reinterpret_cast<uint32_t*>(wb + 4u * npad * 2u + (((uint32_t)SEGS * 2u + 3u) & ~3u));
-  R.rc = u;
-  R.ds = u + SEGS;
-  R.dm = u + 2 * SEGS;
-  R.ne = u + 3 * SEGS;
-  R.rcp = u + 4 * SEGS;
-  R.dsp = u + 5 * SEGS;
-  R.pmx = u + 6 * SEGS;
-  R.smx = u + 7 * SEGS;
-  R.lnea = u + 8 * SEGS;
-  R.xb = reinterpret_cast<int32_t*>(u + 9 * SEGS);
-  R.lnb = reinterpret_cast<int32_t*>(u + 10 * SEGS);
-  R.sp = u + 11 * SEGS;
-  auto SP = [&](int l) { return l ? R.sp + (l - 1) * SEGS : R.dm; };
   const uint16_t* gcur = a.cur + (int64_t)chain * n;
   for (int q = lane; q < n; q += 64) A[q] = gcur[q];
   wave_sync();
   const uint32_t Nm1 = (uint32_t)a.si.N - 1;
   const int cap0 = I.sp.cap[0], st0 = I.sp.start[0];
   const int32_t* dem = I.sp.dem;
-  // greedy split of tokens tok(q), q in [from, to), starting a fresh route:
-  // routes used (closures incl. the final one), duration sum / max, and the
-  // closures before the last customer (-1: no customer)
-  struct SegCost {
-    uint32_t rc, ds, dm;
-    int xs;
+  auto SP = [&](int l) { return l ? T.sp + (l - 1) * RM : T.dur; };
+
+  // greedy split state of one walk and what it has closed so far
+  struct Walk {
+    int load, t;
+    uint32_t prev, cnt, ds, dm;
+    int xs;    // closures before the last customer (-1: none yet)
+    int pret;  // return leg of prev (prefetched walks on a static matrix)
   };
-  auto seg_walk = [&](int from, int to, auto tok) {
-    int load = 0, t = st0;
-    uint32_t prev = 0, cnt = 0, ds = 0, dm = 0;
-    int xs = -1;
-    auto close = [&]() {
-      if (prev) {
-        t += I.D(t, prev, 0);
-        const uint32_t rd = (uint32_t)(t - st0);
-        ds += rd;
-        dm = max(dm, rd);
+  auto fresh = [&](Walk& w) {
+    w.load = 0;
+    w.t = st0;
+    w.prev = 0;
+    w.cnt = w.ds = w.dm = 0;
+    w.xs = -1;
+    w.pret = 0;
+  };
+  auto close = [&](Walk& w) -> uint32_t {  // returns the closed route's duration
+    uint32_t rd = 0;
+    if (w.prev) {
+      w.t += I.D(w.t, w.prev, 0);
+      rd = (uint32_t)(w.t - st0);
+      w.ds += rd;
+      w.dm = max(w.dm, rd);
+    }
+    ++w.cnt;
+    w.load = 0;
+    w.t = st0;
+    w.prev = 0;
+    return rd;
+  };
+  // does token c close the walk's route when processed (separator or no room)?
+  auto closes = [&](const Walk& w, uint32_t c) { return c == 0 || w.load + dem[c] > cap0; };
+  auto add = [&](Walk& w, uint32_t c) {  // customer c after any overflow closure
+    w.t += I.D(w.t, w.prev, c);
+    w.load += dem[c];
+    w.prev = c;
+    w.xs = (int)w.cnt;
+  };
+  auto tokA = [&](int q) { return min((uint32_t)A[q], Nm1); };
+  // the pricing walk's token: customer and (static matrix) prefetched legs
+  struct WTok {
+    uint32_t c, cp;  // token and the token before it
+    int ein, eout, eret;
+  };
+  auto close_tok = [&](Walk& w) {
+    if constexpr (HM == 1) {
+      if (w.prev) {
+        w.t += w.pret;
+        const uint32_t rd = (uint32_t)(w.t - st0);
+        w.ds += rd;
+        w.dm = max(w.dm, rd);
       }
-      ++cnt;
-      load = 0;
-      t = st0;
-      prev = 0;
-    };
-    for (int q = from; q < to; ++q) {
-      const uint32_t c = min((uint32_t)tok(q), Nm1);
-      if (c == 0) {
-        close();
-        continue;
-      }
-      const int d = dem[c];
-      if (load + d > cap0) close();
-      t += I.D(t, prev, c);
-      load += d;
-      prev = c;
-      xs = (int)cnt;
+      ++w.cnt;
+      w.load = 0;
+      w.t = st0;
+      w.prev = 0;
+    } else {
+      close(w);
     }
-    const int xs_last = xs;
-    close();
-    return SegCost{cnt, ds, dm, xs_last};
   };
-  // segment index of every position and each segment's terminator; the
-  // number of separators
-  auto build_segments = [&]() -> int {
-    int carry = 0;
-    for (int base = 0; base < n; base += 64) {
-      const int q = base + lane;
-      const bool z = q < n && A[q] == 0;
-      const uint64_t ball = __ballot(z);
-      const int pre = carry + __popcll(ball & ((1ull << lane) - 1ull));
-      if (q < n) R.segid[q] = (uint16_t)pre;
-      if (z && pre < SEGS - 1) R.send[pre] = (uint16_t)q;
-      carry += __popcll(ball);
+  auto add_tok = [&](Walk& w, const WTok& x, int d) {
+    if constexpr (HM == 1) {
+      w.t += w.prev ? x.ein : x.eout;  // prev is the token before, or 0 after a closure
+      w.load += d;
+      w.prev = x.c;
+      w.pret = x.eret;
+      w.xs = (int)w.cnt;
+    } else {
+      add(w, x.c);
     }
-    if (lane == 0 && carry < SEGS - 1) R.send[carry] = (uint16_t)n;
-    wave_sync();
-    return carry;
   };
-  auto walk_segments = [&](int s0, int s1) {  // segments s0..s1 of A
-    for (int s = s0 + lane; s <= s1; s += 64) {
-      const int from = s ? R.send[s - 1] + 1 : 0, to = R.send[s];
-      const SegCost sc = seg_walk(from, to, [&](int q) { return (uint32_t)A[q]; });
-      R.rc[s] = sc.rc;
-      R.ds[s] = sc.ds;
-      R.dm[s] = sc.dm;
-      R.ne[s] = sc.xs >= 0 ? 1u : 0u;
-    }
-    wave_sync();
-  };
-  // prefix sums / maxima over segments 0..S (entries 0..S+1)
-  auto scan_segments = [&](int S) {
-    uint32_t crc = 0, cds = 0, cmx = 0;
+
+  // per-route prefix tables over routes 0..R-1 (entries 0..R)
+  auto derive = [&](int R) {
+    uint32_t cds = 0, cmx = 0;
     int clnb = -1;
-    for (int base = 0; base <= S + 1; base += 64) {
-      const int s = base + lane;
-      const bool in = s <= S;
-      const uint32_t rc = in ? R.rc[s] : 0u, ds = in ? R.ds[s] : 0u, dm = in ? R.dm[s] : 0u;
-      const uint32_t irc = wave_scan_incl<false>(rc), ids = wave_scan_incl<false>(ds);
-      const uint32_t imx = wave_scan_incl<true>(dm);
-      const int nb = in && R.ne[s] ? s : -1;
-      const int ilnb = (int)wave_scan_incl<true>((uint32_t)(nb + 1)) - 1;  // last nonempty <= s
-      if (s <= S + 1) {  // exclusive: entries for segments < s
-        R.rcp[s] = crc + irc - rc;
-        R.dsp[s] = cds + ids - ds;
-      }
+    for (int base = 0; base <= R; base += 64) {
+      const int r = base + lane;
+      const bool in = r < R;
+      const uint32_t d = in ? T.dur[r] : 0u;
+      const int nb = in && T.cus[r] ? r : -1;
+      const uint32_t ids = wave_scan_incl<false>(d), imx = wave_scan_incl<true>(d);
+      const int ilnb = (int)wave_scan_incl<true>((uint32_t)(nb + 1)) - 1;
       const uint32_t ex_mx = (uint32_t)__shfl_up((int)imx, 1, 64);
       const int ex_lnb = __shfl_up(ilnb, 1, 64);
-      if (s <= S + 1) {
-        R.pmx[s] = max(cmx, lane ? ex_mx : 0u);
-        const int lnb = max(clnb, lane ? ex_lnb : -1);
-        R.xb[s] = lnb;  // segment index for now; turned into closures below
+      if (r <= R) {
+        T.dsp[r] = cds + ids - d;
+        T.pmx[r] = max(cmx, lane ? ex_mx : 0u);
+        T.lnb[r] = max(clnb, lane ? ex_lnb : -1);
       }
-      crc += (uint32_t)__shfl((int)irc, 63, 64);
       cds += (uint32_t)__shfl((int)ids, 63, 64);
       cmx = max(cmx, (uint32_t)__shfl((int)imx, 63, 64));
       clnb = max(clnb, __shfl(ilnb, 63, 64));
     }
-    wave_sync();
-    // suffix max of dm and "any customer at or after s", from the top
     uint32_t smx = 0, sne = 0;
-    for (int top = S + 1; top >= 0; top -= 64) {
-      const int s = top - lane;
-      const bool in = s >= 0 && s <= S;
-      const uint32_t dm = in ? R.dm[s] : 0u, ne = in ? R.ne[s] : 0u;
-      const uint32_t imx = wave_scan_incl<true>(dm), ine = wave_scan_incl<true>(ne);
-      if (s >= 0) {
-        R.smx[s] = max(smx, imx);
-        R.lnea[s] = max(sne, ine);
+    for (int top = R; top >= 0; top -= 64) {
+      const int r = top - lane;
+      const bool in = r >= 0 && r < R;
+      const uint32_t d = in ? T.dur[r] : 0u, ne = in ? (uint32_t)T.cus[r] : 0u;
+      const uint32_t imx = wave_scan_incl<true>(d), ine = wave_scan_incl<true>(ne);
+      if (r >= 0) {
+        T.smx[r] = max(smx, imx);
+        T.lnea[r] = max(sne, ine);
       }
       smx = max(smx, (uint32_t)__shfl((int)imx, 63, 64));
       sne = max(sne, (uint32_t)__shfl((int)ine, 63, 64));
     }
     wave_sync();
-    for (int s = lane; s <= S + 1; s += 64) {
-      const int lnb = R.xb[s];
-      R.lnb[s] = lnb;
-      R.xb[s] = lnb >= 0 ? (int32_t)(R.rcp[lnb + 1] - 1u) : -1;
-    }
-    // sparse table of dm for range maxima between two zones
     for (int l = 1; l < LV; ++l) {
       const int w = 1 << (l - 1);
       const uint32_t* src = SP(l - 1);
       uint32_t* dst = SP(l);
-      for (int s = lane; s + 2 * w <= S + 1; s += 64) dst[s] = max(src[s], src[s + w]);
+      for (int r = lane; r + 2 * w <= R; r += 64) dst[r] = max(src[r], src[r + w]);
       wave_sync();
     }
-    wave_sync();
   };
-  auto range_max = [&](int lo_s, int hi_s) -> uint32_t {  // max dm over segments lo_s..hi_s
-    if (lo_s > hi_s) return 0u;
-    const int l = 31 - __builtin_clz((uint32_t)(hi_s - lo_s + 1));
+  auto range_max = [&](int r0, int r1) -> uint32_t {  // max dur over routes r0..r1
+    if (r0 > r1) return 0u;
+    const int l = 31 - __builtin_clz((uint32_t)(r1 - r0 + 1));
     const uint32_t* t = SP(l);
-    return max(t[lo_s], t[hi_s - (1 << l) + 1]);
+    return max(t[r0], t[r1 - (1 << l) + 1]);
+  };
+
+  // Full route tables of A: separators cut the tour into segments the lanes
+  // split in parallel (two passes: route counts, then routes at their global
+  // index).  Returns R, or -1 when the tables cannot hold the split.
+  auto full_build = [&]() -> int {
+    int S = 0;
+    for (int base = 0; base < n; base += 64) {
+      const int q = base + lane;
+      const bool z = q < n && A[q] == 0;
+      const uint64_t ball = __ballot(z);
+      const int pre = S + __popcll(ball & ((1ull << lane) - 1ull));
+      if (z && pre < SEGS - 1) T.send[pre] = (uint16_t)q;
+      S += __popcll(ball);
+    }
+    if (S > SEGS - 2) return -1;
+    if (lane == 0) T.send[S] = (uint16_t)n;
+    wave_sync();
+    // pass 1: routes per segment (T.smx as scratch), exclusive prefix (T.pmx)
+    for (int s = lane; s <= S; s += 64) {
+      const int from = s ? T.send[s - 1] + 1 : 0, to = T.send[s];
+      Walk w;
+      fresh(w);
+      for (int q = from; q < to; ++q) {
+        const uint32_t c = tokA(q);
+        if (closes(w, c)) close(w);
+        add(w, c);
+      }
+      close(w);
+      T.smx[s] = w.cnt;
+    }
+    wave_sync();
+    uint32_t carry = 0;
+    for (int base = 0; base <= S; base += 64) {
+      const int s = base + lane;
+      const uint32_t v = s <= S ? T.smx[s] : 0u;
+      const uint32_t inc = wave_scan_incl<false>(v);
+      if (s <= S) T.pmx[s] = carry + inc - v;
+      carry += (uint32_t)__shfl((int)inc, 63, 64);
+    }
+    const int R = (int)carry;
+    if (R > RMAX) return -1;
+    wave_sync();
+    // pass 2: each segment's routes at their global index, rid of each position
+    for (int s = lane; s <= S; s += 64) {
+      const int from = s ? T.send[s - 1] + 1 : 0, to = T.send[s];
+      int r = (int)T.pmx[s], start = from;
+      Walk w;
+      fresh(w);
+      for (int q = from; q < to; ++q) {
+        const uint32_t c = tokA(q);
+        if (closes(w, c)) {
+          const bool cu = w.prev != 0;
+          T.dur[r] = close(w);
+          T.cus[r] = cu ? 1 : 0;
+          T.rs[r] = (uint16_t)start;
+          ++r;
+          start = q;
+        }
+        add(w, c);
+        T.rid[q] = (uint8_t)r;
+      }
+      const bool cu = w.prev != 0;
+      T.dur[r] = close(w);
+      T.cus[r] = cu ? 1 : 0;
+      T.rs[r] = (uint16_t)start;
+      if (to < n) T.rid[to] = (uint8_t)r;
+    }
+    if (lane == 0) T.rs[R] = (uint16_t)n;
+    wave_sync();
+    derive(R);
+    return R;
   };
 
   // the current tour
@@ -453,75 +560,169 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
     auto tour = [&](int i) { return (uint32_t)A[i]; };
     ck = eval_tour<true>(I.D, I.sp, tour, n).key;
   }
-  int S = build_segments();
-  const bool route_ok = S + 1 <= K;  // wave-uniform: else every move is re-evaluated in full
-  if (route_ok) {
-    walk_segments(0, S);
-    scan_segments(S);
-  }
+  int R = full_build();
+  bool route_ok = R >= 0;
+  uint16_t* gbest = a.best + (int64_t)chain * n;
   uint64_t bk = a.best_key[chain];
-  bool best_in_lds = false;
   if (ck < bk) {
     bk = ck;
-    for (int q = lane; q < n; q += 64) Best[q] = A[q];
-    best_in_lds = true;
+    for (int q = lane; q < n; q += 64) gbest[q] = A[q];
   }
   float invT = a.inv_t0;
+#ifdef VRPMS_ROUTE_PROF
+  unsigned long long pf[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long pwalk = 0, pblk = 0, pset = 0;
+#endif
   for (int st = 0; st < a.steps && n >= 2; ++st) {
+#ifdef VRPMS_ROUTE_PROF
+    const unsigned long long pt0 = wall_clock64();
+    int wtok = 0;
+#endif
     const uint64_t step = a.step0 + (uint64_t)st;
     const u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)chain,
                            (uint32_t)lane, a.seed_lo, a.seed_hi);
     const Move m = decode_move_window(r.x, r.y, r.z, n, a.window, a.window_types);
-    auto moved = [&](int q) { return (uint32_t)A[moved_index(q, m)]; };
-    uint64_t k;
+    auto moved = [&](int q) { return min((uint32_t)A[moved_index(q, m)], Nm1); };
+    uint64_t k = 0;
     // an unserved customer cannot be accepted from a tour serving everyone
     // when 2^28 * invT puts the acceptance threshold at 0 (tour.hpp)
     const bool shortcut = (ck >> 56) == 0 && invT >= 0x1p-20f;
-    int s_lo = 0, s_hi = 0;
     bool full = !route_ok;
+    // zone bookkeeping (for the accepted move's table update)
+    int r1s = 0, r1e = 0, r2s = 0, r2e = 0, P1 = 0, Z2 = 0, q1 = 0, q2 = 0, dl = 0;
+    uint32_t c1 = 0, c2 = 0;
     if (route_ok) {
-      // the segments a move changes: the one holding each end, plus the next
-      // one when that end is a separator (it merges with or splits off its
-      // neighbour).  Swap / relocate leave the segments between the two ends
-      // intact (a relocate shifts them by one position), so when those groups
-      // do not touch they are priced as two zones; a 2-opt reverses the whole
-      // span, priced as one zone.
       const int lo = min(m.i, m.j), hi = max(m.i, m.j);
-      const int a1 = R.segid[lo], b1 = a1 + (A[lo] == 0 ? 1 : 0);
-      const int a2 = R.segid[hi], b2 = a2 + (A[hi] == 0 ? 1 : 0);
-      const bool two = m.typ != kMove2Opt && b1 < a2;
-      const int from1 = a1 ? R.send[a1 - 1] + 1 : 0;
-      s_lo = a1;
-      s_hi = b2;
-      SegCost z1, z2{0u, 0u, 0u, -1};
-      uint32_t old1, old2 = 0u;  // routes of the old segments each zone replaces
-      int d1, d2 = 0;
-      uint32_t dsum, dmax;
-      if (two) {
-        // tokens between the zones move by dl positions (relocate i < j: -1)
-        const int dl = m.typ == kMoveSwap ? 0 : (m.i < m.j ? -1 : 1);
-        z1 = seg_walk(from1, (int)R.send[b1] + dl, moved);
-        z2 = seg_walk((int)R.send[a2 - 1] + 1 + dl, (int)R.send[b2], moved);
-        old1 = R.rcp[b1 + 1] - R.rcp[a1];
-        old2 = R.rcp[b2 + 1] - R.rcp[a2];
-        dsum = R.dsp[S + 1] - (R.dsp[b1 + 1] - R.dsp[a1]) - (R.dsp[b2 + 1] - R.dsp[a2]) + z1.ds +
-               z2.ds;
-        dmax = max(max(max(R.pmx[a1], R.smx[b2 + 1]), max(z1.dm, z2.dm)), range_max(b1 + 1, a2 - 1));
-        d2 = (int)z2.rc - (int)old2;
-      } else {
-        z1 = seg_walk(from1, (int)R.send[b2], moved);
-        old1 = R.rcp[b2 + 1] - R.rcp[a1];
-        dsum = R.dsp[S + 1] - (R.dsp[b2 + 1] - R.dsp[a1]) + z1.ds;
-        dmax = max(max(R.pmx[a1], R.smx[b2 + 1]), z1.dm);
+      int bq0 = lo + 1;  // first moved position of the shifted middle
+      if (m.typ == kMoveRelocate && m.i < m.j) {
+        dl = -1;
+        bq0 = lo;
+      } else if (m.typ == kMoveRelocate) {
+        dl = 1;
       }
-      d1 = (int)z1.rc - (int)old1;
+      // a changed token also decides whether the route before it closes
+      // there, so each zone starts at the route holding the position before
+      // its first change (a relocate to j > i inserts after A[hi], which stays)
+      r1s = lo > 0 ? T.rid[lo - 1] : 0;
+      P1 = T.rs[r1s];
+      r2s = (m.typ == kMoveRelocate && m.i < m.j) || m.typ == kMove2Opt ? T.rid[hi] : T.rid[hi - 1];
+      Z2 = (int)T.rs[r2s] + dl;
+      const bool two = m.typ != kMove2Opt && Z2 > bq0;
+      int phase = two ? 1 : 3;  // 1: first zone, 2: second zone, 3: one merged zone
+      Walk w, w1;
+      fresh(w);
+      fresh(w1);
+      r2e = R;
+      int q = P1;
+      // The walk goes in blocks of kBlk tokens: their tokens, demands,
+      // depot legs and "current tour starts a route here" flags are read
+      // from LDS, and on a static matrix their edges from the token before
+      // (which depend only on the tokens) are gathered from L2 together, so
+      // a block costs one round trip instead of one per token.  A
+      // time-dependent matrix reads each edge at the clock.
+      bool fin = false;
+#ifdef VRPMS_ROUTE_PROF
+      const unsigned long long pw0 = wall_clock64();
+      pset = pw0 - pt0;
+#endif
+      while (!fin) {
+#ifdef VRPMS_ROUTE_PROF
+        ++pblk;
+#endif
+        WTok blk[kBlk];
+        int dm_[kBlk];
+        bool smid[kBlk], saft[kBlk];
+        {
+          uint32_t cp = q > 0 ? moved(q - 1) : 0u;
+#pragma unroll
+          for (int i = 0; i < kBlk; ++i) {
+            const int qq = q + i;
+            blk[i].c = qq < n ? moved(qq) : 0u;
+            blk[i].cp = cp;
+            cp = blk[i].c;
+          }
+#pragma unroll
+          for (int i = 0; i < kBlk; ++i) {
+            if constexpr (HM == 1) {
+              blk[i].ein = I.D(0, blk[i].cp, blk[i].c);
+              blk[i].eout = (int)legs[blk[i].c];
+              blk[i].eret = (int)legs[a.si.N + blk[i].c];
+            }
+            dm_[i] = dem[blk[i].c];
+            const int qq = q + i, qo = qq - dl;
+            smid[i] = qo >= 0 && qo < n && (int)T.rs[T.rid[qo]] == qo;
+            saft[i] = qq < n && (int)T.rs[T.rid[qq]] == qq;
+          }
+        }
+        int adv = kBlk;
+#pragma unroll
+        for (int i = 0; i < kBlk; ++i) {
+          const int qq = q + i;
+          if (qq >= n) {  // blocks start at or before n: qq == n here
+            fin = true;
+            adv = i;
+            break;
+          }
+          const uint32_t c = blk[i].c;
+          // back in step at a route start of the current tour: the walk's
+          // route is fresh there, or the customer there does not fit (a
+          // separator would close the walk's route, not the tour's empty one)
+          const bool nofit = c != 0 && w.load + dm_[i] > cap0;
+          if (phase == 1 && qq >= bq0) {  // the middle: moved(qq) = A[qq - dl]
+            if (smid[i] && (w.prev == 0 || nofit)) {
+              if (w.prev != 0) close_tok(w);  // the token opens a route in both tours
+              w1 = w;
+              r1e = T.rid[qq - dl];
+              q1 = qq;
+              fresh(w);
+              phase = 2;
+              adv = Z2 - q;  // the second zone starts fresh at Z2
+              break;
+            }
+            if (qq == Z2) phase = 3;  // never back in step before the second end
+          }
+          if (phase >= 2 && qq > hi) {  // after both ends: moved(qq) = A[qq]
+            if (saft[i] && (w.prev == 0 || nofit)) {
+              if (w.prev != 0) close_tok(w);
+              r2e = T.rid[qq];
+              fin = true;
+              adv = i;
+              break;
+            }
+          }
+          if (c == 0 || nofit) close_tok(w);
+          if (c) add_tok(w, blk[i], dm_[i]);
+#ifdef VRPMS_ROUTE_PROF
+          ++wtok;
+#endif
+        }
+        q += adv;
+      }
+#ifdef VRPMS_ROUTE_PROF
+      pwalk = wall_clock64() - pw0;
+#endif
+      if (q >= n) close_tok(w);  // the tour end closes the last route
+      q2 = q;
+      if (phase != 2) {  // one zone: routes r1s .. r2e - 1
+        w1 = w;
+        fresh(w);
+        r1e = r2s = r2e;
+        q1 = Z2 = q2;
+      }
+      c1 = w1.cnt;
+      c2 = w.cnt;
+      const int d1 = (int)w1.cnt - (r1e - r1s), d2 = (int)w.cnt - (r2e - r2s);
       int X;  // closures before the moved tour's last customer
-      if (R.lnea[b2 + 1]) X = R.xb[S + 1] + d1 + d2;
-      else if (z2.xs >= 0) X = (int)R.rcp[a2] + d1 + z2.xs;
-      else if (two && R.lnb[a2] > b1) X = R.xb[a2] + d1;
-      else if (z1.xs >= 0) X = (int)R.rcp[a1] + z1.xs;
-      else X = R.xb[a1];
+      if (T.lnea[r2e]) X = T.lnb[R] + d1 + d2;
+      else if (w.xs >= 0) X = r2s + d1 + w.xs;
+      else if (T.lnb[r2s] >= r1e) X = T.lnb[r2s] + d1;
+      else if (w1.xs >= 0) X = r1s + w1.xs;
+      else X = T.lnb[r1s];
       if (X < K) {
+        const uint32_t dsum = T.dsp[R] - (T.dsp[r1e] - T.dsp[r1s]) - (T.dsp[r2e] - T.dsp[r2s]) +
+                              w1.ds + w.ds;
+        const uint32_t dmax = max(max(max(T.pmx[r1s], T.smx[r2e]), max(w1.dm, w.dm)),
+                                  range_max(r1e, r2s - 1));
         k = cvrp_key(0, dsum, dmax, I.sp.objective);
       } else if (shortcut) {
         k = ~0ull;
@@ -538,12 +739,37 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
       const uint32_t dp = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
       accept = ((uint32_t)wave_bcast((int)r.w, bl) >> 8) < accept_threshold(dp, invT);
     }
+#ifdef VRPMS_ROUTE_PROF
+    const unsigned long long pt1 = wall_clock64();
+    {
+      int mx = wtok, sm = wtok;
+      for (int off = 32; off > 0; off >>= 1) {
+        mx = max(mx, __shfl_xor(mx, off, 64));
+        sm += __shfl_xor(sm, off, 64);
+      }
+      pf[0] += pt1 - pt0;
+      pf[2] += 1;
+      pf[3] += accept ? 1 : 0;
+      pf[4] += (unsigned long long)mx;
+      pf[5] += (unsigned long long)sm;
+      pf[6] += (unsigned long long)__popcll(__ballot(full));
+      unsigned long long wmx = pwalk, bmx = pblk, smx = pset;
+      for (int off = 32; off > 0; off >>= 1) {
+        wmx = max(wmx, (unsigned long long)__shfl_xor((long long)wmx, off, 64));
+        bmx = max(bmx, (unsigned long long)__shfl_xor((long long)bmx, off, 64));
+        smx = max(smx, (unsigned long long)__shfl_xor((long long)smx, off, 64));
+      }
+      pf[8] += wmx;
+      pf[9] += bmx;
+      pf[10] += smx;
+      pblk = 0;
+    }
+#endif
     if (accept) {
       Move mb;
       mb.typ = (uint32_t)wave_bcast((int)m.typ, bl);
       mb.i = wave_bcast(m.i, bl);
       mb.j = wave_bcast(m.j, bl);
-      const int bs_lo = wave_bcast(s_lo, bl), bs_hi = wave_bcast(s_hi, bl);
       for (int q = lane; q < n; q += 64) B[q] = A[moved_index(q, mb)];
       wave_sync();
       uint16_t* t = A;
@@ -552,27 +778,135 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
       ck = k;
       if (ck < bk) {
         bk = ck;
-        for (int q = lane; q < n; q += 64) Best[q] = A[q];
-        best_in_lds = true;
+        for (int q = lane; q < n; q += 64) gbest[q] = A[q];
+      }
+      if (route_ok) {
+        // the accepted lane's zones, in positions of the new tour A
+        const int br1s = wave_bcast(r1s, bl), br1e = wave_bcast(r1e, bl);
+        const int br2s = wave_bcast(r2s, bl), br2e = wave_bcast(r2e, bl);
+        const int bP1 = wave_bcast(P1, bl), bZ2 = wave_bcast(Z2, bl);
+        const int bq1 = wave_bcast(q1, bl), bq2 = wave_bcast(q2, bl), bdl = wave_bcast(dl, bl);
+        const int bc1 = wave_bcast((int)c1, bl), bc2 = wave_bcast((int)c2, bl);
+        const int d1 = bc1 - (br1e - br1s), d2 = bc2 - (br2e - br2s);
+        const int R2 = R + d1 + d2;
+        if (R2 > RMAX || bc1 + bc2 > kRouteZoneMax) {
+          R = full_build();
+          route_ok = R >= 0;
+        } else {
+          // lane 0 re-walks the zones, recording their routes and positions
+          if (lane == 0) {
+            int zi = 0;
+            auto rec_zone = [&](int from, int to, int r0) {
+              Walk w;
+              fresh(w);
+              int start = from, rr = r0;
+              for (int q = from; q < to; ++q) {
+                const uint32_t c = tokA(q);
+#ifdef VRPMS_ROUTE_PROF
+                ++pf[7];
+#endif
+                if (closes(w, c)) {
+                  if (c == 0) {  // the separator ends this route: it belongs to it
+                    const bool cu = w.prev != 0;
+                    T.zd[zi] = close(w);
+                    T.zc[zi] = cu ? 1 : 0;
+                    T.zs[zi] = (uint16_t)start;
+                    T.rid2[q] = (uint8_t)rr;
+                    ++zi;
+                    ++rr;
+                    start = q + 1;
+                    continue;
+                  }
+                  const bool cu = w.prev != 0;
+                  T.zd[zi] = close(w);
+                  T.zc[zi] = cu ? 1 : 0;
+                  T.zs[zi] = (uint16_t)start;
+                  ++zi;
+                  ++rr;
+                  start = q;
+                }
+                add(w, c);
+                T.rid2[q] = (uint8_t)rr;
+              }
+              if (w.prev != 0 || to >= n) {  // resync right after a closed route needs none
+                const bool cu = w.prev != 0;
+                T.zd[zi] = close(w);
+                T.zc[zi] = cu ? 1 : 0;
+                T.zs[zi] = (uint16_t)start;
+                ++zi;
+              }
+            };
+            rec_zone(bP1, bq1, br1s);
+            if (bq1 < bq2) rec_zone(bZ2, bq2, br2s + d1);
+          }
+          // the routes: before the first zone, the first zone's, the middle's
+          // (shifted by dl positions), the second zone's, the rest
+          uint32_t vd[4], vs[4], vc[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int rr = lane + 64 * i;
+            if (rr >= R2) break;
+            int src = -1, sh = 0;  // -1: a recorded zone route (read after the sync)
+            if (rr < br1s) src = rr;
+            else if (rr < br1s + bc1) src = -1;
+            else if (rr < br2s + d1) src = rr - d1, sh = bdl;
+            else if (rr >= br2s + d1 + bc2) src = rr - d1 - d2;
+            vd[i] = vs[i] = vc[i] = 0;
+            if (src >= 0) {
+              vd[i] = T.dur[src];
+              vs[i] = (uint32_t)((int)T.rs[src] + sh);
+              vc[i] = T.cus[src];
+            }
+          }
+          // the positions: unchanged before P1, recorded in the zones,
+          // shifted in the middle, renumbered after
+          for (int q = lane; q < n; q += 64) {
+            if (q < bP1) T.rid2[q] = T.rid[q];
+            else if (q >= bq1 && q < bZ2) T.rid2[q] = (uint8_t)(T.rid[q - bdl] + d1);
+            else if (q >= bq2) T.rid2[q] = (uint8_t)(T.rid[q] + d1 + d2);
+          }
+          wave_sync();
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int rr = lane + 64 * i;
+            if (rr >= R2) break;
+            int zrow = -1;
+            if (rr >= br1s && rr < br1s + bc1) zrow = rr - br1s;
+            else if (rr >= br2s + d1 && rr < br2s + d1 + bc2) zrow = bc1 + (rr - br2s - d1);
+            if (zrow >= 0) {
+              vd[i] = T.zd[zrow];
+              vs[i] = T.zs[zrow];
+              vc[i] = T.zc[zrow];
+            }
+            T.dur[rr] = vd[i];
+            T.rs[rr] = (uint16_t)vs[i];
+            T.cus[rr] = (uint8_t)vc[i];
+          }
+          if (lane == 0) T.rs[R2] = (uint16_t)n;
+          uint8_t* tr = T.rid;
+          T.rid = T.rid2;
+          T.rid2 = tr;
+          R = R2;
+          wave_sync();
+          derive(R);
+        }
       }
       wave_sync();
-      if (route_ok) {  // the move kept the separators of segments < s_lo and > s_hi in place
-        build_segments();
-        walk_segments(bs_lo, bs_hi);
-        scan_segments(S);
-      }
     }
+#ifdef VRPMS_ROUTE_PROF
+    pf[1] += wall_clock64() - pt1;
+#endif
     invT = invT * a.inv_alpha;
   }
   uint16_t* gout = a.cur + (int64_t)chain * n;
   for (int q = lane; q < n; q += 64) gout[q] = A[q];
-  if (best_in_lds) {
-    uint16_t* gb = a.best + (int64_t)chain * n;
-    for (int q = lane; q < n; q += 64) gb[q] = Best[q];
-  }
   if (lane == 0) {
     a.cur_key[chain] = ck;
     a.best_key[chain] = bk;
+#ifdef VRPMS_ROUTE_PROF
+    if (chain < 8192)
+      for (int i = 0; i < 12; ++i) g_route_prof[12 * chain + i] += pf[i];
+#endif
   }
 }
 
@@ -1483,14 +1817,15 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
   // exchangeable vehicles: one capacity, one start time, every demand fits
   const Instance& in = ctx->inst;
   if (p->window > 0 && in.problem == VRPMS_CVRP && in.uniform_cap &&
-      in.min_start == in.max_start && in.max_dem <= in.cap0 && ctx->opt_sa_route != 2) {
+      in.min_start == in.max_start && in.max_dem <= in.cap0 && route_max(in.K) <= 255 &&
+      n <= 65535 && ctx->opt_sa_route != 2) {
     const size_t npad = ((size_t)n + 7) & ~(size_t)7;
-    const size_t segs = (size_t)in.K + 2;
-    const size_t wbytes = ((size_t)route_wave_bytes((int)npad, (int)segs) + 15) & ~(size_t)15;
-    size_t lds = inst_lds_bytes_host(a.si) + 4 * wbytes;
+    const size_t wbytes = ((size_t)route_wave_bytes((int)npad, in.K) + 15) & ~(size_t)15;
+    const size_t legs = in.H == 1 ? (size_t)2 * in.N * (in.use16 ? 2 : 4) : 0;
+    size_t lds = inst_lds_bytes_host(a.si) + 4 * wbytes + legs;
     if (lds > ctx->max_lds) {
       a.si.mat_lds = 0;
-      lds = inst_lds_bytes_host(a.si) + 4 * wbytes;
+      lds = inst_lds_bytes_host(a.si) + 4 * wbytes + legs;
     }
     if (lds <= ctx->max_lds)
       return launch_inst<RouteK>(ctx, dim3((p->chains + 3) / 4), dim3(256), lds,
@@ -1733,3 +2068,16 @@ extern "C" int vrpms_tsp_batch_sa(vrpms_ctx* ctx, const int32_t* d_mats, int32_t
   VRPMS_HIP(hipGetLastError());
   return VRPMS_OK;
 }
+
+#ifdef VRPMS_ROUTE_PROF
+extern "C" int vrpms_debug_route_prof(unsigned long long* out, int count, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vrpms::g_route_prof),
+                          sizeof(unsigned long long) * count) != hipSuccess)
+    return -2;
+  if (reset) {
+    static unsigned long long zero[12 * 8192];
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(vrpms::g_route_prof), zero, sizeof(zero));
+  }
+  return 0;
+}
+#endif
