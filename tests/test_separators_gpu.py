@@ -185,6 +185,10 @@ ROUTE_CASES = [
     ("cvrp150_hot", lambda: synth.cvrp(150, 12, seed=3), "greedy", 8, 30, 1e-7, 8, 0),
     ("cvrp150_pack_hot", lambda: synth.cvrp(150, 12, seed=5, slack=1.02), "pack", 8, 40, 1e-7, 6,
      2),
+    # no separators at all: one segment, re-synchronising walks cascade over many
+    # routes (more than a lane records: the accepted zones are re-walked)
+    ("cvrp200_no_seps", lambda: synth.cvrp(200, 16, seed=7, slack=1.3), "nosep", 8, 80,
+     1 / 50.0, 12, 2),
     # many separators per route (S > K - 1 is never route-local; S < K - 1 is)
     ("cvrp120_few_seps", lambda: synth.cvrp(120, 10, seed=6), "pack_few", 8, 40, 1 / 100.0, 5, 2),
 ]
@@ -198,8 +202,10 @@ def test_route_local_sa_matches_c_restatement(ctx, coracle, name, maker, start, 
     restatement's full re-evaluation, and against sa_kernel on the device."""
     inst = maker()
     load(ctx, inst)
-    S = inst.K - 1 if start != "pack_few" else inst.K - 4
-    if start != "random":
+    S = {"pack_few": inst.K - 4, "nosep": 0}.get(start, inst.K - 1)
+    if start == "nosep":
+        P = synth.random_perms(chains, inst.n, seed=9, dtype=np.uint16)
+    elif start != "random":
         P0 = synth.random_perms(chains, inst.n, seed=9, dtype=np.uint16)
         f = spec.insert_separators if start == "greedy" else spec.pack_separators
         P = np.array([f(p, S, inst.demand, inst.capacities) for p in P0])

@@ -52,7 +52,7 @@ if "--schedule" not in sys.argv:
 # many current tours leave customers unserved (their moves re-walk in full)
 if "--schedule" in sys.argv:
     import bench
-    r = runners.SARunner(ctx, x.n, chains=4096, seed=1000, total_steps=1000,
+    r = runners.SARunner(ctx, x.n, chains=2048, seed=1000, total_steps=1000,
                          durations=x.durations, t0=0.5 * edge, t_end=0.002 * edge,
                          n_sep=x.K - 1, window=32, window_types=2, start="pack")
     cool = bench._TimedCooling(6.0, 0.5 * edge, 0.002 * edge)

@@ -66,10 +66,12 @@ def run():
             "walk_tokens_wave_max": round(a[4] / st, 1),
             "walk_tokens_lane_mean": round(a[5] / st / 64, 1),
             "full_lanes_per_step": round(a[6] / st, 2),
-            "rewalk_tokens_per_accept": round(a[7] / max(a[3], 1), 1),
+            "full_builds_per_accept": round(a[7] / max(a[3], 1), 4),
             "us_walk_wave_max": round(a[8] / st / 100.0, 2),
             "blocks_wave_max": round(a[9] / st, 2),
-            "us_before_walk_wave_max": round(a[10] / st / 100.0, 2),
+            "us_prologue_mean": round(a[10] / chains / 100.0, 1),
+            "ms_chain_kernel_mean": round(a[11] / chains / 1e5, 2),
+            "ms_launch_wall": round(dt * 1e3, 2),
             "best": r.best()[0] >> 28 & (2 ** 28 - 1)}), flush=True)
 
     r = runners.SARunner(ctx, x.n, chains=chains, seed=1000, total_steps=1000,

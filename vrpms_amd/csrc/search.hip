@@ -251,8 +251,8 @@ __global__ __launch_bounds__(256) void sa_kernel(SaArgs a) {
 // move re-walks its zones once, recording their routes, and the per-route
 // tables are rebuilt around them.
 // ===========================================================================
-constexpr int kRouteZoneMax = 64;  // routes one accepted zone pair may record
-constexpr int kBlk = 8;            // tokens a pricing walk reads (and fetches legs for) at once
+constexpr int kBlk = 8;         // tokens a pricing walk reads (and gathers edges for) at once
+constexpr int kTourRegs = 18;   // tour positions per lane held in registers on an accept
 
 __host__ __device__ inline int route_max(int K) { return 2 * K + 2; }  // routes stored
 __host__ __device__ inline int route_rm(int K) { return (route_max(K) + 1 + 7) & ~7; }
@@ -262,26 +262,27 @@ __host__ __device__ inline int route_levels(int rm) {
   return lv;
 }
 __host__ __device__ inline int route_segs(int K) { return (K + 2 + 7) & ~7; }
-// per-chain LDS: u32 tables, then u16 arrays, then u8 arrays
+// per-chain LDS: u32 [tour | demand], u32 tables, u32 route-start bits,
+// then u16 route starts / separator positions, then u8 route ids / flags
 __host__ __device__ inline uint32_t route_wave_bytes(int npad, int K) {
   const uint32_t rm = (uint32_t)route_rm(K), lv = (uint32_t)route_levels(route_rm(K));
-  const uint32_t u32s = (6u + (lv - 1u)) * rm + kRouteZoneMax;
-  const uint32_t u16s = 2u * (uint32_t)npad + rm + (uint32_t)route_segs(K) + kRouteZoneMax;
-  const uint32_t u8s = 2u * (uint32_t)npad + rm + kRouteZoneMax;
+  const uint32_t words = (uint32_t)npad / 32u + 4u;
+  const uint32_t u32s = (uint32_t)npad + (6u + (lv - 1u)) * rm + words;
+  const uint32_t u16s = rm + (uint32_t)route_segs(K);
+  const uint32_t u8s = (uint32_t)npad + rm;
   return 4u * u32s + 2u * u16s + u8s;
 }
 
 struct RouteTabs {
+  uint32_t* at;      // [npad] token | demand << 16 of each position (the current tour)
   uint32_t *dur, *dsp, *pmx, *smx, *lnea;  // per route; prefix sum / max, suffix max, customers >= r
   int32_t* lnb;      // last route < r holding a customer (-1: none)
   uint32_t* sp;      // sparse table of dur, level l >= 1 at sp + (l - 1) * rm
-  uint32_t* zd;      // recorded zone routes: duration
+  uint32_t* bits;    // bit q: a route starts at position q
   uint16_t* rs;      // first position of route r (rs[R] = n)
-  uint16_t* send;    // separator positions (init only)
-  uint16_t* zs;      // recorded zone routes: first position
-  uint8_t *rid, *rid2;  // route of each position (current, scratch)
+  uint16_t* send;    // separator positions (full builds only)
+  uint8_t* rid;      // route of each position
   uint8_t* cus;      // route holds a customer
-  uint8_t* zc;       // recorded zone routes: holds a customer
 };
 
 // Wave-wide inclusive scan (add or max) of v over lanes (shuffle steps).
@@ -299,13 +300,17 @@ VRPMS_DEV uint32_t wave_scan_incl(uint32_t v) {
 #ifdef VRPMS_ROUTE_PROF
 // per-chain counters (A/B builds only: tools/route_prof.py): pricing and
 // accept ticks (wall_clock64, 100 MHz), steps, accepts, walked tokens (wave
-// max, lane sum), lanes re-evaluated in full, tokens re-walked on accepts
+// max, lane sum), lanes re-evaluated in full, walk ticks (wave max), walk
+// blocks (wave max)
 __device__ unsigned long long g_route_prof[12 * 8192];
 #endif
 
 template <typename MatT, int HM>
 __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+#ifdef VRPMS_ROUTE_PROF
+  const unsigned long long pk0 = wall_clock64();
+#endif
   const StagedInst<MatT, HM> I = stage_inst<MatT, HM>(a.si, smem);
   const int n = a.n;
   const int wave = threadIdx.x >> 6, lane = lane_id();
@@ -316,15 +321,16 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
   const uint32_t npad = ((uint32_t)n + 7u) & ~7u;
   const uint32_t wbytes = (route_wave_bytes((int)npad, K) + 15u) & ~15u;
   unsigned char* wb = smem + inst_lds_bytes(a.si) + wave * wbytes;
+  const uint32_t N = (uint32_t)a.si.N;
   // static matrix: the depot legs out(c) = D(0, c) and ret(c) = D(c, 0) in
-  // LDS, so a pricing walk gathers one matrix entry per token from L2
+  // LDS (one u32 per node for a u16 matrix), so a pricing walk gathers one
+  // matrix entry per token from L2
   MatT* legs = reinterpret_cast<MatT*>(smem + inst_lds_bytes(a.si) + 4 * wbytes);
   if constexpr (HM == 1) {
     const MatT* M = static_cast<const MatT*>(a.si.mat);
-    const uint32_t N = (uint32_t)a.si.N;
     for (uint32_t c = threadIdx.x; c < N; c += blockDim.x) {
-      legs[c] = M[c];
-      legs[N + c] = M[(size_t)c * N];
+      legs[2 * c] = M[c];
+      legs[2 * c + 1] = M[(size_t)c * N];
     }
     __syncthreads();
   }
@@ -332,6 +338,8 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
   RouteTabs T;
   {
     uint32_t* u = reinterpret_cast<uint32_t*>(wb);
+    T.at = u;
+    u += npad;
     T.dur = u;
     T.dsp = u + RM;
     T.pmx = u + 2 * RM;
@@ -339,25 +347,26 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
     T.lnea = u + 4 * RM;
     T.lnb = reinterpret_cast<int32_t*>(u + 5 * RM);
     T.sp = u + 6 * RM;
-    T.zd = u + (6 + LV - 1) * RM;
-    uint16_t* h = reinterpret_cast<uint16_t*>(T.zd + kRouteZoneMax);
-    T.rs = h + 2 * npad;
-    T.send = T.rs + RM;
-    T.zs = T.send + SEGS;
-    uint8_t* b = reinterpret_cast<uint8_t*>(T.zs + kRouteZoneMax);
+    T.bits = u + (6 + LV - 1) * RM;
+    uint16_t* h = reinterpret_cast<uint16_t*>(T.bits + npad / 32u + 4u);
+    T.rs = h;
+    T.send = h + RM;
+    uint8_t* b = reinterpret_cast<uint8_t*>(T.send + SEGS);
     T.rid = b;
-    T.rid2 = b + npad;
-    T.cus = b + 2 * npad;
-    T.zc = T.cus + RM;
+    T.cus = b + npad;
   }
-  uint16_t* A = reinterpret_cast<uint16_t*>(T.zd + kRouteZoneMax);
-  uint16_t* B = A + npad;
-  const uint16_t* gcur = a.cur + (int64_t)chain * n;
-  for (int q = lane; q < n; q += 64) A[q] = gcur[q];
-  wave_sync();
-  const uint32_t Nm1 = (uint32_t)a.si.N - 1;
+  const uint32_t Nm1 = N - 1;
   const int cap0 = I.sp.cap[0], st0 = I.sp.start[0];
   const int32_t* dem = I.sp.dem;
+  {
+    const uint16_t* gcur = a.cur + (int64_t)chain * n;
+    for (int q = lane; q < n; q += 64) {
+      const uint32_t c = min((uint32_t)gcur[q], Nm1);
+      T.at[q] = c | ((uint32_t)dem[c] << 16);
+    }
+    wave_sync();
+  }
+  auto tokA = [&](int q) { return T.at[q] & 0xffffu; };
   auto SP = [&](int l) { return l ? T.sp + (l - 1) * RM : T.dur; };
 
   // greedy split state of one walk and what it has closed so far
@@ -365,7 +374,7 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
     int load, t;
     uint32_t prev, cnt, ds, dm;
     int xs;    // closures before the last customer (-1: none yet)
-    int pret;  // return leg of prev (prefetched walks on a static matrix)
+    int pret;  // return leg of prev (static matrix)
   };
   auto fresh = [&](Walk& w) {
     w.load = 0;
@@ -375,10 +384,19 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
     w.xs = -1;
     w.pret = 0;
   };
+  auto leg_out = [&](uint32_t c) -> int {
+    if constexpr (HM == 1) return (int)legs[2 * c];
+    else return 0;
+  };
+  auto leg_ret = [&](uint32_t c) -> int {
+    if constexpr (HM == 1) return (int)legs[2 * c + 1];
+    else return 0;
+  };
   auto close = [&](Walk& w) -> uint32_t {  // returns the closed route's duration
     uint32_t rd = 0;
     if (w.prev) {
-      w.t += I.D(w.t, w.prev, 0);
+      if constexpr (HM == 1) w.t += w.pret;
+      else w.t += I.D(w.t, w.prev, 0);
       rd = (uint32_t)(w.t - st0);
       w.ds += rd;
       w.dm = max(w.dm, rd);
@@ -389,46 +407,22 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
     w.prev = 0;
     return rd;
   };
-  // does token c close the walk's route when processed (separator or no room)?
-  auto closes = [&](const Walk& w, uint32_t c) { return c == 0 || w.load + dem[c] > cap0; };
-  auto add = [&](Walk& w, uint32_t c) {  // customer c after any overflow closure
-    w.t += I.D(w.t, w.prev, c);
-    w.load += dem[c];
+  // customer c with demand d, entered from prev (edge e_in when prev is the
+  // token before it on a static matrix, else the depot leg)
+  auto add = [&](Walk& w, uint32_t c, int d, int e_in) {
+    if constexpr (HM == 1) {
+      w.t += w.prev ? e_in : leg_out(c);
+      w.pret = leg_ret(c);
+    } else {
+      w.t += I.D(w.t, w.prev, c);
+    }
+    w.load += d;
     w.prev = c;
     w.xs = (int)w.cnt;
   };
-  auto tokA = [&](int q) { return min((uint32_t)A[q], Nm1); };
-  // the pricing walk's token: customer and (static matrix) prefetched legs
-  struct WTok {
-    uint32_t c, cp;  // token and the token before it
-    int ein, eout, eret;
-  };
-  auto close_tok = [&](Walk& w) {
-    if constexpr (HM == 1) {
-      if (w.prev) {
-        w.t += w.pret;
-        const uint32_t rd = (uint32_t)(w.t - st0);
-        w.ds += rd;
-        w.dm = max(w.dm, rd);
-      }
-      ++w.cnt;
-      w.load = 0;
-      w.t = st0;
-      w.prev = 0;
-    } else {
-      close(w);
-    }
-  };
-  auto add_tok = [&](Walk& w, const WTok& x, int d) {
-    if constexpr (HM == 1) {
-      w.t += w.prev ? x.ein : x.eout;  // prev is the token before, or 0 after a closure
-      w.load += d;
-      w.prev = x.c;
-      w.pret = x.eret;
-      w.xs = (int)w.cnt;
-    } else {
-      add(w, x.c);
-    }
+  auto edge = [&](uint32_t x, uint32_t y) -> int {  // static matrix entry (L2)
+    if constexpr (HM == 1) return I.D(0, x, y);
+    else return 0;
   };
 
   // per-route prefix tables over routes 0..R-1 (entries 0..R)
@@ -481,15 +475,26 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
     const uint32_t* t = SP(l);
     return max(t[r0], t[r1 - (1 << l) + 1]);
   };
+  // route-start bits from the route ids (a route starts where the id changes)
+  auto build_bits = [&]() {
+    for (int base = 0; base < (int)npad + 64; base += 64) {
+      const int q = base + lane;
+      const bool s = q < n && (q == 0 || T.rid[q] != T.rid[q - 1]);
+      const uint64_t ball = __ballot(s);
+      if (lane < 2 && (base >> 5) + lane < (int)(npad / 32u + 4u))
+        T.bits[(base >> 5) + lane] = (uint32_t)(lane ? ball >> 32 : ball);
+    }
+    wave_sync();
+  };
 
-  // Full route tables of A: separators cut the tour into segments the lanes
-  // split in parallel (two passes: route counts, then routes at their global
-  // index).  Returns R, or -1 when the tables cannot hold the split.
+  // Full route tables of the current tour: separators cut it into segments
+  // the lanes split in parallel (two passes: route counts, then routes at
+  // their global index).  Returns R, or -1 when the tables cannot hold it.
   auto full_build = [&]() -> int {
     int S = 0;
     for (int base = 0; base < n; base += 64) {
       const int q = base + lane;
-      const bool z = q < n && A[q] == 0;
+      const bool z = q < n && tokA(q) == 0;
       const uint64_t ball = __ballot(z);
       const int pre = S + __popcll(ball & ((1ull << lane) - 1ull));
       if (z && pre < SEGS - 1) T.send[pre] = (uint16_t)q;
@@ -504,9 +509,10 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
       Walk w;
       fresh(w);
       for (int q = from; q < to; ++q) {
-        const uint32_t c = tokA(q);
-        if (closes(w, c)) close(w);
-        add(w, c);
+        const uint32_t at = T.at[q], c = at & 0xffffu;
+        const int d = (int)(at >> 16);
+        if (w.load + d > cap0) close(w);
+        add(w, c, d, w.prev ? edge(w.prev, c) : 0);
       }
       close(w);
       T.smx[s] = w.cnt;
@@ -523,15 +529,16 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
     const int R = (int)carry;
     if (R > RMAX) return -1;
     wave_sync();
-    // pass 2: each segment's routes at their global index, rid of each position
+    // pass 2: each segment's routes at their global index, the route of each position
     for (int s = lane; s <= S; s += 64) {
       const int from = s ? T.send[s - 1] + 1 : 0, to = T.send[s];
       int r = (int)T.pmx[s], start = from;
       Walk w;
       fresh(w);
       for (int q = from; q < to; ++q) {
-        const uint32_t c = tokA(q);
-        if (closes(w, c)) {
+        const uint32_t at = T.at[q], c = at & 0xffffu;
+        const int d = (int)(at >> 16);
+        if (w.load + d > cap0) {
           const bool cu = w.prev != 0;
           T.dur[r] = close(w);
           T.cus[r] = cu ? 1 : 0;
@@ -539,7 +546,7 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
           ++r;
           start = q;
         }
-        add(w, c);
+        add(w, c, d, w.prev ? edge(w.prev, c) : 0);
         T.rid[q] = (uint8_t)r;
       }
       const bool cu = w.prev != 0;
@@ -551,13 +558,14 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
     if (lane == 0) T.rs[R] = (uint16_t)n;
     wave_sync();
     derive(R);
+    build_bits();
     return R;
   };
 
   // the current tour
   uint64_t ck;
   {
-    auto tour = [&](int i) { return (uint32_t)A[i]; };
+    auto tour = [&](int i) { return tokA(i); };
     ck = eval_tour<true>(I.D, I.sp, tour, n).key;
   }
   int R = full_build();
@@ -566,31 +574,38 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
   uint64_t bk = a.best_key[chain];
   if (ck < bk) {
     bk = ck;
-    for (int q = lane; q < n; q += 64) gbest[q] = A[q];
+    for (int q = lane; q < n; q += 64) gbest[q] = (uint16_t)tokA(q);
   }
   float invT = a.inv_t0;
 #ifdef VRPMS_ROUTE_PROF
   unsigned long long pf[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long pwalk = 0, pblk = 0, pset = 0;
+  pf[10] = wall_clock64() - pk0;
 #endif
   for (int st = 0; st < a.steps && n >= 2; ++st) {
 #ifdef VRPMS_ROUTE_PROF
     const unsigned long long pt0 = wall_clock64();
-    int wtok = 0;
+    int wtok = 0, wblk = 0;
+    unsigned long long pwalk = 0;
 #endif
     const uint64_t step = a.step0 + (uint64_t)st;
     const u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)chain,
                            (uint32_t)lane, a.seed_lo, a.seed_hi);
     const Move m = decode_move_window(r.x, r.y, r.z, n, a.window, a.window_types);
-    auto moved = [&](int q) { return min((uint32_t)A[moved_index(q, m)], Nm1); };
+    const MoveMap mm = move_map(m);
+    auto moved = [&](int q) { return tokA(map_src(mm, q)); };
     uint64_t k = 0;
     // an unserved customer cannot be accepted from a tour serving everyone
     // when 2^28 * invT puts the acceptance threshold at 0 (tour.hpp)
     const bool shortcut = (ck >> 56) == 0 && invT >= 0x1p-20f;
     bool full = !route_ok;
-    // zone bookkeeping (for the accepted move's table update)
+    // zone bookkeeping and the routes each zone closes (for an accept)
     int r1s = 0, r1e = 0, r2s = 0, r2e = 0, P1 = 0, Z2 = 0, q1 = 0, q2 = 0, dl = 0;
     uint32_t c1 = 0, c2 = 0;
+    // route starts of each zone as bits over its positions (zone start = bit
+    // 0; bits at or past the zone's end are ignored); zones of more than 128
+    // positions are re-walked on an accept
+    uint64_t zm[4] = {1ull, 0ull, 1ull, 0ull};
+    bool zovf = false;
     if (route_ok) {
       const int lo = min(m.i, m.j), hi = max(m.i, m.j);
       int bq0 = lo + 1;  // first moved position of the shifted middle
@@ -614,46 +629,56 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
       fresh(w1);
       r2e = R;
       int q = P1;
-      // The walk goes in blocks of kBlk tokens: their tokens, demands,
-      // depot legs and "current tour starts a route here" flags are read
-      // from LDS, and on a static matrix their edges from the token before
-      // (which depend only on the tokens) are gathered from L2 together, so
-      // a block costs one round trip instead of one per token.  A
-      // time-dependent matrix reads each edge at the clock.
+      int zbase = P1;  // first position of the zone being walked
+      bool z2 = false;
+      // close the walk's route; the next route starts at `next`
+      auto close_rec = [&](Walk& ww, int next) {
+        close(ww);
+        const uint32_t off = (uint32_t)(next - zbase);
+        if (off >= 128u) zovf = true;
+        const uint64_t b = 1ull << (off & 63u);
+        if (off < 64u) {
+          if (z2) zm[2] |= b;
+          else zm[0] |= b;
+        } else if (off < 128u) {
+          if (z2) zm[3] |= b;
+          else zm[1] |= b;
+        }
+      };
+      // The walk goes in blocks of kBlk tokens: their tokens and demands,
+      // depot legs and route-start bits are read from LDS, and on a static
+      // matrix their edges from the token before (which depend only on the
+      // tokens) are gathered from L2 together, so a block costs one round
+      // trip instead of one per token.  A time-dependent matrix reads each
+      // edge at the clock.
       bool fin = false;
 #ifdef VRPMS_ROUTE_PROF
       const unsigned long long pw0 = wall_clock64();
-      pset = pw0 - pt0;
 #endif
       while (!fin) {
 #ifdef VRPMS_ROUTE_PROF
-        ++pblk;
+        ++wblk;
 #endif
-        WTok blk[kBlk];
-        int dm_[kBlk];
-        bool smid[kBlk], saft[kBlk];
+        uint32_t cb[kBlk];
+        int db[kBlk], eb[kBlk];
         {
           uint32_t cp = q > 0 ? moved(q - 1) : 0u;
 #pragma unroll
           for (int i = 0; i < kBlk; ++i) {
             const int qq = q + i;
-            blk[i].c = qq < n ? moved(qq) : 0u;
-            blk[i].cp = cp;
-            cp = blk[i].c;
-          }
-#pragma unroll
-          for (int i = 0; i < kBlk; ++i) {
-            if constexpr (HM == 1) {
-              blk[i].ein = I.D(0, blk[i].cp, blk[i].c);
-              blk[i].eout = (int)legs[blk[i].c];
-              blk[i].eret = (int)legs[a.si.N + blk[i].c];
-            }
-            dm_[i] = dem[blk[i].c];
-            const int qq = q + i, qo = qq - dl;
-            smid[i] = qo >= 0 && qo < n && (int)T.rs[T.rid[qo]] == qo;
-            saft[i] = qq < n && (int)T.rs[T.rid[qq]] == qq;
+            const uint32_t at = qq < n ? T.at[map_src(mm, qq)] : 0u;
+            cb[i] = at & 0xffffu;
+            db[i] = (int)(at >> 16);
+            eb[i] = edge(cp, cb[i]);
+            cp = cb[i];
           }
         }
+        // route-start bits at the current tour's positions of the middle
+        // (q + i - dl) and of the rest (q + i), as 8-bit windows
+        const int bm = q - dl;
+        const uint64_t wm = bm >= 0 ? (((uint64_t)T.bits[(bm >> 5) + 1] << 32) | T.bits[bm >> 5]) >> (bm & 31)
+                                    : 0ull;
+        const uint64_t wa = (((uint64_t)T.bits[(q >> 5) + 1] << 32) | T.bits[q >> 5]) >> (q & 31);
         int adv = kBlk;
 #pragma unroll
         for (int i = 0; i < kBlk; ++i) {
@@ -663,45 +688,51 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
             adv = i;
             break;
           }
-          const uint32_t c = blk[i].c;
+          const uint32_t c = cb[i];
           // back in step at a route start of the current tour: the walk's
           // route is fresh there, or the customer there does not fit (a
           // separator would close the walk's route, not the tour's empty one)
-          const bool nofit = c != 0 && w.load + dm_[i] > cap0;
+          const bool nofit = c != 0 && w.load + db[i] > cap0;
           if (phase == 1 && qq >= bq0) {  // the middle: moved(qq) = A[qq - dl]
-            if (smid[i] && (w.prev == 0 || nofit)) {
-              if (w.prev != 0) close_tok(w);  // the token opens a route in both tours
+            if (((wm >> i) & 1u) && (w.prev == 0 || nofit)) {
+              if (w.prev != 0) close_rec(w, qq);  // the token opens a route in both tours
               w1 = w;
               r1e = T.rid[qq - dl];
               q1 = qq;
               fresh(w);
               phase = 2;
+              z2 = true;
+              zbase = Z2;
               adv = Z2 - q;  // the second zone starts fresh at Z2
               break;
             }
             if (qq == Z2) phase = 3;  // never back in step before the second end
           }
           if (phase >= 2 && qq > hi) {  // after both ends: moved(qq) = A[qq]
-            if (saft[i] && (w.prev == 0 || nofit)) {
-              if (w.prev != 0) close_tok(w);
+            if (((wa >> i) & 1u) && (w.prev == 0 || nofit)) {
+              if (w.prev != 0) close_rec(w, qq);
               r2e = T.rid[qq];
               fin = true;
               adv = i;
               break;
             }
           }
-          if (c == 0 || nofit) close_tok(w);
-          if (c) add_tok(w, blk[i], dm_[i]);
+          if (c == 0) {
+            close_rec(w, qq + 1);  // the separator ends the walk's route
+          } else {
+            if (nofit) close_rec(w, qq);
+            add(w, c, db[i], eb[i]);
+          }
 #ifdef VRPMS_ROUTE_PROF
           ++wtok;
 #endif
         }
         q += adv;
       }
+      if (q >= n) close_rec(w, n);  // the tour end closes the last route
 #ifdef VRPMS_ROUTE_PROF
       pwalk = wall_clock64() - pw0;
 #endif
-      if (q >= n) close_tok(w);  // the tour end closes the last route
       q2 = q;
       if (phase != 2) {  // one zone: routes r1s .. r2e - 1
         w1 = w;
@@ -742,10 +773,13 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
 #ifdef VRPMS_ROUTE_PROF
     const unsigned long long pt1 = wall_clock64();
     {
-      int mx = wtok, sm = wtok;
+      int mx = wtok, sm = wtok, bx = wblk;
+      unsigned long long wx = pwalk;
       for (int off = 32; off > 0; off >>= 1) {
         mx = max(mx, __shfl_xor(mx, off, 64));
         sm += __shfl_xor(sm, off, 64);
+        bx = max(bx, __shfl_xor(bx, off, 64));
+        wx = max(wx, (unsigned long long)__shfl_xor((long long)wx, off, 64));
       }
       pf[0] += pt1 - pt0;
       pf[2] += 1;
@@ -753,16 +787,8 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
       pf[4] += (unsigned long long)mx;
       pf[5] += (unsigned long long)sm;
       pf[6] += (unsigned long long)__popcll(__ballot(full));
-      unsigned long long wmx = pwalk, bmx = pblk, smx = pset;
-      for (int off = 32; off > 0; off >>= 1) {
-        wmx = max(wmx, (unsigned long long)__shfl_xor((long long)wmx, off, 64));
-        bmx = max(bmx, (unsigned long long)__shfl_xor((long long)bmx, off, 64));
-        smx = max(smx, (unsigned long long)__shfl_xor((long long)smx, off, 64));
-      }
-      pf[8] += wmx;
-      pf[9] += bmx;
-      pf[10] += smx;
-      pblk = 0;
+      pf[8] += wx;
+      pf[9] += (unsigned long long)bx;
     }
 #endif
     if (accept) {
@@ -770,128 +796,206 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
       mb.typ = (uint32_t)wave_bcast((int)m.typ, bl);
       mb.i = wave_bcast(m.i, bl);
       mb.j = wave_bcast(m.j, bl);
-      for (int q = lane; q < n; q += 64) B[q] = A[moved_index(q, mb)];
-      wave_sync();
-      uint16_t* t = A;
-      A = B;
-      B = t;
-      ck = k;
-      if (ck < bk) {
-        bk = ck;
-        for (int q = lane; q < n; q += 64) gbest[q] = A[q];
-      }
-      if (route_ok) {
-        // the accepted lane's zones, in positions of the new tour A
-        const int br1s = wave_bcast(r1s, bl), br1e = wave_bcast(r1e, bl);
-        const int br2s = wave_bcast(r2s, bl), br2e = wave_bcast(r2e, bl);
-        const int bP1 = wave_bcast(P1, bl), bZ2 = wave_bcast(Z2, bl);
-        const int bq1 = wave_bcast(q1, bl), bq2 = wave_bcast(q2, bl), bdl = wave_bcast(dl, bl);
-        const int bc1 = wave_bcast((int)c1, bl), bc2 = wave_bcast((int)c2, bl);
-        const int d1 = bc1 - (br1e - br1s), d2 = bc2 - (br2e - br2s);
-        const int R2 = R + d1 + d2;
-        if (R2 > RMAX || bc1 + bc2 > kRouteZoneMax) {
-          R = full_build();
-          route_ok = R >= 0;
-        } else {
-          // lane 0 re-walks the zones, recording their routes and positions
-          if (lane == 0) {
-            int zi = 0;
-            auto rec_zone = [&](int from, int to, int r0) {
-              Walk w;
-              fresh(w);
-              int start = from, rr = r0;
-              for (int q = from; q < to; ++q) {
-                const uint32_t c = tokA(q);
-#ifdef VRPMS_ROUTE_PROF
-                ++pf[7];
-#endif
-                if (closes(w, c)) {
-                  if (c == 0) {  // the separator ends this route: it belongs to it
-                    const bool cu = w.prev != 0;
-                    T.zd[zi] = close(w);
-                    T.zc[zi] = cu ? 1 : 0;
-                    T.zs[zi] = (uint16_t)start;
-                    T.rid2[q] = (uint8_t)rr;
-                    ++zi;
-                    ++rr;
-                    start = q + 1;
-                    continue;
-                  }
-                  const bool cu = w.prev != 0;
-                  T.zd[zi] = close(w);
-                  T.zc[zi] = cu ? 1 : 0;
-                  T.zs[zi] = (uint16_t)start;
-                  ++zi;
-                  ++rr;
-                  start = q;
-                }
-                add(w, c);
-                T.rid2[q] = (uint8_t)rr;
-              }
-              if (w.prev != 0 || to >= n) {  // resync right after a closed route needs none
-                const bool cu = w.prev != 0;
-                T.zd[zi] = close(w);
-                T.zc[zi] = cu ? 1 : 0;
-                T.zs[zi] = (uint16_t)start;
-                ++zi;
-              }
-            };
-            rec_zone(bP1, bq1, br1s);
-            if (bq1 < bq2) rec_zone(bZ2, bq2, br2s + d1);
-          }
-          // the routes: before the first zone, the first zone's, the middle's
-          // (shifted by dl positions), the second zone's, the rest
-          uint32_t vd[4], vs[4], vc[4];
+      const MoveMap mmb = move_map(mb);
+      const bool regs = n <= 64 * kTourRegs;
+      // the accepted lane's zones, in positions of the new tour
+      const int br1s = wave_bcast(r1s, bl), br1e = wave_bcast(r1e, bl);
+      const int br2s = wave_bcast(r2s, bl), br2e = wave_bcast(r2e, bl);
+      const int bP1 = wave_bcast(P1, bl), bZ2 = wave_bcast(Z2, bl);
+      const int bq1 = wave_bcast(q1, bl), bq2 = wave_bcast(q2, bl), bdl = wave_bcast(dl, bl);
+      const int bc1 = wave_bcast((int)c1, bl), bc2 = wave_bcast((int)c2, bl);
+      const bool bovf = wave_bcast(zovf ? 1 : 0, bl) != 0 || bc1 + bc2 > 64;
+      uint64_t bm[4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int rr = lane + 64 * i;
-            if (rr >= R2) break;
-            int src = -1, sh = 0;  // -1: a recorded zone route (read after the sync)
-            if (rr < br1s) src = rr;
-            else if (rr < br1s + bc1) src = -1;
-            else if (rr < br2s + d1) src = rr - d1, sh = bdl;
-            else if (rr >= br2s + d1 + bc2) src = rr - d1 - d2;
-            vd[i] = vs[i] = vc[i] = 0;
-            if (src >= 0) {
-              vd[i] = T.dur[src];
-              vs[i] = (uint32_t)((int)T.rs[src] + sh);
-              vc[i] = T.cus[src];
-            }
-          }
-          // the positions: unchanged before P1, recorded in the zones,
-          // shifted in the middle, renumbered after
-          for (int q = lane; q < n; q += 64) {
-            if (q < bP1) T.rid2[q] = T.rid[q];
-            else if (q >= bq1 && q < bZ2) T.rid2[q] = (uint8_t)(T.rid[q - bdl] + d1);
-            else if (q >= bq2) T.rid2[q] = (uint8_t)(T.rid[q] + d1 + d2);
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t lo = (uint32_t)wave_bcast((int)(uint32_t)zm[i], bl);
+        const uint32_t hi = (uint32_t)wave_bcast((int)(uint32_t)(zm[i] >> 32), bl);
+        bm[i] = ((uint64_t)hi << 32) | lo;
+      }
+      const int d1 = bc1 - (br1e - br1s), d2 = bc2 - (br2e - br2s);
+      const int R2 = R + d1 + d2;
+      const bool incremental = route_ok && regs && R2 <= RMAX;
+#ifdef VRPMS_ROUTE_PROF
+      pf[7] += incremental ? (bovf ? 1 : 0) : 1000000;
+#endif
+      // route starts of zone z (bits over its positions) at or before offset off
+      auto starts_upto = [&](int z, int off) {
+        const uint64_t lo = bm[2 * z], hi = bm[2 * z + 1];
+        if (off < 64) return __popcll(lo & (off == 63 ? ~0ull : ((2ull << off) - 1ull)));
+        return __popcll(lo) + __popcll(hi & (off >= 127 ? ~0ull : ((2ull << (off - 64)) - 1ull)));
+      };
+      // apply the move in place: each lane holds its positions' new entries
+      // (and, incrementally, their new route ids) in registers over one sync
+      if (regs) {
+        {
+          uint32_t v[kTourRegs];
+#pragma unroll
+          for (int i = 0; i < kTourRegs; ++i) {
+            const int q = lane + 64 * i;
+            v[i] = q < n ? T.at[map_src(mmb, q)] : 0u;
           }
           wave_sync();
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int rr = lane + 64 * i;
-            if (rr >= R2) break;
-            int zrow = -1;
-            if (rr >= br1s && rr < br1s + bc1) zrow = rr - br1s;
-            else if (rr >= br2s + d1 && rr < br2s + d1 + bc2) zrow = bc1 + (rr - br2s - d1);
-            if (zrow >= 0) {
-              vd[i] = T.zd[zrow];
-              vs[i] = T.zs[zrow];
-              vc[i] = T.zc[zrow];
+          for (int i = 0; i < kTourRegs; ++i) {
+            const int q = lane + 64 * i;
+            if (q < n) T.at[q] = v[i];
+          }
+        }
+        if (incremental) {
+          uint32_t rv[kTourRegs];
+#pragma unroll
+          for (int i = 0; i < kTourRegs; ++i) {
+            const int q = lane + 64 * i;
+            rv[i] = 0;
+            if (q >= n) continue;
+            if (q < bP1) rv[i] = T.rid[q];
+            else if (q < bq1) rv[i] = bovf ? 0u : (uint32_t)(br1s + starts_upto(0, q - bP1) - 1);
+            else if (q < bZ2) rv[i] = (uint32_t)((int)T.rid[q - bdl] + d1);  // the middle, shifted
+            else if (q < bq2) rv[i] = bovf ? 0u : (uint32_t)(br2s + d1 + starts_upto(1, q - bZ2) - 1);
+            else rv[i] = (uint32_t)((int)T.rid[q] + d1 + d2);
+          }
+          wave_sync();
+#pragma unroll
+          for (int i = 0; i < kTourRegs; ++i) {
+            const int q = lane + 64 * i;
+            if (q < n) T.rid[q] = (uint8_t)rv[i];
+          }
+          if (bovf) {
+            // one lane re-walks the zones of the new tour, writing their
+            // positions' route ids and their routes into scratch (the
+            // derived tables smx / lnea / lnb, rebuilt by derive below)
+            wave_sync();
+            if (lane == 0) {
+              int zi = 0;
+              auto rec = [&](int from, int to, int r0) {
+                Walk w;
+                fresh(w);
+                int start = from, rr = r0;
+                auto put = [&](int next) {
+                  const bool cu = w.prev != 0;
+                  T.smx[zi] = close(w);
+                  T.lnea[zi] = (uint32_t)start;
+                  T.lnb[zi] = cu ? 1 : 0;
+                  ++zi;
+                  ++rr;
+                  start = next;
+                };
+                for (int q = from; q < to; ++q) {
+                  const uint32_t at = T.at[q], c = at & 0xffffu;
+                  const int d = (int)(at >> 16);
+                  if (c == 0) {  // the separator ends this route: it belongs to it
+                    T.rid[q] = (uint8_t)rr;
+                    put(q + 1);
+                    continue;
+                  }
+                  if (w.load + d > cap0) put(q);
+                  add(w, c, d, w.prev ? edge(w.prev, c) : 0);
+                  T.rid[q] = (uint8_t)rr;
+                }
+                if (w.prev != 0 || to >= n) put(to);  // back in step right after a closure: none
+              };
+              rec(bP1, bq1, br1s);
+              if (bq1 < bq2) rec(bZ2, bq2, br2s + d1);
             }
+          }
+        }
+        wave_sync();
+      } else {  // tours too long for registers: stage the new tour in HBM (the cur row)
+        uint16_t* gscr = a.cur + (int64_t)chain * n;
+        for (int q = lane; q < n; q += 64) gscr[q] = (uint16_t)tokA(map_src(mmb, q));
+        __threadfence_block();
+        wave_sync();
+        for (int q = lane; q < n; q += 64) {
+          const uint32_t c = gscr[q];
+          T.at[q] = c | ((uint32_t)dem[c] << 16);
+        }
+        wave_sync();
+      }
+      ck = k;
+      if (ck < bk) {
+        bk = ck;
+        for (int q = lane; q < n; q += 64) gbest[q] = (uint16_t)tokA(q);
+      }
+      if (incremental) {
+        // the routes: before the first zone, the first zone's, the middle's
+        // (shifted by dl positions), the second zone's, the rest
+        uint32_t vd[4], vs[4], vc[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int rr = lane + 64 * i;
+          vd[i] = vs[i] = vc[i] = 0;
+          if (rr >= R2) continue;
+          int src = -1, sh = 0, zr = -1;  // zr: scratch row of a re-walked zone route
+          if (rr < br1s) src = rr;
+          else if (rr < br1s + bc1) zr = rr - br1s;
+          else if (rr < br2s + d1) src = rr - d1, sh = bdl;
+          else if (rr < br2s + d1 + bc2) zr = bc1 + (rr - br2s - d1);
+          else src = rr - d1 - d2;
+          if (src >= 0) {
+            vd[i] = T.dur[src];
+            vs[i] = (uint32_t)((int)T.rs[src] + sh);
+            vc[i] = T.cus[src];
+          } else if (bovf) {
+            vd[i] = T.smx[zr];
+            vs[i] = T.lnea[zr];
+            vc[i] = (uint32_t)T.lnb[zr];
+          } else {
+            vs[i] = 0xffffffffu;  // a zone route: start from the bits, duration walked below
+          }
+        }
+        wave_sync();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int rr = lane + 64 * i;
+          if (rr < R2 && vs[i] != 0xffffffffu) {
             T.dur[rr] = vd[i];
             T.rs[rr] = (uint16_t)vs[i];
             T.cus[rr] = (uint8_t)vc[i];
           }
-          if (lane == 0) T.rs[R2] = (uint16_t)n;
-          uint8_t* tr = T.rid;
-          T.rid = T.rid2;
-          T.rid2 = tr;
-          R = R2;
-          wave_sync();
-          derive(R);
         }
+        if (!bovf) {
+          // zone route starts: the set bits below each zone's length, in order
+#pragma unroll
+          for (int z = 0; z < 2; ++z) {
+            const int len = z ? bq2 - bZ2 : bq1 - bP1, base = z ? bZ2 : bP1;
+            const int r0 = z ? br2s + d1 : br1s;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int off = 64 * h + lane;
+              if (off < len && ((bm[2 * z + h] >> lane) & 1ull))
+                T.rs[r0 + starts_upto(z, off) - 1] = (uint16_t)(base + off);
+            }
+          }
+        }
+        if (lane == 0) T.rs[R2] = (uint16_t)n;
+        wave_sync();
+        if (!bovf) {
+          // one lane per zone route walks it (a single route: no closure
+          // before its end) for its duration and whether it serves anyone
+          const int nz = bc1 + bc2;
+          if (lane < nz) {
+            const int rr = lane < bc1 ? br1s + lane : br2s + d1 + (lane - bc1);
+            const int from = T.rs[rr], to = T.rs[rr + 1];
+            Walk w;
+            fresh(w);
+            for (int q = from; q < to; ++q) {
+              const uint32_t at = T.at[q], c = at & 0xffffu;
+              if (c == 0) break;  // a separator ends the route
+              add(w, c, (int)(at >> 16), w.prev ? edge(w.prev, c) : 0);
+            }
+            const bool cu = w.prev != 0;
+            T.dur[rr] = close(w);
+            T.cus[rr] = cu ? 1 : 0;
+          }
+          wave_sync();
+        }
+        R = R2;
+        derive(R);
+        build_bits();
+      } else {
+        R = full_build();
+        route_ok = R >= 0;
       }
-      wave_sync();
     }
 #ifdef VRPMS_ROUTE_PROF
     pf[1] += wall_clock64() - pt1;
@@ -899,11 +1003,12 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
     invT = invT * a.inv_alpha;
   }
   uint16_t* gout = a.cur + (int64_t)chain * n;
-  for (int q = lane; q < n; q += 64) gout[q] = A[q];
+  for (int q = lane; q < n; q += 64) gout[q] = (uint16_t)tokA(q);
   if (lane == 0) {
     a.cur_key[chain] = ck;
     a.best_key[chain] = bk;
 #ifdef VRPMS_ROUTE_PROF
+    pf[11] = wall_clock64() - pk0;
     if (chain < 8192)
       for (int i = 0; i < 12; ++i) g_route_prof[12 * chain + i] += pf[i];
 #endif
@@ -1817,7 +1922,8 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
   // exchangeable vehicles: one capacity, one start time, every demand fits
   const Instance& in = ctx->inst;
   if (p->window > 0 && in.problem == VRPMS_CVRP && in.uniform_cap &&
-      in.min_start == in.max_start && in.max_dem <= in.cap0 && route_max(in.K) <= 255 &&
+      in.min_start == in.max_start && in.max_dem <= in.cap0 && in.max_dem <= 65535 &&
+      route_max(in.K) <= 255 &&
       n <= 65535 && ctx->opt_sa_route != 2) {
     const size_t npad = ((size_t)n + 7) & ~(size_t)7;
     const size_t wbytes = ((size_t)route_wave_bytes((int)npad, in.K) + 15) & ~(size_t)15;
