@@ -5,6 +5,9 @@
 
 Writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (as produced)
+  profiles/<tag>_kernel_grid.csv    mean duration per (kernel, grid size) from the kernel
+                                    trace: the stats average mixes the headline launch
+                                    with the small launches of the other legs
   profiles/<tag>_pmc.json           per-counter mean per dispatch of the kernel, plus
                                     HBM traffic per launch: FETCH_SIZE x 2 (gfx950 reports
                                     half the bytes of a wide coalesced read,
@@ -38,6 +41,22 @@ def pmc_means(kernel):
     return {k: sum(v) / len(v) for k, v in agg.items()}, meta
 
 
+def per_grid(tag):
+    traces = glob.glob(os.path.join(OUT, "prof", "*kernel_trace.csv"))
+    if not traces:
+        return
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(traces[0])):
+        agg[(r["Kernel_Name"], int(r["Grid_Size_X"]), int(r["Workgroup_Size_X"]))].append(
+            int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    rows = sorted(agg.items(), key=lambda kv: -sum(kv[1]))
+    with open(os.path.join(PROF, f"{tag}_kernel_grid.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Name", "Grid_Size_X", "Workgroup_Size_X", "Calls", "AverageNs", "MinNs", "MaxNs"])
+        for (name, grid, wg), v in rows:
+            w.writerow([name, grid, wg, len(v), f"{sum(v) / len(v):.1f}", min(v), max(v)])
+
+
 def main():
     tag = sys.argv[1]
     kernel = sys.argv[2] if len(sys.argv) > 2 else "eval_cvrp_words"
@@ -45,6 +64,7 @@ def main():
     stats = glob.glob(os.path.join(OUT, "prof", "*kernel_stats.csv"))
     if stats:
         shutil.copy(stats[0], os.path.join(PROF, f"{tag}_kernel_stats.csv"))
+    per_grid(tag)
     means, meta = pmc_means(kernel)
     rec = {"tag": tag, "kernel_filter": kernel, **meta, "counters_mean_per_dispatch": means}
     if "FETCH_SIZE" in means and "WRITE_SIZE" in means:
