@@ -152,7 +152,9 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
     0.5 to 0.002 x the mean edge spread over the wall-time budget by
     _TimedCooling) on the GPU -- `chains` chains with elite migration every 5
     epochs (across ranks when N > 1) -- and on the host cores
-    (oracle/oracle_c.c, one chain per OpenMP thread).  Both legs run until
+    (oracle/oracle_c.c oracle_sa_run_resync, one chain per OpenMP thread,
+    each candidate priced by walking only the span the move can change and
+    jumping over unchanged routes -- the same trajectories as the full walk).  Both legs run until
     `seconds` of wall time are spent.  Both legs search giant tours with
     n_sep A10 route separators (default K - 1, the front-end's VRP SA), so
     the moves place route boundaries too; `window` > 0 samples A11 windowed
@@ -225,7 +227,8 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
                 break
             coracle.sa_run(inst.durations, cur, best, bk, steps, float(cool.inv_t), float(inv_a),
                            1, step, inst.demand, inst.capacities, inst.start_times,
-                           threads=threads, window=window, window_types=window_types)
+                           threads=threads, window=window, window_types=window_types,
+                           resync=True)
             cool.advance(steps, inv_a)
             step += steps
         cpu_wall = cool.elapsed()
@@ -233,7 +236,8 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
         out["cpu"] = {"chains": threads, "cores": threads, "steps_per_chain": step,
                       "wall_s": cpu_wall, "unvisited": ck >> 56,
                       "duration_sum": (ck >> 28) & (2**28 - 1),
-                      "kind": "port (oracle/oracle_c.c oracle_sa_run)"}
+                      "kind": "port (oracle/oracle_c.c oracle_sa_run_resync: "
+                              "candidates priced by walking only what the move changes)"}
         g, c = out["gpu"], out["cpu"]
         ok = g["unvisited"] == 0 and c["unvisited"] == 0 and c["duration_sum"]
         out["gap"] = (g["duration_sum"] - c["duration_sum"]) / c["duration_sum"] if ok else None

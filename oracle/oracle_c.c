@@ -14,6 +14,7 @@
  * keeps every value inside int32 for the device.
  */
 #include <math.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -540,4 +541,297 @@ int oracle_max_threads(void) {
 #else
   return 1;
 #endif
+}
+
+/* ------------------------------------------------------------------------
+ * oracle_sa_run_resync: the same SA as oracle_sa_run (same streams, same
+ * moves, same keys, so the same trajectories bit for bit), with each
+ * candidate priced by walking only the part of the moved tour whose split
+ * can differ -- the CPU baseline of the quality leg, so that the host side
+ * is not handicapped by full re-walks while the GPU prices route-locally.
+ *
+ * On a uniform fleet (one capacity, one start time) the greedy split's
+ * future from a position depends on the state (load, t, prev) only, not on
+ * which vehicle is driving.  Tokens before lo = min(i, j) are unchanged, so
+ * the walk starts from the current tour's state after lo - 1.  Where the
+ * moved tour reads a contiguous run of the current tour (src(q) = q + off),
+ * a walk state equal to the current state at src(q) stays equal to the end
+ * of the run: the walk jumps there, adding the routes the current tour
+ * closes in between (prefix sums of route durations, a sparse table for
+ * their maximum).  A walk that would reach the K-th vehicle, a current tour
+ * that exhausts the fleet, a non-uniform fleet and TSP fall back to the full
+ * walk (tour_key), so every key equals tour_key's.
+ * ---------------------------------------------------------------------- */
+typedef struct {
+  int64_t load, t, s, mx;
+  int prev, k;
+} walk_t;
+
+typedef struct {
+  int n, K, levels;
+  int64_t *load, *t; /* after-state of position q */
+  int *prev, *k;     /* k = routes closed after q */
+  int* lastcust;     /* last position <= q holding a customer (-1: none) */
+  int* pos_cl;       /* position of the token that made closure r */
+  int kpos;          /* position of the closure that used the K-th vehicle (n: none) */
+  int64_t *cd;       /* duration of closure r (0: empty route) */
+  int64_t *cs;       /* cs[r] = sum of cd[0..r-1] */
+  int64_t *sp;       /* sparse table [levels][K + 1] of cd maxima */
+  int alive;         /* the current tour leaves no customer unvisited */
+} split_t;
+
+static int64_t sp_max(const split_t* S, int a, int b) { /* max cd[a..b], 0 when empty */
+  if (b < a) return 0;
+  int l = 31 - __builtin_clz((unsigned)(b - a + 1));
+  const int64_t* row = S->sp + (int64_t)l * (S->K + 1);
+  int64_t x = row[a], y = row[b - (1 << l) + 1];
+  return x > y ? x : y;
+}
+
+static inline void close_route(const inst_t* I, walk_t* w) {
+  if (w->prev != 0) {
+    int64_t rd = w->t + edge(I->D, I->H, I->N, w->t, w->prev, 0) - I->st[w->k];
+    w->s += rd;
+    if (rd > w->mx) w->mx = rd;
+  }
+  ++w->k;
+  if (w->k < I->K) {
+    w->load = 0;
+    w->t = I->st[w->k];
+    w->prev = 0;
+  }
+}
+
+/* one token of the greedy split (tour_key's loop body); returns 0 when a
+ * customer finds the fleet exhausted (the caller then prices the move in
+ * full).  Once k >= K the state is stale and only separators may follow. */
+static inline int walk_token(const inst_t* I, walk_t* w, int x) {
+  if (x == 0) {
+    if (w->k < I->K) close_route(I, w);
+    return 1;
+  }
+  while (w->k < I->K && w->load + I->dem[x] > I->cap[w->k]) close_route(I, w);
+  if (w->k >= I->K) return 0;
+  w->t += edge(I->D, I->H, I->N, w->t, w->prev, x);
+  w->load += I->dem[x];
+  w->prev = x;
+  return 1;
+}
+
+static uint64_t walk_finish(const inst_t* I, walk_t* w) {
+  if (w->k < I->K && w->prev != 0) {
+    int64_t rd = w->t + edge(I->D, I->H, I->N, w->t, w->prev, 0) - I->st[w->k];
+    w->s += rd;
+    if (rd > w->mx) w->mx = rd;
+  }
+  return I->objective ? pack_key(0, w->mx, w->s) : pack_key(0, w->s, w->mx);
+}
+
+static void split_build(const inst_t* I, const uint16_t* T, split_t* S) {
+  walk_t w = {0, I->K ? I->st[0] : 0, 0, 0, 0, 0};
+  int last = -1;
+  S->alive = 1;
+  S->kpos = S->n;
+  for (int q = 0; q < S->n; ++q) {
+    int k0 = w.k;
+    int64_t s0 = w.s;
+    if (!walk_token(I, &w, T[q])) {
+      S->alive = 0;
+      return;
+    }
+    /* closures k0..w.k-1: the first one carries the route's duration, later
+     * ones (oversize demand) are empty routes */
+    for (int r = k0; r < w.k; ++r) {
+      S->cd[r] = r == k0 ? w.s - s0 : 0;
+      S->pos_cl[r] = q;
+    }
+    if (k0 < I->K && w.k >= I->K) S->kpos = q;
+    if (T[q] != 0) last = q;
+    S->lastcust[q] = last;
+    S->load[q] = w.load;
+    S->t[q] = w.t;
+    S->prev[q] = w.prev;
+    S->k[q] = w.k;
+  }
+  const int ncl = w.k;
+  S->cs[0] = 0;
+  for (int r = 0; r < ncl; ++r) S->cs[r + 1] = S->cs[r] + S->cd[r];
+  for (int r = 0; r < ncl; ++r) S->sp[r] = S->cd[r];
+  for (int l = 1; l < S->levels; ++l) {
+    int64_t* row = S->sp + (int64_t)l * (S->K + 1);
+    const int64_t* pr = row - (S->K + 1);
+    for (int r = 0; r + (1 << l) <= ncl; ++r) {
+      int64_t x = pr[r], y = pr[r + (1 << (l - 1))];
+      row[r] = x > y ? x : y;
+    }
+  }
+}
+
+/* Jump the walk, whose state equals the current tour's after position a,
+ * to position b (> a) of the current tour, adding the routes it closes in
+ * between.  Returns the position reached (b, or the last one before the
+ * current tour used its K-th vehicle), or -1 when the walk would leave a
+ * customer unvisited there. */
+static inline int walk_jump(const split_t* S, walk_t* w, int a, int b, int K) {
+  if (S->k[b] >= K) b = S->kpos - 1; /* past kpos the current state is stale */
+  if (b <= a) return a;
+  const int r0 = S->k[a], r1 = S->k[b], room = K - w->k;
+  int rl = r1; /* closures r0..rl-1 happen in the walk */
+  if (r1 - r0 >= room) {
+    /* the walk uses its K-th vehicle at closure r0 + room - 1: only
+     * separators may follow it up to b */
+    rl = r0 + room;
+    if (S->lastcust[b] >= S->pos_cl[rl - 1]) return -1;
+  }
+  w->s += S->cs[rl] - S->cs[r0];
+  int64_t m = sp_max(S, r0, rl - 1);
+  if (m > w->mx) w->mx = m;
+  w->k += rl - r0;
+  w->load = S->load[b];
+  w->t = S->t[b];
+  w->prev = S->prev[b];
+  return b;
+}
+
+/* `hopeless`: the current tour serves everyone and a key with unvisited
+ * customers can never be accepted at this temperature (dp >= 2^28 gives a
+ * zero threshold), so such a move is given the largest key instead of being
+ * counted exactly -- it cannot win over a feasible move, and a winner that
+ * is infeasible is rejected either way (as on the device). */
+static uint64_t resync_key(const inst_t* I, const uint16_t* T, int n, const move_t* m,
+                           const split_t* S, int hopeless) {
+  int i = m->i, j = m->j;
+  int lo = i < j ? i : j;
+  /* runs of the moved tour that read the current tour contiguously:
+   * (start, end, offset), at most two */
+  int rs[2], re[2], ro[2], nr = 0;
+  if (m->typ == 0) {
+    if (i + 1 <= j - 1) { rs[nr] = i + 1; re[nr] = j - 1; ro[nr++] = 0; }
+    if (j + 1 <= n - 1) { rs[nr] = j + 1; re[nr] = n - 1; ro[nr++] = 0; }
+  } else if (m->typ == 1) {
+    if (j + 1 <= n - 1) { rs[nr] = j + 1; re[nr] = n - 1; ro[nr++] = 0; }
+  } else if (i < j) {
+    rs[nr] = i; re[nr] = j - 1; ro[nr++] = 1;
+    if (j + 1 <= n - 1) { rs[nr] = j + 1; re[nr] = n - 1; ro[nr++] = 0; }
+  } else {
+    rs[nr] = j + 1; re[nr] = i; ro[nr++] = -1;
+    if (i + 1 <= n - 1) { rs[nr] = i + 1; re[nr] = n - 1; ro[nr++] = 0; }
+  }
+  walk_t w;
+  if (lo == 0 || S->k[lo - 1] >= I->K) {
+    if (lo) return tour_key(I, T, n, m); /* (a current tour that ends in exhaustion) */
+    w.load = 0; w.t = I->st[0]; w.prev = 0; w.k = 0; w.s = 0; w.mx = 0;
+  } else {
+    int a = lo - 1, r = S->k[a];
+    w.load = S->load[a]; w.t = S->t[a]; w.prev = S->prev[a]; w.k = r;
+    w.s = S->cs[r];
+    w.mx = sp_max(S, 0, r - 1);
+  }
+  int run = 0;
+  for (int q = lo; q < n; ++q) {
+    if (!walk_token(I, &w, T[moved_index(q, m)]))
+      return hopeless ? ~0ull : tour_key(I, T, n, m);
+    while (run < nr && re[run] < q) ++run;
+    if (run < nr && q >= rs[run] && q < re[run] && w.k < I->K) {
+      const int c = q + ro[run];
+      if (S->k[c] < I->K && w.load == S->load[c] && w.t == S->t[c] && w.prev == S->prev[c]) {
+        const int b = walk_jump(S, &w, c, re[run] + ro[run], I->K);
+        if (b < 0) return hopeless ? ~0ull : tour_key(I, T, n, m);
+        q = b - ro[run];
+      }
+    }
+  }
+  return walk_finish(I, &w);
+}
+
+int oracle_sa_run_resync(int problem, const int32_t* D, int H, int N, const int32_t* dem,
+                         const int32_t* cap, const int32_t* st, int K, int objective,
+                         uint16_t* cur, uint64_t* cur_key, uint16_t* best, uint64_t* best_key,
+                         int chains, int n, int steps, float inv_t0, float inv_alpha,
+                         uint64_t seed, uint64_t step0, int window, uint32_t window_types,
+                         int threads) {
+  int uniform = problem == 1 && K > 0;
+  for (int k = 1; uniform && k < K; ++k) uniform = cap[k] == cap[0] && st[k] == st[0];
+  if (!uniform || n < 2)
+    return oracle_sa_run(problem, D, H, N, dem, cap, st, K, objective, cur, cur_key, best,
+                         best_key, chains, n, steps, inv_t0, inv_alpha, seed, step0, window,
+                         window_types, threads);
+  inst_t I = {problem, H, N, K, objective, D, dem, cap, st};
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  int levels = 1;
+  while ((1 << levels) <= K) ++levels;
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel
+#endif
+  {
+    split_t S;
+    S.n = n;
+    S.K = K;
+    S.levels = levels;
+    S.load = (int64_t*)malloc(sizeof(int64_t) * (size_t)n);
+    S.t = (int64_t*)malloc(sizeof(int64_t) * (size_t)n);
+    S.prev = (int*)malloc(sizeof(int) * (size_t)n);
+    S.k = (int*)malloc(sizeof(int) * (size_t)n);
+    S.lastcust = (int*)malloc(sizeof(int) * (size_t)n);
+    S.pos_cl = (int*)malloc(sizeof(int) * (size_t)(K + 1));
+    S.cd = (int64_t*)malloc(sizeof(int64_t) * (size_t)(K + 1));
+    S.cs = (int64_t*)malloc(sizeof(int64_t) * (size_t)(K + 2));
+    S.sp = (int64_t*)malloc(sizeof(int64_t) * (size_t)levels * (size_t)(K + 1));
+    uint16_t* tmp = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)n);
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+    for (int c = 0; c < chains; ++c) {
+      uint16_t* A = cur + (int64_t)c * n;
+      uint16_t* Bst = best + (int64_t)c * n;
+      uint64_t ck = tour_key(&I, A, n, NULL), bk = best_key[c];
+      if (ck < bk) {
+        bk = ck;
+        memcpy(Bst, A, (size_t)n * 2);
+      }
+      split_build(&I, A, &S);
+      float invT = inv_t0;
+      for (int s = 0; s < steps; ++s) {
+        uint64_t step = step0 + (uint64_t)s;
+        uint64_t kbest = ~0ull;
+        move_t mbest = {0, 0, 0};
+        uint32_t wbest = 0;
+        const int hopeless = (ck >> 56) == 0 && accept_threshold(1u << 28, invT) == 0;
+        for (int lane = 0; lane < 64; ++lane) {
+          u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)c, (uint32_t)lane,
+                           k0, k1);
+          move_t m = decode_move_window(r.x, r.y, r.z, n, window, window_types);
+          uint64_t kk = S.alive ? resync_key(&I, A, n, &m, &S, hopeless) : tour_key(&I, A, n, &m);
+          if (kk < kbest) {
+            kbest = kk;
+            mbest = m;
+            wbest = r.w;
+          }
+        }
+        int acc = kbest <= ck;
+        if (!acc) {
+          uint64_t d = (kbest >> 28) - (ck >> 28);
+          uint32_t dp = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
+          acc = (wbest >> 8) < accept_threshold(dp, invT);
+        }
+        if (acc) {
+          for (int q = 0; q < n; ++q) tmp[q] = A[moved_index(q, &mbest)];
+          memcpy(A, tmp, (size_t)n * 2);
+          ck = kbest;
+          split_build(&I, A, &S);
+          if (ck < bk) {
+            bk = ck;
+            memcpy(Bst, A, (size_t)n * 2);
+          }
+        }
+        invT = invT * inv_alpha;
+      }
+      cur_key[c] = ck;
+      best_key[c] = bk;
+    }
+    free(S.load); free(S.t); free(S.prev); free(S.k); free(S.lastcust); free(S.pos_cl);
+    free(S.cd); free(S.cs); free(S.sp); free(tmp);
+  }
+  return 0;
 }

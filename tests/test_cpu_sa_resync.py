@@ -1,0 +1,75 @@
+"""oracle_sa_run_resync (the quality leg's CPU baseline) against the full-walk
+oracle_sa_run: same streams and moves, so cur / best tours and keys must be
+equal bit for bit on every instance shape the quality sweep and the front-end
+use (X-1000 windowed, CVRP-100 with random separators, TD-200, full-range
+moves, a tight fleet that exhausts, a non-uniform fleet that falls back)."""
+import numpy as np
+import pytest
+
+from oracle import coracle, pool, spec
+from vrpms_amd import synth
+
+
+def _starts(inst, chains, n_sep, start, seed):
+    rows = []
+    for c in range(chains):
+        if start == "pack":
+            p = pool.philox_tour(inst.n, seed, c)
+            rows.append(spec.pack_separators(p, n_sep, inst.demand, inst.capacities))
+        else:
+            rows.append(pool.philox_tour(inst.n, seed, c, n_sep=n_sep))
+    return np.array(rows, dtype=np.uint16)
+
+
+def _both(inst, P, steps, inv_t0, inv_a, seed, window=0, types=0, step0=0):
+    out = []
+    for resync in (False, True):
+        cur, best = P.copy(), P.copy()
+        bk = np.full(P.shape[0], 2**64 - 1, dtype=np.uint64)
+        ck = coracle.sa_run(inst.durations, cur, best, bk, steps, inv_t0, inv_a, seed, step0,
+                            inst.demand, inst.capacities, inst.start_times, threads=4,
+                            window=window, window_types=types, resync=resync)
+        out.append((cur, best, bk, ck))
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
+    return out[1]
+
+
+@pytest.mark.parametrize("types", [2, 0])
+def test_resync_x1000_windowed(types):
+    inst = synth.x_style(1000, seed=1)
+    P = _starts(inst, 4, inst.K - 1, "pack", 3)
+    edge = float(np.asarray(inst.durations)[np.asarray(inst.durations) > 0].mean())
+    cur, _, bk, _ = _both(inst, P, 300, 1 / (0.5 * edge), 1 / 0.995, 9, window=32, types=types)
+    assert (bk >> np.uint64(56) == 0).all()
+
+
+def test_resync_cvrp100_random_separators_full_range():
+    inst = synth.cvrp(100, 8, seed=2)
+    P = _starts(inst, 6, inst.K - 1, "random", 5)
+    _both(inst, P, 400, 1 / 150.0, 1 / 0.99, 4)
+
+
+def test_resync_td200_windowed():
+    inst = synth.td_cvrp(200, 16, seed=0)
+    P = _starts(inst, 4, inst.K - 1, "pack", 1)
+    _both(inst, P, 200, 1 / 120.0, 1 / 0.99, 7, window=16, types=0, step0=13)
+
+
+def test_resync_tight_fleet_and_plain_giant_tours():
+    # slack 1.0: the fleet is barely enough, walks meet the K-th vehicle
+    inst = synth.cvrp(60, 6, seed=3, slack=1.0)
+    P = _starts(inst, 6, 0, "random", 2)
+    _both(inst, P, 300, 1 / 60.0, 1 / 0.99, 11)
+    P = _starts(inst, 6, inst.K - 1, "random", 2)
+    _both(inst, P, 300, 1 / 60.0, 1 / 0.99, 12)
+
+
+def test_resync_nonuniform_fleet_falls_back():
+    inst = synth.cvrp(40, 4, seed=4)
+    caps = np.asarray(inst.capacities).copy()
+    caps[1] += 7
+    inst = inst._replace(capacities=caps) if hasattr(inst, "_replace") else inst
+    if hasattr(inst, "_replace"):
+        P = _starts(inst, 3, inst.K - 1, "random", 6)
+        _both(inst, P, 100, 1 / 60.0, 1 / 0.99, 3)
