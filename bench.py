@@ -146,7 +146,8 @@ class _TimedCooling:
 
 
 def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label="cvrp100_k8 seed 0",
-            gpu_seed=None, n_sep=None, window=0, window_types=0, start="random"):
+            gpu_seed=None, n_sep=None, window=0, window_types=0, start="random", moves=64,
+            cpu_moves=64):
     """Best-cost gap at fixed wall time (the metric's second half): the same SA
     (Philox streams, 64 sampled moves per step, geometric cooling from
     0.5 to 0.002 x the mean edge spread over the wall-time budget by
@@ -160,7 +161,9 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
     the moves place route boundaries too; `window` > 0 samples A11 windowed
     moves of the A12 types `window_types`, and `start` places the separators
     of the start tours ("random", "greedy": the greedy split's route
-    boundaries, "pack": first-fit routes -- large instances).  gap = (gpu - cpu) / cpu on the
+    boundaries, "pack": first-fit routes -- large instances).  `moves` is the
+    GPU leg's move sample per step (64 W on W wavefronts per chain, at about
+    the per-step latency of one), `cpu_moves` the host leg's.  gap = (gpu - cpu) / cpu on the
     objective key's primary term (durationSum) with unvisited == 0."""
     import torch
     from vrpms_amd import islands, runners
@@ -169,43 +172,44 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
     dev = ctx.dev
     edge = runners.typical_edge(inst.durations)
     t0, t_end = 0.5 * edge, 0.002 * edge
-    warm = runners.SARunner(ctx, n, chains=chains, total_steps=1000, durations=inst.durations,
-                            n_sep=n_sep, window=window, window_types=window_types, start=start)
-    warm.epoch(20)                       # first launch: code object load, LDS setup
-    torch.cuda.synchronize(dev)
-    del warm
-    seed = (1000 + rank) if gpu_seed is None else gpu_seed
-    r = runners.SARunner(ctx, n, chains=chains, seed=seed, total_steps=1000,
-                         durations=inst.durations, t0=t0, t_end=t_end, n_sep=n_sep,
-                         window=window, window_types=window_types, start=start)
-    if world > 1:
-        dist.barrier()
-    cool = _TimedCooling(seconds, t0, t_end)
-    e = 0
-    while True:
-        steps, inv_a = cool.plan(r.step)
-        if steps == 0:
-            break
-        r.inv_alpha = inv_a
-        r.epoch(steps)
-        cool.advance(steps, inv_a)
-        e += 1
-        if e % 5 == 0:
-            if world > 1:
-                islands.exchange(r, 16)
-            else:
-                r.inject(*r.elites(16))
-        torch.cuda.synchronize(dev)
-    gpu_wall = cool.elapsed()
-    key, tour = r.best()
-    if world > 1:
-        key, _ = islands.global_best(r)
     out = {"T_s": seconds, "algorithm": "sa", "instance": label, "cooling": "wall-time geometric",
-           "separators": n_sep, "window": window, "window_types": window_types,
-           "start": start,
-           "gpu": {"chains_per_gpu": chains, "steps_per_chain": r.step, "epochs": e,
-                   "wall_s": gpu_wall, "unvisited": key >> 56,
-                   "duration_sum": (key >> 28) & (2**28 - 1)}}
+           "separators": n_sep, "window": window, "window_types": window_types, "start": start}
+    if gpu:
+        warm = runners.SARunner(ctx, n, chains=chains, total_steps=1000, durations=inst.durations,
+                                n_sep=n_sep, window=window, window_types=window_types, start=start,
+                                moves=moves)
+        warm.epoch(20)                       # first launch: code object load, LDS setup
+        torch.cuda.synchronize(dev)
+        del warm
+        seed = (1000 + rank) if gpu_seed is None else gpu_seed
+        r = runners.SARunner(ctx, n, chains=chains, seed=seed, total_steps=1000,
+                             durations=inst.durations, t0=t0, t_end=t_end, n_sep=n_sep,
+                             window=window, window_types=window_types, start=start, moves=moves)
+        if world > 1:
+            dist.barrier()
+        cool = _TimedCooling(seconds, t0, t_end)
+        e = 0
+        while True:
+            steps, inv_a = cool.plan(r.step)
+            if steps == 0:
+                break
+            r.inv_alpha = inv_a
+            r.epoch(steps)
+            cool.advance(steps, inv_a)
+            e += 1
+            if e % 5 == 0:
+                if world > 1:
+                    islands.exchange(r, 16)
+                else:
+                    r.inject(*r.elites(16))
+            torch.cuda.synchronize(dev)
+        gpu_wall = cool.elapsed()
+        key, tour = r.best()
+        if world > 1:
+            key, _ = islands.global_best(r)
+        out["gpu"] = {"chains_per_gpu": chains, "moves_per_step": moves, "steps_per_chain": r.step,
+                      "epochs": e, "wall_s": gpu_wall, "unvisited": key >> 56,
+                      "duration_sum": (key >> 28) & (2**28 - 1)}
     if with_cpu:
         from oracle import coracle
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or coracle.max_threads()
@@ -228,20 +232,22 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
             coracle.sa_run(inst.durations, cur, best, bk, steps, float(cool.inv_t), float(inv_a),
                            1, step, inst.demand, inst.capacities, inst.start_times,
                            threads=threads, window=window, window_types=window_types,
-                           resync=True)
+                           resync=True, moves=cpu_moves)
             cool.advance(steps, inv_a)
             step += steps
         cpu_wall = cool.elapsed()
         ck = int(bk.min())
-        out["cpu"] = {"chains": threads, "cores": threads, "steps_per_chain": step,
+        out["cpu"] = {"chains": threads, "cores": threads, "moves_per_step": cpu_moves,
+                      "steps_per_chain": step,
                       "wall_s": cpu_wall, "unvisited": ck >> 56,
                       "duration_sum": (ck >> 28) & (2**28 - 1),
                       "kind": "port (oracle/oracle_c.c oracle_sa_run_resync: "
                               "candidates priced by walking only what the move changes)"}
-        g, c = out["gpu"], out["cpu"]
-        ok = g["unvisited"] == 0 and c["unvisited"] == 0 and c["duration_sum"]
-        out["gap"] = (g["duration_sum"] - c["duration_sum"]) / c["duration_sum"] if ok else None
-        out["gap_sign"] = "negative = GPU better"
+        if gpu:
+            g, c = out["gpu"], out["cpu"]
+            ok = g["unvisited"] == 0 and c["unvisited"] == 0 and c["duration_sum"]
+            out["gap"] = (g["duration_sum"] - c["duration_sum"]) / c["duration_sum"] if ok else None
+            out["gap_sign"] = "negative = GPU better"
     return out
 
 

@@ -176,6 +176,11 @@ typedef struct {
                        position within W of the first (large tours) */
   uint32_t window_types; /* A12: move types the window applies to, bit t for
                             type t (1 swap, 2 2-opt, 4 relocate); 0 = all */
+  int32_t moves;    /* moves sampled per step: 0 or 64 = one wavefront per chain;
+                       64 W (W = 2..8) = W wavefronts per chain, move index
+                       lane + 64 w (route-local kernel: window > 0 on a fleet
+                       of one capacity and start time).  vrpms_tsp_batch_sa
+                       ignores it. */
 } vrpms_sa_params;
 
 /* d_cur [chains][n] in/out (cur_key out); d_best/d_best_key in/out (set

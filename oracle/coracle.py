@@ -33,7 +33,7 @@ def load():
         f32, u64 = ctypes.c_float, ctypes.c_uint64
         lib.oracle_sa_run.restype = ctypes.c_int
         lib.oracle_sa_run.argtypes = [i32, vp, i32, i32, vp, vp, vp, i32, i32, vp, vp, vp, vp, i32,
-                                      i32, i32, f32, f32, u64, u64, i32, ctypes.c_uint32, i32]
+                                      i32, i32, f32, f32, u64, u64, i32, ctypes.c_uint32, i32, i32]
         lib.oracle_sa_run_resync.restype = ctypes.c_int
         lib.oracle_sa_run_resync.argtypes = lib.oracle_sa_run.argtypes
         lib.oracle_bf.restype = ctypes.c_int
@@ -77,7 +77,8 @@ def eval_batch(durations, perms, demand=None, capacities=None, start_times=(0,),
 
 def sa_run(durations, cur, best, best_key, steps, inv_t0, inv_alpha, seed, step0,
            demand=None, capacities=None, start_times=(0,), problem: int = 1, objective: int = 0,
-           threads: int = 0, window: int = 0, window_types: int = 0, resync: bool = False):
+           threads: int = 0, window: int = 0, window_types: int = 0, resync: bool = False,
+           moves: int = 64):
     """C/OpenMP SA (same streams as vrpms_sa_run); cur/best uint16 [chains][n]
     and best_key uint64 [chains] are updated in place; returns cur_key.
     resync=True prices candidates by oracle_sa_run_resync (walks only what
@@ -96,7 +97,7 @@ def sa_run(durations, cur, best, best_key, steps, inv_t0, inv_alpha, seed, step0
     fn(problem, _p(D), H, N, _p(dem), _p(cap), _p(st), st.shape[0], objective,
        _p(cur), _p(cur_key), _p(best), _p(best_key), chains, n, int(steps),
        float(inv_t0), float(inv_alpha), int(seed) & (2**64 - 1), int(step0),
-       int(window), int(window_types), threads)
+       int(window), int(window_types), threads, int(moves))
     return cur_key
 
 

@@ -139,7 +139,7 @@ int oracle_eval_batch(int problem, const int32_t* D, int H, int N, const int32_t
 
 /* ------------------------------------------------------------------------
  * SA restatement (oracle/search.py sa_run, SURVEY.md §8a' sa_chain_step):
- * per chain and step, 64 Philox-sampled moves are scored, the best
+ * per chain and step, `moves` (64 W) Philox-sampled moves are scored, the best
  * (key, lane) is accepted if no worse or if (u >> 8) < threshold(dp, invT).
  * Used as the CPU solver at equal wall time (bench.py "quality") and as a
  * large-size parity check of the GPU SA.  Build with -ffp-contract=off.
@@ -315,7 +315,7 @@ int oracle_sa_run(int problem, const int32_t* D, int H, int N, const int32_t* de
                   const int32_t* cap, const int32_t* st, int K, int objective, uint16_t* cur,
                   uint64_t* cur_key, uint16_t* best, uint64_t* best_key, int chains, int n,
                   int steps, float inv_t0, float inv_alpha, uint64_t seed, uint64_t step0,
-                  int window, uint32_t window_types, int threads) {
+                  int window, uint32_t window_types, int threads, int moves) {
   inst_t I = {problem, H, N, K, objective, D, dem, cap, st};
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 #ifdef _OPENMP
@@ -338,7 +338,7 @@ int oracle_sa_run(int problem, const int32_t* D, int H, int N, const int32_t* de
       int lbest = 0;
       move_t mbest = {0, 0, 0};
       uint32_t wbest = 0;
-      for (int lane = 0; lane < 64; ++lane) {
+      for (int lane = 0; lane < moves; ++lane) {
         u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)c, (uint32_t)lane, k0,
                          k1);
         move_t m = decode_move_window(r.x, r.y, r.z, n, window, window_types);
@@ -749,13 +749,13 @@ int oracle_sa_run_resync(int problem, const int32_t* D, int H, int N, const int3
                          uint16_t* cur, uint64_t* cur_key, uint16_t* best, uint64_t* best_key,
                          int chains, int n, int steps, float inv_t0, float inv_alpha,
                          uint64_t seed, uint64_t step0, int window, uint32_t window_types,
-                         int threads) {
+                         int threads, int moves) {
   int uniform = problem == 1 && K > 0;
   for (int k = 1; uniform && k < K; ++k) uniform = cap[k] == cap[0] && st[k] == st[0];
   if (!uniform || n < 2)
     return oracle_sa_run(problem, D, H, N, dem, cap, st, K, objective, cur, cur_key, best,
                          best_key, chains, n, steps, inv_t0, inv_alpha, seed, step0, window,
-                         window_types, threads);
+                         window_types, threads, moves);
   inst_t I = {problem, H, N, K, objective, D, dem, cap, st};
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   int levels = 1;
@@ -798,7 +798,7 @@ int oracle_sa_run_resync(int problem, const int32_t* D, int H, int N, const int3
         move_t mbest = {0, 0, 0};
         uint32_t wbest = 0;
         const int hopeless = (ck >> 56) == 0 && accept_threshold(1u << 28, invT) == 0;
-        for (int lane = 0; lane < 64; ++lane) {
+        for (int lane = 0; lane < moves; ++lane) {
           u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)c, (uint32_t)lane,
                            k0, k1);
           move_t m = decode_move_window(r.x, r.y, r.z, n, window, window_types);

@@ -51,14 +51,14 @@ class StandInContext:
         return _i64([int(x) for x in k])
 
     def sa_run(self, cur, cur_key, best, best_key, steps, inv_t0, inv_alpha, seed, step0,
-               window=0, window_types=0):
+               window=0, window_types=0, moves=64):
         c = cur.numpy().view(np.uint16).copy()
         b = best.numpy().view(np.uint16).copy()
         bk = np.array(_u64(best_key), dtype=np.uint64)
         ck = coracle.sa_run(self.inst.durations, c, b, bk, steps, inv_t0, inv_alpha, seed, step0,
                             self.inst.demand, self.inst.capacities, self.inst.start_times,
                             self.problem, self.objective, window=window,
-                            window_types=window_types)
+                            window_types=window_types, resync=True, moves=moves)
         cur.copy_(_as_i16(c))
         best.copy_(_as_i16(b))
         cur_key.copy_(_i64([int(x) for x in ck]))

@@ -165,6 +165,16 @@ def _run_sa(ctx, P, steps, inv_t0, inv_alpha, seed, step0, window, types=0):
     return cur.cpu().numpy(), u64(ck), best.cpu().numpy(), u64(bk)
 
 
+def _asym(inst, seed, scale=1):
+    """inst with an asymmetric static matrix (the route kernel's reverse-edge
+    cache); scale > 1 pushes entries past 65535 (int32 matrix)."""
+    import dataclasses
+    rng = np.random.default_rng(seed)
+    D = inst.durations[0] * scale + rng.integers(0, 40, size=inst.durations.shape[1:])
+    np.fill_diagonal(D, 0)
+    return dataclasses.replace(inst, durations=D[None])
+
+
 ROUTE_CASES = [
     # cfg 4: X-1000, K - 1 separators where the greedy split closes routes
     ("x1000_greedy", lambda: synth.x_style(1000, seed=1), "greedy", 16, 40, 1 / 300.0, 32, 0),
@@ -191,6 +201,11 @@ ROUTE_CASES = [
      1 / 50.0, 12, 2),
     # many separators per route (S > K - 1 is never route-local; S < K - 1 is)
     ("cvrp120_few_seps", lambda: synth.cvrp(120, 10, seed=6), "pack_few", 8, 40, 1 / 100.0, 5, 2),
+    # asymmetric static matrices: reversed adjacencies read the reverse-edge cache
+    ("x1000_asym_u16", lambda: _asym(synth.x_style(1000, seed=3), 1), "pack", 8, 120, 1 / 300.0,
+     32, 0),
+    ("cvrp300_asym_i32", lambda: _asym(synth.cvrp(300, 24, seed=8), 2, scale=60), "pack", 8, 120,
+     1 / 18000.0, 24, 0),
 ]
 
 
@@ -231,6 +246,70 @@ def test_route_local_sa_matches_c_restatement(ctx, coracle, name, maker, start, 
     finally:
         ctx.set_sa_route(0)
     assert (full[0] == got[0]).all() and full[1] == got[1] and full[3] == got[3]
+
+
+MULTIWAVE_CASES = [
+    # (case, moves): W = moves / 64 wavefronts per chain price 64 W moves per step
+    ("x1000_pack_2opt", 512),
+    ("x1000_pack_long_hot", 256),
+    ("td200_random", 256),
+    ("cvrp150_hot", 128),
+    ("cvrp200_no_seps", 192),
+    ("x1000_asym_u16", 512),
+]
+
+
+@pytest.mark.parametrize("name,moves", MULTIWAVE_CASES, ids=[f"{c}-m{m}" for c, m in MULTIWAVE_CASES])
+def test_route_local_multiwave_matches_c_restatement(ctx, coracle, name, moves):
+    """W wavefronts per chain (64 W moves per step, move index lane + 64 w,
+    (key, index) minimum across wavefronts) against the C restatement with
+    the same `moves`, full re-walk and route-resync pricing alike."""
+    case = {c[0]: c for c in ROUTE_CASES}[name]
+    _, maker, start, chains, steps, inv_t0, window, types = case
+    inst = maker()
+    load(ctx, inst)
+    S = {"pack_few": inst.K - 4, "nosep": 0}.get(start, inst.K - 1)
+    if start == "nosep":
+        P = synth.random_perms(chains, inst.n, seed=9, dtype=np.uint16)
+    elif start != "random":
+        P0 = synth.random_perms(chains, inst.n, seed=9, dtype=np.uint16)
+        f = spec.insert_separators if start == "greedy" else spec.pack_separators
+        P = np.array([f(p, S, inst.demand, inst.capacities) for p in P0])
+    else:
+        P = sep_tours(chains, inst.n, S, seed=9, dtype=np.uint16)
+    P = P.astype(np.int16)
+    torch = torch_()
+    cur = torch.from_numpy(P).to(ctx.dev)
+    best = cur.clone()
+    ck = torch.empty(chains, dtype=torch.int64, device=ctx.dev)
+    bk = torch.full((chains,), -1, dtype=torch.int64, device=ctx.dev)
+    ctx.sa_run(cur, ck, best, bk, steps=steps, inv_t0=inv_t0, inv_alpha=1 / 0.99, seed=21,
+               step0=7, window=window, window_types=types, moves=moves)
+    for resync in (False, True):
+        ccur, cbest = P.view(np.uint16).copy(), P.view(np.uint16).copy()
+        cbk = np.full(chains, 2**64 - 1, dtype=np.uint64)
+        cck = coracle.sa_run(inst.durations, ccur, cbest, cbk, steps, inv_t0, 1 / 0.99, 21, 7,
+                             inst.demand, inst.capacities, inst.start_times, window=window,
+                             window_types=types, resync=resync, moves=moves)
+        assert (cur.cpu().numpy().view(np.uint16) == ccur).all()
+        assert u64(ck) == [int(x) for x in cck] and u64(bk) == [int(x) for x in cbk]
+        assert (best.cpu().numpy().view(np.uint16) == cbest).all()
+
+
+def test_sa_moves_validation(ctx):
+    inst = synth.cvrp(30, 4, seed=1)
+    load(ctx, inst)
+    torch = torch_()
+    P = torch.from_numpy(synth.random_perms(4, inst.n, seed=1, dtype=np.uint16).astype(np.int16))
+    cur = P.to(ctx.dev)
+    ck = torch.empty(4, dtype=torch.int64, device=ctx.dev)
+    bk = torch.full((4,), -1, dtype=torch.int64, device=ctx.dev)
+    with pytest.raises(RuntimeError):   # not a multiple of 64
+        ctx.sa_run(cur, ck, cur.clone(), bk, 2, 0.01, 1.0, 1, 0, window=4, moves=100)
+    with pytest.raises(RuntimeError):   # more than 8 wavefronts
+        ctx.sa_run(cur, ck, cur.clone(), bk, 2, 0.01, 1.0, 1, 0, window=4, moves=576)
+    with pytest.raises(RuntimeError):   # window 0: not the route-local kernel
+        ctx.sa_run(cur, ck, cur.clone(), bk, 2, 0.01, 1.0, 1, 0, window=0, moves=128)
 
 
 def test_route_local_sa_small_matches_python_oracle(ctx):

@@ -20,7 +20,7 @@ LIB = os.path.join(ROOT, "build_ab", "gaprof", "libvrpms.so")
 def build():
     from vrpms_amd import build as b
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    cmd = [b.HIPCC, *b.FLAGS, "-DVRPMS_GA_PROF", "-o", LIB, *b.sources(), "-L/opt/rocm/lib",
+    cmd = [b.HIPCC, *b.FLAGS, "-shared", "-DVRPMS_GA_PROF", "-o", LIB, *b.sources(), "-L/opt/rocm/lib",
            "-lrccl"]
     subprocess.run(cmd, check=True)
 

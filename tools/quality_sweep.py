@@ -41,6 +41,10 @@ def main():
                     help="cfg 2 CVRP-100 K=8, CVRP-200 K=16, or cfg 4 X-style CVRP-1000")
     ap.add_argument("--sep", type=int, default=None,
                     help="A10 route separators per tour (default K - 1; 0 = plain giant tours)")
+    ap.add_argument("--moves", type=int, default=64,
+                    help="GPU moves per step (64 W: W wavefronts per chain)")
+    ap.add_argument("--cpu-moves", type=int, nargs="+", default=[64],
+                    help="host moves per step; several values: each cell reports the host's best")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "quality_sweep.json"))
     args = ap.parse_args()
 
@@ -63,17 +67,35 @@ def main():
         for T in args.T:
             window = args.window if args.window is not None else (
                 0 if args.instance == "cvrp100" else 32)
-            q = bench.quality(ctx, inst, T, 1, 0, None, with_cpu=True,
-                              chains=args.chains or (4096 if args.instance == "cvrp100" else 2048),
+            chains = args.chains or (4096 if args.instance == "cvrp100" else 2048) * 64 // args.moves
+            q = bench.quality(ctx, inst, T, 1, 0, None, with_cpu=True, chains=chains,
+                              moves=args.moves, cpu_moves=args.cpu_moves[0],
                               label=f"{args.instance} seed {seed}", n_sep=args.sep,
                               window=window,
                               window_types=args.types if args.types is not None else 2,
                               start=args.start or ("random" if args.instance == "cvrp100"
                                                    else "pack"))
+            print(json.dumps({"progress": f"seed {seed} T {T}: gpu {q['gpu']['duration_sum']} "
+                                          f"cpu(m={args.cpu_moves[0]}) {q['cpu']['duration_sum']}"}),
+                  flush=True)
+            for cm in args.cpu_moves[1:]:   # the host leg at its best sample size
+                q2 = bench.quality(ctx, inst, T, 1, 0, None, with_cpu=True, chains=chains,
+                                   moves=args.moves, cpu_moves=cm, gpu=False,
+                                   label=f"{args.instance} seed {seed}", n_sep=args.sep,
+                                   window=window,
+                                   window_types=args.types if args.types is not None else 2,
+                                   start=args.start or ("random" if args.instance == "cvrp100"
+                                                        else "pack"))
+                q.setdefault("cpu_alternatives", []).append(q2["cpu"])
+                if q2["cpu"]["unvisited"] == 0 and q2["cpu"]["duration_sum"] < q["cpu"]["duration_sum"]:
+                    q["cpu_alternatives"][-1] = q["cpu"]
+                    q["cpu"] = q2["cpu"]
+                    q["gap"] = (q["gpu"]["duration_sum"] - q["cpu"]["duration_sum"]) / q["cpu"]["duration_sum"]
             q["seed"] = seed
             cells.append(q)
             print(json.dumps({"seed": seed, "T_s": T, "gpu": q["gpu"]["duration_sum"],
-                              "cpu": q["cpu"]["duration_sum"], "gap": q["gap"],
+                              "cpu": q["cpu"]["duration_sum"], "cpu_moves": q["cpu"]["moves_per_step"],
+                              "gap": q["gap"],
                               "gpu_wall": round(q["gpu"]["wall_s"], 3),
                               "cpu_wall": round(q["cpu"]["wall_s"], 3),
                               "elapsed": round(time.time() - t_start, 1)}), flush=True)

@@ -25,7 +25,7 @@ def build():
     from vrpms_amd import build as b
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     extra = [f"-DVRPMS_ROUTE_{VARIANT}"] if VARIANT else []
-    cmd = [b.HIPCC, *b.FLAGS, "-DVRPMS_ROUTE_PROF", *extra, "-o", LIB, *b.sources(),
+    cmd = [b.HIPCC, *b.FLAGS, "-shared", "-DVRPMS_ROUTE_PROF", *extra, "-o", LIB, *b.sources(),
            "-L/opt/rocm/lib", "-lrccl"]
     subprocess.run(cmd, check=True)
 

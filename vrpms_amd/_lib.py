@@ -47,7 +47,7 @@ _u64 = _c.c_uint64
 class SaParams(ctypes.Structure):
     _fields_ = [("chains", _i32), ("steps", _i32), ("inv_t0", ctypes.c_float),
                 ("inv_alpha", ctypes.c_float), ("seed", _u64), ("step0", _u64),
-                ("window", _i32), ("window_types", _c.c_uint32)]
+                ("window", _i32), ("window_types", _c.c_uint32), ("moves", _i32)]
 
 
 class GaParams(ctypes.Structure):

@@ -222,13 +222,15 @@ class Context:
 
     # -- search kernels (state lives in caller-owned device tensors) ----------
     def sa_run(self, cur, cur_key, best, best_key, steps: int, inv_t0: float, inv_alpha: float,
-               seed: int, step0: int, window: int = 0, window_types: int = 0):
+               seed: int, step0: int, window: int = 0, window_types: int = 0, moves: int = 64):
         """Advance every chain (rows of the int16 [chains][n] tensor ``cur``);
         window > 0 samples A11 windowed moves of the A12 types
-        ``window_types`` (bit t for move type t, 0 = all)."""
+        ``window_types`` (bit t for move type t, 0 = all); ``moves`` per step
+        (64 W: W wavefronts per chain)."""
         chains, n = cur.shape
         p = _lib.SaParams(chains, int(steps), float(inv_t0), float(inv_alpha),
-                          int(seed) & (2**64 - 1), int(step0), int(window), int(window_types))
+                          int(seed) & (2**64 - 1), int(step0), int(window), int(window_types),
+                          int(moves))
         check(self.lib.vrpms_sa_run(self._ctx, ctypes.byref(p), cur.data_ptr(),
                                     cur_key.data_ptr(), best.data_ptr(), best_key.data_ptr(), n,
                                     self.stream()))

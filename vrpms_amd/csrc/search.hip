@@ -123,6 +123,7 @@ struct SaArgs {
   uint64_t* cur_key;    // [chains]
   uint16_t* best;       // [chains][n]
   uint64_t* best_key;   // [chains]
+  int wpc;              // sa_route_kernel: wavefronts per chain (1: 4 chains per workgroup)
 };
 
 template <typename MatT, int HM, bool CVRP>
@@ -263,14 +264,26 @@ __host__ __device__ inline int route_levels(int rm) {
 }
 __host__ __device__ inline int route_segs(int K) { return (K + 2 + 7) & ~7; }
 // per-chain LDS: u32 [tour | demand], u32 tables, u32 route-start bits,
-// then u16 route starts / separator positions, then u8 route ids / flags
+// then u16 route starts / separator positions, then u8 route ids / flags,
+// then (16-byte aligned) the cross-wavefront exchange of a multi-wave chain
+constexpr int kRouteMaxWaves = 8;
+constexpr uint32_t kRouteXBytes = 2 * kRouteMaxWaves * 16 + 16;
 __host__ __device__ inline uint32_t route_wave_bytes(int npad, int K) {
   const uint32_t rm = (uint32_t)route_rm(K), lv = (uint32_t)route_levels(route_rm(K));
   const uint32_t words = (uint32_t)npad / 32u + 4u;
   const uint32_t u32s = (uint32_t)npad + (6u + (lv - 1u)) * rm + words;
   const uint32_t u16s = rm + (uint32_t)route_segs(K);
   const uint32_t u8s = (uint32_t)npad + rm;
-  return 4u * u32s + 2u * u16s + u8s;
+  return ((4u * u32s + 2u * u16s + u8s + 15u) & ~15u) + kRouteXBytes;
+}
+
+// LDS after the per-chain tables: the depot legs (static matrix), then per
+// chain the edge cache ein (+ erev on an asymmetric matrix)
+__host__ __device__ inline uint32_t route_legs_bytes(int hm, int N, int elem) {
+  return hm == 1 ? ((uint32_t)(2 * N * elem) + 15u) & ~15u : 0u;
+}
+__host__ __device__ inline uint32_t route_edge_bytes(int hm, int npad, int elem, bool sym) {
+  return hm == 1 ? ((uint32_t)(npad * elem * (sym ? 1 : 2)) + 15u) & ~15u : 0u;
 }
 
 struct RouteTabs {
@@ -306,7 +319,7 @@ __device__ unsigned long long g_route_prof[12 * 8192];
 #endif
 
 template <typename MatT, int HM>
-__global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
+__global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 #ifdef VRPMS_ROUTE_PROF
   const unsigned long long pk0 = wall_clock64();
@@ -314,20 +327,38 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
   const StagedInst<MatT, HM> I = stage_inst<MatT, HM>(a.si, smem);
   const int n = a.n;
   const int wave = threadIdx.x >> 6, lane = lane_id();
-  const int chain = blockIdx.x * 4 + wave;
+  // W = 1: four chains per workgroup, one wavefront each.  W > 1: one chain
+  // per workgroup, its W wavefronts price 64 W moves per step (move index
+  // lane + 64 cw), the (key, index) minimum meets in LDS, and the winning
+  // wavefront applies an accepted move to the chain's tables.
+  const int W = a.wpc;
+  const int cw = W > 1 ? wave : 0;  // wavefront within the chain
+  const int slot = W > 1 ? 0 : wave;
+  const int CPW = W > 1 ? 1 : 4;    // chains per workgroup
+  const int chain = W > 1 ? (int)blockIdx.x : (int)blockIdx.x * 4 + wave;
+  const uint32_t mlane = (uint32_t)(lane + 64 * cw);
   const int K = a.si.K;
   const int RMAX = route_max(K), RM = route_rm(K), LV = route_levels(RM);
   const int SEGS = route_segs(K);
   const uint32_t npad = ((uint32_t)n + 7u) & ~7u;
   const uint32_t wbytes = (route_wave_bytes((int)npad, K) + 15u) & ~15u;
-  unsigned char* wb = smem + inst_lds_bytes(a.si) + wave * wbytes;
+  unsigned char* wb = smem + inst_lds_bytes(a.si) + slot * wbytes;
+  // cross-wavefront exchange (W > 1): two buffers of W (key, index, u) slots
+  // (by step parity), then R and route_ok after an accept
+  struct XSlot {
+    uint64_t key;
+    uint32_t idx, u;
+  };
+  XSlot* xs = reinterpret_cast<XSlot*>(wb + wbytes - kRouteXBytes);
+  int32_t* xr = reinterpret_cast<int32_t*>(xs + 2 * kRouteMaxWaves);
   const uint32_t N = (uint32_t)a.si.N;
   // static matrix: the depot legs out(c) = D(0, c) and ret(c) = D(c, 0) in
   // LDS (one u32 per node for a u16 matrix), so a pricing walk gathers one
   // matrix entry per token from L2
-  MatT* legs = reinterpret_cast<MatT*>(smem + inst_lds_bytes(a.si) + 4 * wbytes);
+  MatT* legs = reinterpret_cast<MatT*>(smem + inst_lds_bytes(a.si) + CPW * wbytes);
+  const MatT* M0 = static_cast<const MatT*>(a.si.mat);  // hour 0 in global memory (L2)
   if constexpr (HM == 1) {
-    const MatT* M = static_cast<const MatT*>(a.si.mat);
+    const MatT* M = M0;
     for (uint32_t c = threadIdx.x; c < N; c += blockDim.x) {
       legs[2 * c] = M[c];
       legs[2 * c + 1] = M[(size_t)c * N];
@@ -358,7 +389,7 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
   const uint32_t Nm1 = N - 1;
   const int cap0 = I.sp.cap[0], st0 = I.sp.start[0];
   const int32_t* dem = I.sp.dem;
-  {
+  if (cw == 0) {  // the chain's first wavefront owns every table write outside an accept
     const uint16_t* gcur = a.cur + (int64_t)chain * n;
     for (int q = lane; q < n; q += 64) {
       const uint32_t c = min((uint32_t)gcur[q], Nm1);
@@ -367,6 +398,28 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
     wave_sync();
   }
   auto tokA = [&](int q) { return T.at[q] & 0xffffu; };
+  // static matrix: the edge into each position from the token before it
+  // (ein; erev = the reverse edge, its own array on an asymmetric matrix),
+  // kept with the tour, so a pricing walk reads the edges of every adjacency
+  // the move keeps (forward or reversed) from LDS and gathers only the <= 4
+  // junction edges it creates from L2
+  const bool sym = a.si.symmetric != 0;
+  MatT* ein = reinterpret_cast<MatT*>(smem + inst_lds_bytes(a.si) + CPW * wbytes +
+                                      route_legs_bytes(HM, (int)N, (int)sizeof(MatT)) +
+                                      slot * route_edge_bytes(HM, (int)npad, (int)sizeof(MatT), sym));
+  MatT* erev = sym ? ein : ein + npad;
+  auto edge_cache = [&]() {
+    if constexpr (HM == 1) {
+      for (int q = lane; q < n; q += 64) {
+        const uint32_t c = tokA(q), p = q ? tokA(q - 1) : 0u;
+        ein[q] = M0[(size_t)p * N + c];
+        if (!sym) erev[q] = M0[(size_t)c * N + p];
+      }
+      wave_sync();
+    }
+  };
+  if (cw == 0) edge_cache();
+  if (W > 1) __syncthreads();
   auto SP = [&](int l) { return l ? T.sp + (l - 1) * RM : T.dur; };
 
   // greedy split state of one walk and what it has closed so far
@@ -422,6 +475,11 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
   };
   auto edge = [&](uint32_t x, uint32_t y) -> int {  // static matrix entry (L2)
     if constexpr (HM == 1) return I.D(0, x, y);
+    else return 0;
+  };
+  // the current tour's edge into position q (static matrix, LDS)
+  auto ein_q = [&](int q) -> int {
+    if constexpr (HM == 1) return (int)ein[q];
     else return 0;
   };
 
@@ -512,7 +570,7 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
         const uint32_t at = T.at[q], c = at & 0xffffu;
         const int d = (int)(at >> 16);
         if (w.load + d > cap0) close(w);
-        add(w, c, d, w.prev ? edge(w.prev, c) : 0);
+        add(w, c, d, w.prev ? ein_q(q) : 0);
       }
       close(w);
       T.smx[s] = w.cnt;
@@ -546,7 +604,7 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
           ++r;
           start = q;
         }
-        add(w, c, d, w.prev ? edge(w.prev, c) : 0);
+        add(w, c, d, w.prev ? ein_q(q) : 0);
         T.rid[q] = (uint8_t)r;
       }
       const bool cu = w.prev != 0;
@@ -568,13 +626,22 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
     auto tour = [&](int i) { return tokA(i); };
     ck = eval_tour<true>(I.D, I.sp, tour, n).key;
   }
-  int R = full_build();
+  int R = 0;
+  if (cw == 0) {
+    R = full_build();
+    if (lane == 0) xr[0] = R;
+  }
+  if (W > 1) {
+    __syncthreads();
+    R = xr[0];
+  }
   bool route_ok = R >= 0;
   uint16_t* gbest = a.best + (int64_t)chain * n;
   uint64_t bk = a.best_key[chain];
   if (ck < bk) {
     bk = ck;
-    for (int q = lane; q < n; q += 64) gbest[q] = (uint16_t)tokA(q);
+    if (cw == 0)
+      for (int q = lane; q < n; q += 64) gbest[q] = (uint16_t)tokA(q);
   }
   float invT = a.inv_t0;
 #ifdef VRPMS_ROUTE_PROF
@@ -588,8 +655,8 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
     unsigned long long pwalk = 0;
 #endif
     const uint64_t step = a.step0 + (uint64_t)st;
-    const u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)chain,
-                           (uint32_t)lane, a.seed_lo, a.seed_hi);
+    const u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)chain, mlane,
+                           a.seed_lo, a.seed_hi);
     const Move m = decode_move_window(r.x, r.y, r.z, n, a.window, a.window_types);
     const MoveMap mm = move_map(m);
     auto moved = [&](int q) { return tokA(map_src(mm, q)); };
@@ -600,6 +667,10 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
     bool full = !route_ok;
     // zone bookkeeping and the routes each zone closes (for an accept)
     int r1s = 0, r1e = 0, r2s = 0, r2e = 0, P1 = 0, Z2 = 0, q1 = 0, q2 = 0, dl = 0;
+    // junction edges: every adjacency of the moved tour except at positions
+    // lo, lo + 1, hi, hi + 1 is one of the current tour's (forward or
+    // reversed), read from the edge cache; these four are gathered here
+    int jx0 = 0, jx1 = 0, jx2 = 0, jx3 = 0;
     uint32_t c1 = 0, c2 = 0;
     // route starts of each zone as bits over its positions (zone start = bit
     // 0; bits at or past the zone's end are ignored); zones of more than 128
@@ -608,6 +679,13 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
     bool zovf = false;
     if (route_ok) {
       const int lo = min(m.i, m.j), hi = max(m.i, m.j);
+      if constexpr (HM == 1) {
+        auto jedge = [&](int p) { return p >= 1 && p < n ? edge(moved(p - 1), moved(p)) : 0; };
+        jx0 = jedge(lo);
+        jx1 = jedge(lo + 1);
+        jx2 = jedge(hi);
+        jx3 = jedge(hi + 1);
+      }
       int bq0 = lo + 1;  // first moved position of the shifted middle
       if (m.typ == kMoveRelocate && m.i < m.j) {
         dl = -1;
@@ -661,16 +739,24 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
 #endif
         uint32_t cb[kBlk];
         int db[kBlk], eb[kBlk];
-        {
-          uint32_t cp = q > 0 ? moved(q - 1) : 0u;
 #pragma unroll
-          for (int i = 0; i < kBlk; ++i) {
-            const int qq = q + i;
-            const uint32_t at = qq < n ? T.at[map_src(mm, qq)] : 0u;
-            cb[i] = at & 0xffffu;
-            db[i] = (int)(at >> 16);
-            eb[i] = edge(cp, cb[i]);
-            cp = cb[i];
+        for (int i = 0; i < kBlk; ++i) {
+          const int qq = q + i;
+          const int sq = map_src(mm, qq), sp = map_src(mm, qq - 1);
+          const uint32_t at = qq < n ? T.at[sq] : 0u;
+          cb[i] = at & 0xffffu;
+          db[i] = (int)(at >> 16);
+          if constexpr (HM == 1) {
+            // forward adjacency: the current edge into sq; reversed (sp ==
+            // sq + 1): the reverse of the current edge into sp
+            int e = qq < n ? (sp + 1 == sq ? (int)ein[sq] : (int)erev[max(sp, 0)]) : 0;
+            e = qq == lo ? jx0 : e;
+            e = qq == lo + 1 ? jx1 : e;
+            e = qq == hi ? jx2 : e;
+            e = qq == hi + 1 ? jx3 : e;
+            eb[i] = e;
+          } else {
+            eb[i] = 0;
           }
         }
         // route-start bits at the current tour's positions of the middle
@@ -764,11 +850,29 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
     if (full) k = eval_tour<true>(I.D, I.sp, moved, n).key;
     int bl;
     k = wave_argmin_lane(k, bl);  // wave-uniform (key, lane) minimum
+    uint32_t uw = (uint32_t)wave_bcast((int)r.w, bl);
+    int ww = 0;  // winning wavefront of the chain
+    if (W > 1) {
+      // the chain's (key, move index) minimum over its wavefronts; two slot
+      // buffers by step parity, so a slot is rewritten only after the next
+      // step's barrier
+      XSlot* xb = xs + (st & 1) * kRouteMaxWaves;
+      if (lane == 0) xb[cw] = XSlot{k, (uint32_t)(64 * cw + bl), uw};
+      __syncthreads();
+      XSlot b = xb[0];
+      for (int v = 1; v < W; ++v) {
+        const XSlot o = xb[v];
+        if (o.key < b.key) b = o;  // equal keys: the lower index (earlier slot) stays
+      }
+      k = b.key;
+      uw = b.u;
+      ww = (int)(b.idx >> 6);
+    }
     bool accept = k <= ck;
     if (!accept) {
       const uint64_t d = (k >> 28) - (ck >> 28);
       const uint32_t dp = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
-      accept = ((uint32_t)wave_bcast((int)r.w, bl) >> 8) < accept_threshold(dp, invT);
+      accept = (uw >> 8) < accept_threshold(dp, invT);
     }
 #ifdef VRPMS_ROUTE_PROF
     const unsigned long long pt1 = wall_clock64();
@@ -791,7 +895,13 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
       pf[9] += (unsigned long long)bx;
     }
 #endif
-    if (accept) {
+    if (accept && cw != ww) {  // another wavefront applies it: wait for its tables
+      __syncthreads();
+      R = xr[0];
+      route_ok = xr[1] != 0;
+      ck = k;
+      bk = ck < bk ? ck : bk;
+    } else if (accept) {
       Move mb;
       mb.typ = (uint32_t)wave_bcast((int)m.typ, bl);
       mb.i = wave_bcast(m.i, bl);
@@ -828,17 +938,57 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
       // (and, incrementally, their new route ids) in registers over one sync
       if (regs) {
         {
-          uint32_t v[kTourRegs];
+          // the new tour's entries and its edge cache: kept adjacencies come
+          // from the current cache, the four junction edges from the winner's
+          // gathers (or from L2 when it priced in full)
+          const int blo = min(mb.i, mb.j), bhi = max(mb.i, mb.j);
+          const int bj0 = wave_bcast(jx0, bl), bj1 = wave_bcast(jx1, bl);
+          const int bj2 = wave_bcast(jx2, bl), bj3 = wave_bcast(jx3, bl);
+          // one register per position: the entry, and the new cache entries
+          // packed (u16 matrix: ein | erev << 16; int32 symmetric: ein; an
+          // int32 asymmetric matrix rebuilds its cache from L2 instead)
+          constexpr bool kPack = sizeof(MatT) == 2;
+          const bool regcache = HM == 1 && (kPack || sym);
+          uint32_t v[kTourRegs], fr[kTourRegs];
 #pragma unroll
           for (int i = 0; i < kTourRegs; ++i) {
             const int q = lane + 64 * i;
-            v[i] = q < n ? T.at[map_src(mmb, q)] : 0u;
+            const int sq = map_src(mmb, q), sp = map_src(mmb, q - 1);
+            v[i] = q < n ? T.at[sq] : 0u;
+            fr[i] = 0;
+            if (regcache && q < n) {
+              const bool fwd = sp + 1 == sq;
+              const int spc = max(sp, 0);
+              uint32_t fe = fwd ? (uint32_t)ein[sq] : (uint32_t)erev[spc];
+              uint32_t re = fwd ? (uint32_t)erev[sq] : (uint32_t)ein[spc];
+              const uint32_t c = v[i] & 0xffffu;
+              if (q == 0) {
+                fe = (uint32_t)legs[2 * c];
+                re = (uint32_t)legs[2 * c + 1];
+              } else if (q == blo || q == blo + 1 || q == bhi || q == bhi + 1) {
+                const uint32_t pc = tokA(sp);
+                fe = route_ok ? (uint32_t)(q == blo ? bj0 : q == blo + 1 ? bj1 : q == bhi ? bj2 : bj3)
+                              : (uint32_t)M0[(size_t)pc * N + c];
+                re = sym ? fe : (uint32_t)M0[(size_t)c * N + pc];
+              }
+              fr[i] = kPack ? (fe | (re << 16)) : fe;
+            }
           }
           wave_sync();
 #pragma unroll
           for (int i = 0; i < kTourRegs; ++i) {
             const int q = lane + 64 * i;
-            if (q < n) T.at[q] = v[i];
+            if (q < n) {
+              T.at[q] = v[i];
+              if (regcache) {
+                ein[q] = (MatT)(kPack ? (fr[i] & 0xffffu) : fr[i]);
+                if (!sym) erev[q] = (MatT)(fr[i] >> 16);
+              }
+            }
+          }
+          if (HM == 1 && !regcache) {
+            wave_sync();
+            edge_cache();
           }
         }
         if (incremental) {
@@ -889,7 +1039,7 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
                     continue;
                   }
                   if (w.load + d > cap0) put(q);
-                  add(w, c, d, w.prev ? edge(w.prev, c) : 0);
+                  add(w, c, d, w.prev ? ein_q(q) : 0);
                   T.rid[q] = (uint8_t)rr;
                 }
                 if (w.prev != 0 || to >= n) put(to);  // back in step right after a closure: none
@@ -910,6 +1060,7 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
           T.at[q] = c | ((uint32_t)dem[c] << 16);
         }
         wave_sync();
+        edge_cache();
       }
       ck = k;
       if (ck < bk) {
@@ -981,7 +1132,7 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
             for (int q = from; q < to; ++q) {
               const uint32_t at = T.at[q], c = at & 0xffffu;
               if (c == 0) break;  // a separator ends the route
-              add(w, c, (int)(at >> 16), w.prev ? edge(w.prev, c) : 0);
+              add(w, c, (int)(at >> 16), w.prev ? ein_q(q) : 0);
             }
             const bool cu = w.prev != 0;
             T.dur[rr] = close(w);
@@ -996,12 +1147,20 @@ __global__ __launch_bounds__(256) void sa_route_kernel(SaArgs a) {
         R = full_build();
         route_ok = R >= 0;
       }
+      if (W > 1) {  // publish the tables' route count to the chain's other wavefronts
+        if (lane == 0) {
+          xr[0] = R;
+          xr[1] = route_ok ? 1 : 0;
+        }
+        __syncthreads();
+      }
     }
 #ifdef VRPMS_ROUTE_PROF
     pf[1] += wall_clock64() - pt1;
 #endif
     invT = invT * a.inv_alpha;
   }
+  if (cw != 0) return;
   uint16_t* gout = a.cur + (int64_t)chain * n;
   for (int q = lane; q < n; q += 64) gout[q] = (uint16_t)tokA(q);
   if (lane == 0) {
@@ -1896,9 +2055,15 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
     return fail(VRPMS_EINVAL, "vrpms_sa_run: NULL state buffer");
   if (p->window_types > 7u) return fail(VRPMS_EINVAL, "vrpms_sa_run: window_types is a 3-bit mask");
   const uint32_t wtypes = p->window_types ? p->window_types : 7u;
+  // moves per step: 64 (one wavefront per chain) or 64 W, W = 2..8 wavefronts
+  // per chain (route-local kernel only)
+  const int moves = p->moves ? p->moves : 64;
+  if (moves % 64 != 0 || moves < 64 || moves > 64 * kRouteMaxWaves)
+    return fail(VRPMS_EINVAL, "vrpms_sa_run: moves must be 64 * W, W = 1..8");
+  const int wpc = moves / 64;
   VRPMS_HIP(hipSetDevice(ctx->device));
   FastSplit f;
-  if (ctx->inst.H == 1 && fast_split_params(ctx, n, &f)) {
+  if (wpc == 1 && ctx->inst.H == 1 && fast_split_params(ctx, n, &f)) {
     const uint32_t tb = ((uint32_t)n + 12u + 15u) & ~15u;
     const size_t lds = (((size_t)f.N * f.N * 8 + 15) & ~(size_t)15) +
                        (size_t)kSaPackedWaves * 3 * tb;
@@ -1917,7 +2082,7 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
   }
   SaArgs a{search_inst(ctx), p->chains, n, p->steps, p->window, wtypes, p->inv_t0, p->inv_alpha,
            (uint32_t)p->seed, (uint32_t)(p->seed >> 32), p->step0, d_cur, d_cur_key, d_best,
-           d_best_key};
+           d_best_key, wpc};
   // route-local pricing (sa_route_kernel) for windowed SA on a fleet of
   // exchangeable vehicles: one capacity, one start time, every demand fits
   const Instance& in = ctx->inst;
@@ -1927,16 +2092,24 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
       n <= 65535 && ctx->opt_sa_route != 2) {
     const size_t npad = ((size_t)n + 7) & ~(size_t)7;
     const size_t wbytes = ((size_t)route_wave_bytes((int)npad, in.K) + 15) & ~(size_t)15;
-    const size_t legs = in.H == 1 ? (size_t)2 * in.N * (in.use16 ? 2 : 4) : 0;
-    size_t lds = inst_lds_bytes_host(a.si) + 4 * wbytes + legs;
+    const int elem = in.use16 ? 2 : 4;
+    const size_t cpw = wpc > 1 ? 1 : 4;  // chains per workgroup
+    const size_t legs = route_legs_bytes(in.H, in.N, elem) +
+                        cpw * (size_t)route_edge_bytes(in.H, (int)npad, elem, a.si.symmetric != 0);
+    size_t lds = inst_lds_bytes_host(a.si) + cpw * wbytes + legs;
     if (lds > ctx->max_lds) {
       a.si.mat_lds = 0;
-      lds = inst_lds_bytes_host(a.si) + 4 * wbytes + legs;
+      lds = inst_lds_bytes_host(a.si) + cpw * wbytes + legs;
     }
-    if (lds <= ctx->max_lds)
-      return launch_inst<RouteK>(ctx, dim3((p->chains + 3) / 4), dim3(256), lds,
-                                 (hipStream_t)stream, a);
+    if (lds <= ctx->max_lds) {
+      const dim3 grid(wpc > 1 ? p->chains : (p->chains + 3) / 4), block(wpc > 1 ? 64 * wpc : 256);
+      return launch_inst<RouteK>(ctx, grid, block, lds, (hipStream_t)stream, a);
+    }
   }
+  if (wpc > 1)
+    return fail(VRPMS_EINVAL,
+                "vrpms_sa_run: moves > 64 needs the route-local kernel (window > 0, CVRP, one "
+                "capacity and start time, every demand fits a vehicle)");
   const size_t npad = ((size_t)n + 7) & ~(size_t)7;
   size_t lds = inst_lds_bytes_host(a.si) + 4 * 3 * npad * 2;
   if (lds > ctx->max_lds) {

@@ -71,7 +71,8 @@ class SARunner(_Base):
     (CVRP) ride in every tour, so the moves also place route boundaries;
     tours then hold n + n_sep tokens (self.n).  `window` > 0 samples A11
     windowed moves of the A12 types `window_types` (0 = all; priced
-    route-locally on an exchangeable fleet).  `start` places the separators:
+    route-locally on an exchangeable fleet; `moves` = 64 W samples per step
+    on W wavefronts per chain).  `start` places the separators:
     "random" (Philox tokens), "greedy" (where the greedy split of a random
     order closes routes) or "pack" (first-fit routes of a random order, a
     feasible start when the fleet has little spare capacity)."""
@@ -79,10 +80,11 @@ class SARunner(_Base):
     def __init__(self, ctx: Context, n: int, chains: int = 1024, seed: int = 0,
                  total_steps: int = 2000, steps_per_epoch: int = 250, t0: float | None = None,
                  t_end: float | None = None, durations=None, n_sep: int = 0, window: int = 0,
-                 window_types: int = 0, start: str = "random"):
+                 window_types: int = 0, start: str = "random", moves: int = 64):
         torch = _torch()
         self.ctx, self.n, self.seed = ctx, n + n_sep, seed
         self.n_sep, self.window, self.window_types = n_sep, window, window_types
+        self.moves = moves
         self.chains = chains
         edge = typical_edge(durations) if durations is not None else 100.0
         t0 = t0 if t0 is not None else 0.5 * edge
@@ -105,7 +107,7 @@ class SARunner(_Base):
         s = self.steps_per_epoch if steps is None else steps
         self.ctx.sa_run(self.cur, self.cur_key, self.best_t, self.best_key, s, float(self.inv_t),
                         float(self.inv_alpha), self.seed, self.step, window=self.window,
-                        window_types=self.window_types)
+                        window_types=self.window_types, moves=self.moves)
         for _ in range(s):      # same float32 recurrence as the kernel
             self.inv_t = np.float32(self.inv_t * self.inv_alpha)
         self.step += s
