@@ -147,7 +147,7 @@ class _TimedCooling:
 
 def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label="cvrp100_k8 seed 0",
             gpu_seed=None, n_sep=None, window=0, window_types=0, start="random", moves=64,
-            cpu_moves=64):
+            cpu_moves=64, gpu=True):
     """Best-cost gap at fixed wall time (the metric's second half): the same SA
     (Philox streams, 64 sampled moves per step, geometric cooling from
     0.5 to 0.002 x the mean edge spread over the wall-time budget by

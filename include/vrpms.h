@@ -138,6 +138,12 @@ int vrpms_eval_path(vrpms_ctx* ctx, int32_t perm_bytes, int64_t ld, const void* 
  *   moves route-locally, sa_route_kernel), 2 = force full re-evaluation of
  *   every move (sa_kernel); A/B. */
 #define VRPMS_OPT_SA_ROUTE 8
+/*   VRPMS_OPT_ROUTE_WG_PER_CU: workgroups of sa_route_kernel per CU (0 =
+ *   auto: 1 for multi-wavefront chains, whose LDS request is padded past
+ *   half the CU so each wavefront has a SIMD to itself -- the pricing walk
+ *   is VALU-issue bound, so a lone wavefront steps up to twice as fast --
+ *   and as many as fit for one-wavefront chains; 1 or 2 force). */
+#define VRPMS_OPT_ROUTE_WG_PER_CU 9
 int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value);
 
 /* Decode ONE giant tour into the result dict of api/vrp/ga/index.py:49-53

@@ -45,6 +45,9 @@ def main():
                     help="GPU moves per step (64 W: W wavefronts per chain)")
     ap.add_argument("--cpu-moves", type=int, nargs="+", default=[64],
                     help="host moves per step; several values: each cell reports the host's best")
+    ap.add_argument("--wg-per-cu", type=int, default=0,
+                    help="sa_route_kernel workgroups per CU (0 = auto)")
+    ap.add_argument("--no-cpu", action="store_true", help="GPU legs only (parameter scans)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "quality_sweep.json"))
     args = ap.parse_args()
 
@@ -55,7 +58,9 @@ def main():
 
     torch.cuda.set_device(0)
     ctx = Context(0)
+    ctx.set_route_wg_per_cu(args.wg_per_cu)
     cells = []
+    summary = {}
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     t_start = time.time()
     make = {"cvrp100": lambda s: synth.cvrp(100, 8, seed=s),
@@ -68,13 +73,18 @@ def main():
             window = args.window if args.window is not None else (
                 0 if args.instance == "cvrp100" else 32)
             chains = args.chains or (4096 if args.instance == "cvrp100" else 2048) * 64 // args.moves
-            q = bench.quality(ctx, inst, T, 1, 0, None, with_cpu=True, chains=chains,
+            q = bench.quality(ctx, inst, T, 1, 0, None, with_cpu=not args.no_cpu, chains=chains,
                               moves=args.moves, cpu_moves=args.cpu_moves[0],
                               label=f"{args.instance} seed {seed}", n_sep=args.sep,
                               window=window,
                               window_types=args.types if args.types is not None else 2,
                               start=args.start or ("random" if args.instance == "cvrp100"
                                                    else "pack"))
+            if args.no_cpu:
+                print(json.dumps({"seed": seed, "T_s": T, "moves": args.moves, "chains": chains,
+                                  "gpu": q["gpu"]["duration_sum"],
+                                  "steps_per_chain": q["gpu"]["steps_per_chain"]}), flush=True)
+                continue
             print(json.dumps({"progress": f"seed {seed} T {T}: gpu {q['gpu']['duration_sum']} "
                                           f"cpu(m={args.cpu_moves[0]}) {q['cpu']['duration_sum']}"}),
                   flush=True)
@@ -115,7 +125,8 @@ def main():
                            "start": cells[0]["start"],
                            "cpu_cores": cells[0]["cpu"]["cores"],
                            "summary": summary, "cells": cells}, f, indent=1)
-    print(json.dumps({"summary": summary}), flush=True)
+    if cells:
+        print(json.dumps({"summary": summary}), flush=True)
 
 
 if __name__ == "__main__":

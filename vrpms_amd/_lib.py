@@ -32,6 +32,7 @@ OPT_WORDS_LOOKAHEAD = 5
 OPT_ROWS_CONFIG = 6
 OPT_GA_FUSED = 7
 OPT_SA_ROUTE = 8
+OPT_ROUTE_WG_PER_CU = 9
 OBJ_SUM = 0
 OBJ_MAX = 1
 INJECT_WORST = 0

@@ -174,6 +174,11 @@ class Context:
         """0 = auto (route-local move pricing for windowed SA), 2 = full re-evaluation."""
         check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_SA_ROUTE, int(mode)))
 
+    def set_route_wg_per_cu(self, wg: int):
+        """sa_route_kernel workgroups per CU: 0 = auto (1 for multi-wavefront
+        chains), 1 or 2 force."""
+        check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_ROUTE_WG_PER_CU, int(wg)))
+
     def set_ga_fused(self, mode: int):
         """0 = auto (fused one-workgroup-per-island GA when it fits), 2 = three kernels."""
         check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_GA_FUSED, int(mode)))

@@ -234,6 +234,12 @@ int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value) {
     ctx->opt_sa_route = value;
     return VRPMS_OK;
   }
+  if (option == VRPMS_OPT_ROUTE_WG_PER_CU) {
+    if (value < 0 || value > 2)
+      return fail(VRPMS_EINVAL, "vrpms_set_option: route workgroups per CU must be 0 (auto), 1 or 2");
+    ctx->opt_route_wg_per_cu = value;
+    return VRPMS_OK;
+  }
   if (option == VRPMS_OPT_GA_FUSED) {
     if (value != 0 && value != 2)
       return fail(VRPMS_EINVAL, "vrpms_set_option: GA fused must be 0 (auto) or 2 (three kernels)");

@@ -50,6 +50,7 @@ struct vrpms_ctx {
   size_t max_lds = 160 * 1024;
   int opt_split_mode = 0;       // VRPMS_OPT_SPLIT_MODE (0 auto, 2 force branchy)
   int opt_staged_m = 0;         // VRPMS_OPT_STAGED_M (0 auto, 1, 2 or 3)
+  int opt_route_wg_per_cu = 0;  // sa_route_kernel workgroups per CU (0 auto, 1, 2)
   int opt_words_ilp = 0;        // candidates per lane in eval_cvrp_words2 (0 auto, 1, 2 or 3)
   int opt_words_lookahead = 0;  // VRPMS_OPT_WORDS_LOOKAHEAD (words2 gather lookahead, A/B)
   int opt_words_kernel = 0;     // VRPMS_OPT_WORDS_KERNEL (0 auto = words2/rows2, 1 = first generation)

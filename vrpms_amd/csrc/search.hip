@@ -447,9 +447,12 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
   };
   auto close = [&](Walk& w) -> uint32_t {  // returns the closed route's duration
     uint32_t rd = 0;
-    if (w.prev) {
-      if constexpr (HM == 1) w.t += w.pret;
-      else w.t += I.D(w.t, w.prev, 0);
+    if constexpr (HM == 1) {  // branch-free: the return leg rides in pret
+      rd = w.prev ? (uint32_t)(w.t + w.pret - st0) : 0u;
+      w.ds += rd;
+      w.dm = max(w.dm, rd);
+    } else if (w.prev) {
+      w.t += I.D(w.t, w.prev, 0);
       rd = (uint32_t)(w.t - st0);
       w.ds += rd;
       w.dm = max(w.dm, rd);
@@ -713,15 +716,13 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
       auto close_rec = [&](Walk& ww, int next) {
         close(ww);
         const uint32_t off = (uint32_t)(next - zbase);
-        if (off >= 128u) zovf = true;
-        const uint64_t b = 1ull << (off & 63u);
-        if (off < 64u) {
-          if (z2) zm[2] |= b;
-          else zm[0] |= b;
-        } else if (off < 128u) {
-          if (z2) zm[3] |= b;
-          else zm[1] |= b;
-        }
+        zovf = zovf || off >= 128u;
+        const uint64_t b = off < 128u ? 1ull << (off & 63u) : 0ull;
+        const uint64_t bl0 = off < 64u ? b : 0ull, bh0 = off < 64u ? 0ull : b;
+        zm[0] |= z2 ? 0ull : bl0;
+        zm[1] |= z2 ? 0ull : bh0;
+        zm[2] |= z2 ? bl0 : 0ull;
+        zm[3] |= z2 ? bh0 : 0ull;
       };
       // The walk goes in blocks of kBlk tokens: their tokens and demands,
       // depot legs and route-start bits are read from LDS, and on a static
@@ -738,7 +739,7 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
         ++wblk;
 #endif
         uint32_t cb[kBlk];
-        int db[kBlk], eb[kBlk];
+        int db[kBlk], eb[kBlk], ob[kBlk], rb[kBlk];
 #pragma unroll
         for (int i = 0; i < kBlk; ++i) {
           const int qq = q + i;
@@ -755,8 +756,10 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
             e = qq == hi ? jx2 : e;
             e = qq == hi + 1 ? jx3 : e;
             eb[i] = e;
+            ob[i] = leg_out(cb[i]);
+            rb[i] = leg_ret(cb[i]);
           } else {
-            eb[i] = 0;
+            eb[i] = ob[i] = rb[i] = 0;
           }
         }
         // route-start bits at the current tour's positions of the middle
@@ -766,52 +769,82 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
                                     : 0ull;
         const uint64_t wa = (((uint64_t)T.bits[(q >> 5) + 1] << 32) | T.bits[q >> 5]) >> (q & 31);
         int adv = kBlk;
+        // Each token is straight-line predicated code: a lane that leaves the
+        // block early sets `stop`, and the rare events that end a zone (back
+        // in step in the middle: the second zone starts; back in step after
+        // both ends: the walk is done) are applied after the block, so the
+        // unrolled tokens carry no loop exits and no copies of the walk state.
+        bool stop = false;
+        int ev = 0, evq = 0;  // event (1: zone switch, 2: done) and its position
 #pragma unroll
         for (int i = 0; i < kBlk; ++i) {
           const int qq = q + i;
-          if (qq >= n) {  // blocks start at or before n: qq == n here
+          const uint32_t c = cb[i];
+          if (!stop && qq >= n) {  // blocks start at or before n: qq == n here
             fin = true;
             adv = i;
-            break;
+            stop = true;
           }
-          const uint32_t c = cb[i];
           // back in step at a route start of the current tour: the walk's
           // route is fresh there, or the customer there does not fit (a
           // separator would close the walk's route, not the tour's empty one)
           const bool nofit = c != 0 && w.load + db[i] > cap0;
-          if (phase == 1 && qq >= bq0) {  // the middle: moved(qq) = A[qq - dl]
-            if (((wm >> i) & 1u) && (w.prev == 0 || nofit)) {
-              if (w.prev != 0) close_rec(w, qq);  // the token opens a route in both tours
-              w1 = w;
-              r1e = T.rid[qq - dl];
-              q1 = qq;
-              fresh(w);
-              phase = 2;
-              z2 = true;
-              zbase = Z2;
-              adv = Z2 - q;  // the second zone starts fresh at Z2
-              break;
-            }
-            if (qq == Z2) phase = 3;  // never back in step before the second end
-          }
-          if (phase >= 2 && qq > hi) {  // after both ends: moved(qq) = A[qq]
-            if (((wa >> i) & 1u) && (w.prev == 0 || nofit)) {
-              if (w.prev != 0) close_rec(w, qq);
-              r2e = T.rid[qq];
-              fin = true;
-              adv = i;
-              break;
-            }
-          }
-          if (c == 0) {
-            close_rec(w, qq + 1);  // the separator ends the walk's route
-          } else {
-            if (nofit) close_rec(w, qq);
-            add(w, c, db[i], eb[i]);
+          const bool insync = w.prev == 0 || nofit;
+          const bool mid = !stop && phase == 1 && qq >= bq0;  // moved(qq) = A[qq - dl]
+          const bool sw = mid && ((wm >> i) & 1u) && insync;
+          phase = mid && !sw && qq == Z2 ? 3 : phase;  // never back in step before the second end
+          const bool done = !stop && !sw && phase >= 2 && qq > hi && ((wa >> i) & 1u) && insync;
+          ev = sw ? 1 : done ? 2 : ev;
+          evq = sw || done ? qq : evq;
+          const bool act = !stop && !sw && !done;
+          stop = stop || sw || done;
+          // a separator ends the walk's route (the next one starts after it);
+          // a customer that does not fit closes it and opens the next
+          if constexpr (HM == 1) {
+            const bool closing = act && (c == 0 || nofit);
+            const uint32_t rd = closing && w.prev ? (uint32_t)(w.t + w.pret - st0) : 0u;
+            w.ds += rd;
+            w.dm = max(w.dm, rd);
+            w.cnt += closing ? 1u : 0u;
+            const uint32_t off = (uint32_t)((c == 0 ? qq + 1 : qq) - zbase);
+            zovf = zovf || (closing && off >= 128u);
+            const uint64_t bb = closing && off < 128u ? 1ull << (off & 63u) : 0ull;
+            const uint64_t bl0 = off < 64u ? bb : 0ull, bh0 = off < 64u ? 0ull : bb;
+            zm[0] |= z2 ? 0ull : bl0;
+            zm[1] |= z2 ? 0ull : bh0;
+            zm[2] |= z2 ? bl0 : 0ull;
+            zm[3] |= z2 ? bh0 : 0ull;
+            const int t0 = closing ? st0 : w.t, l0 = closing ? 0 : w.load;
+            const uint32_t p0 = closing ? 0u : w.prev;
+            const bool addf = act && c != 0;
+            w.t = addf ? t0 + (p0 ? eb[i] : ob[i]) : t0;
+            w.load = addf ? l0 + db[i] : l0;
+            w.prev = addf ? c : p0;
+            w.pret = addf ? rb[i] : w.pret;
+            w.xs = addf ? (int)w.cnt : w.xs;
+          } else if (act) {
+            if (c == 0 || nofit) close_rec(w, c == 0 ? qq + 1 : qq);
+            if (c != 0) add(w, c, db[i], eb[i]);
           }
 #ifdef VRPMS_ROUTE_PROF
-          ++wtok;
+          if (act) ++wtok;
 #endif
+        }
+        if (ev == 1) {  // back in step in the middle: the second zone starts fresh at Z2
+          if (w.prev != 0) close_rec(w, evq);  // the token opens a route in both tours
+          w1 = w;
+          r1e = T.rid[evq - dl];
+          q1 = evq;
+          fresh(w);
+          phase = 2;
+          z2 = true;
+          zbase = Z2;
+          adv = Z2 - q;
+        } else if (ev == 2) {  // back in step after both ends
+          if (w.prev != 0) close_rec(w, evq);
+          r2e = T.rid[evq];
+          fin = true;
+          adv = evq - q;
         }
         q += adv;
       }
@@ -2102,6 +2135,9 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
       lds = inst_lds_bytes_host(a.si) + cpw * wbytes + legs;
     }
     if (lds <= ctx->max_lds) {
+      // one workgroup per CU: request more than half the CU's LDS
+      const int per_cu = ctx->opt_route_wg_per_cu ? ctx->opt_route_wg_per_cu : (wpc > 1 ? 1 : 2);
+      if (per_cu == 1) lds = std::max(lds, ctx->max_lds / 2 + 16);
       const dim3 grid(wpc > 1 ? p->chains : (p->chains + 3) / 4), block(wpc > 1 ? 64 * wpc : 256);
       return launch_inst<RouteK>(ctx, grid, block, lds, (hipStream_t)stream, a);
     }
