@@ -33,6 +33,7 @@ for step in "$@"; do
     probe) run sa_probe 300 python tools/sa_probe.py ;;
     quality) run quality_sweep 1100 python -u tools/quality_sweep.py ;;
     quality_short) run quality_sweep 400 python -u tools/quality_sweep.py --T 1 10 ;;
+    qcustom) run quality_custom 1100 python -u tools/quality_sweep.py $QARGS ;;
     prof)
       cd /tmp
       run rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv \
