@@ -347,6 +347,38 @@ def test_aco_iterations_match_oracle(ctx, name, maker):
         assert all((got_tau[c] == rtau[c]).all() for c in range(colonies))
 
 
+ACO_SIZES = [
+    # register path, 1 / 2 / 4 chunks of 64 nodes per lane (words layout for CVRP), and the
+    # LDS path past 256 nodes
+    ("tsp60", lambda: synth.Instance("tsp60", synth.random_symmetric(60, np.random.default_rng(3))[None],
+                                     None, None, np.array([0]), "tsp")),
+    ("cvrp100", lambda: synth.cvrp(100, 8, seed=0)),
+    ("cvrp150", lambda: synth.cvrp(150, 12, seed=2)),
+    ("cvrp300", lambda: synth.cvrp(300, 24, seed=5)),
+]
+
+
+@pytest.mark.parametrize("name,maker", ACO_SIZES, ids=[s[0] for s in ACO_SIZES])
+def test_aco_iterations_match_oracle_at_size(ctx, name, maker):
+    inst = maker()
+    load(ctx, inst)
+    colonies, ants, tau0 = 2, 8, 1 << 20
+    tau, eta = ctx.aco_init(colonies, tau0)
+    ref_eta = search.aco_eta(inst.durations[0])
+    rtau = [np.full((inst.N, inst.N), tau0, dtype=np.int64) for _ in range(colonies)]
+    sc = scorer(inst)
+    for it in range(2):
+        tours, keys, ib = ctx.aco_iteration(tau, eta, ants, seed=11, it=it, evap_shift=3,
+                                            tau_min=1 << 10, tau_max=1 << 30)
+        rt, rk, rib = search.aco_iteration(sc, rtau, ref_eta, ants, inst.n, 11, it, 3, 1 << 10,
+                                           1 << 30)
+        assert tours.cpu().numpy().tolist() == rt
+        assert u64(keys) == [k for ks in rk for k in ks]
+        assert [(a & (2**64 - 1), b) for a, b in ib.cpu().tolist()] == rib
+        got_tau = tau.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+        assert all((got_tau[c] == rtau[c]).all() for c in range(colonies))
+
+
 @pytest.mark.parametrize("name,maker", SMALL, ids=[s[0] for s in SMALL])
 def test_bf_matches_oracle(ctx, name, maker):
     inst = maker()

@@ -27,6 +27,7 @@ run() {  # name, seconds, cmd...
 for step in "$@"; do
   case $step in
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    tsel) run pytest_sel 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread -k "$TSEL" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     benchq) run bench_quick 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;

@@ -106,7 +106,7 @@ VRPMS_DEV int tourney2(const uint64_t* keys, int pop, uint32_t r0, uint32_t r1) 
 __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int P = a.pop, n = a.n, island = blockIdx.x;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const uint32_t rs = a.rs;
   const uint32_t words = ((uint32_t)a.f.N + 31u) / 32u;
   uint8_t* rows = smem + a.off_rows;

@@ -131,7 +131,7 @@ __global__ __launch_bounds__(256) void sa_kernel(SaArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const StagedInst<MatT, HM> I = stage_inst<MatT, HM>(a.si, smem);
   const int n = a.n;
-  const int wave = threadIdx.x >> 6, lane = lane_id();
+  const int wave = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
   const int chain = blockIdx.x * 4 + wave;
   const uint32_t npad = ((uint32_t)n + 7u) & ~7u;
   uint16_t* buf = reinterpret_cast<uint16_t*>(smem + inst_lds_bytes(a.si)) + wave * 3 * npad;
@@ -326,7 +326,7 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
 #endif
   const StagedInst<MatT, HM> I = stage_inst<MatT, HM>(a.si, smem);
   const int n = a.n;
-  const int wave = threadIdx.x >> 6, lane = lane_id();
+  const int wave = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
   // W = 1: four chains per workgroup, one wavefront each.  W > 1: one chain
   // per workgroup, its W wavefronts price 64 W moves per step (move index
   // lane + 64 cw), the (key, index) minimum meets in LDS, and the winning
@@ -1304,7 +1304,7 @@ __global__ __launch_bounds__(1024) void sa_packed_kernel(SaPackedArgs a) {
   }
   __syncthreads();
   const int n = a.n;
-  const int wave = threadIdx.x >> 6, lane = lane_id();
+  const int wave = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
   const int chain = blockIdx.x * kSaPackedWaves + wave;
   if (chain >= a.chains) return;  // no block-wide barrier after this point
   const uint32_t N8 = 8u * (uint32_t)N, tb = a.tb;
@@ -1402,7 +1402,7 @@ VRPMS_DEV int tourney(const uint64_t* keys, int pop, uint32_t r0, uint32_t r1) {
 template <bool WORDS>
 __global__ __launch_bounds__(256) void ga_breed_kernel(GaBreedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int wave = threadIdx.x >> 6, lane = lane_id();
+  const int wave = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
   const int64_t gid = (int64_t)blockIdx.x * 4 + wave;  // child id = island * pop + i
   const int n = a.n;
   const uint32_t words = ((uint32_t)a.N + 31u) / 32u;
@@ -1587,11 +1587,21 @@ struct AcoArgs {
 // WORDS (n <= 255): the ant's tour is also kept in a wave-private LDS byte
 // buffer and written out in the word-interleaved layout, so the colony is
 // scored by eval_cvrp_words2 (the headline kernel).
-template <bool WORDS>
+//
+// CH > 0 (N <= 64 CH): lane l owns nodes l + 64c (c < CH) -- their visited
+// bits in a register mask and their weights in registers -- so a step is ONE
+// gather round trip for the tau / eta row (the LDS path below gathers the row
+// twice, once per pass), one DPP scan per chunk whose row totals give the
+// colony total, and ballots for the first free node and the pick: no LDS
+// visited set, no atomics, no wave barriers inside the construction.  Same
+// weights, same sums (exact integers), same pick as the LDS path.
+template <bool WORDS, int CH>
 __global__ __launch_bounds__(256) void aco_construct_kernel(AcoArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int wave = threadIdx.x >> 6, lane = lane_id();
-  const int64_t gid = (int64_t)blockIdx.x * 4 + wave;
+  const int wave = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
+  // wave-uniform in SGPRs (threadIdx.x >> 6 is not uniform to the compiler),
+  // so the ant's Philox blocks and row addresses run on the scalar unit
+  const int64_t gid = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(wave);
   const int N = a.N, n = a.n;
   const uint32_t words = ((uint32_t)N + 31u) / 32u;
   uint32_t* vis = reinterpret_cast<uint32_t*>(smem) + wave * words;
@@ -1604,65 +1614,121 @@ __global__ __launch_bounds__(256) void aco_construct_kernel(AcoArgs a) {
   const int colony = (int)(gid / a.ants), ant = (int)(gid % a.ants);
   const uint32_t* T = a.tau + (int64_t)colony * N * N;
   uint16_t* out = a.tours + gid * n;
-  for (uint32_t w = lane; w < words; w += 64) vis[w] = 0u;
-  wave_sync();
-  if (lane == 0) atomicOr(&vis[0], 1u);  // depot
-  wave_sync();
-  uint32_t cur = 0;
-  for (int s = 0; s < n; ++s) {
-    const u32x4 r = philox((uint32_t)a.iter, (uint32_t)(a.iter >> 32),
-                           (uint32_t)(colony * a.ants + ant), (uint32_t)s, a.seed_lo, a.seed_hi);
-    const uint32_t* Tr = T + (int64_t)cur * N;
-    const uint32_t* Er = a.eta + (int64_t)cur * N;
-    // pass 1: total weight (integer, so the order of summation is irrelevant)
-    uint64_t tot = 0;
-    int first_free = INT_MAX;
-    for (int j = lane; j < N; j += 64) {
-      if (!((vis[j >> 5] >> (j & 31)) & 1u)) {
-        tot += (uint64_t)(Tr[j] >> 8) * Er[j];
-        first_free = min(first_free, j);
+  if constexpr (CH > 0) {
+    uint32_t vm = lane == 0 ? 1u : 0u;  // bit c: node lane + 64c visited (or past N); depot
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+      if (lane + 64 * c >= N) vm |= 1u << c;
+    uint32_t cur = 0;
+    for (int s = 0; s < n; ++s) {
+      const u32x4 r = philox((uint32_t)a.iter, (uint32_t)(a.iter >> 32),
+                             (uint32_t)(colony * a.ants + ant), (uint32_t)s, a.seed_lo, a.seed_hi);
+      const uint32_t* Tr = T + (int64_t)cur * N;
+      const uint32_t* Er = a.eta + (int64_t)cur * N;
+      uint32_t tv[CH], ev[CH];
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const bool fr = !((vm >> c) & 1u);
+        tv[c] = fr ? Tr[lane + 64 * c] : 0u;
+        ev[c] = fr ? Er[lane + 64 * c] : 0u;
       }
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-      tot += __shfl_xor(tot, off, 64);
-      first_free = min(first_free, __shfl_xor(first_free, off, 64));
-    }
-    uint32_t pick;
-    if (tot == 0) {
-      pick = (uint32_t)first_free;
-    } else {
-      const uint64_t rr = (((uint64_t)r.y << 32) | r.x) % tot;
-      // pass 2: scan chunks of 64 consecutive j; lane-level inclusive prefix
-      uint64_t run = 0;
-      pick = 0xffffffffu;
-      for (int base = 0; base < N && pick == 0xffffffffu; base += 64) {
-        const int j = base + lane;
-        uint64_t w = 0;
-        if (j < N && !((vis[j >> 5] >> (j & 31)) & 1u)) w = (uint64_t)(Tr[j] >> 8) * Er[j];
-        uint64_t inc = w;
-        for (int off = 1; off < 64; off <<= 1) {
-          const uint64_t o = __shfl_up(inc, off, 64);
-          if (lane >= off) inc += o;
+      uint64_t w[CH], inc[CH], ct[CH], tot = 0;
+      uint32_t pick = 0xffffffffu;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        w[c] = (uint64_t)(tv[c] >> 8) * ev[c];
+        inc[c] = w[c];
+        ct[c] = wave_scan_add_u64(inc[c]);
+        tot += ct[c];
+        const uint64_t fb = __ballot(!((vm >> c) & 1u));
+        if (pick == 0xffffffffu && fb) pick = (uint32_t)(64 * c + __ffsll((long long)fb) - 1);
+      }
+      if (tot != 0) {  // else: the first free node
+        const uint64_t rr = umod64(((uint64_t)r.y << 32) | r.x, tot);
+        uint64_t run = 0;
+        uint32_t hp = 0xffffffffu;
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+          const uint64_t ball = __ballot(w[c] > 0 && run + inc[c] > rr);
+          if (hp == 0xffffffffu && ball) hp = (uint32_t)(64 * c + __ffsll((long long)ball) - 1);
+          run += ct[c];
         }
-        const bool hit = w > 0 && run + inc > rr;
-        const uint64_t ball = __ballot(hit);
-        if (ball) pick = (uint32_t)(base + __ffsll((long long)ball) - 1);
-        run += __shfl(inc, 63, 64);
+        if (hp != 0xffffffffu) pick = hp;  // always: tot > rr
       }
-      if (pick == 0xffffffffu) pick = (uint32_t)first_free;  // unreachable: tot > rr
+      if (lane == 0) {
+        out[s] = (uint16_t)pick;
+        if constexpr (WORDS) tbuf[s] = (uint8_t)pick;
+      }
+      if (lane == (int)(pick & 63u)) vm |= 1u << (pick >> 6);
+      cur = pick;
     }
-    if (lane == 0) {
-      out[s] = (uint16_t)pick;
-      if constexpr (WORDS) tbuf[s] = (uint8_t)pick;
-      atomicOr(&vis[pick >> 5], 1u << (pick & 31u));
+    if constexpr (WORDS) {
+      wave_sync();
+      const int nw = (n + 3) >> 2;
+      for (int w = lane; w < nw; w += 64)
+        a.words[(int64_t)w * total_ants + gid] = reinterpret_cast<const uint32_t*>(tbuf)[w];
     }
+  } else {  // LDS path (N > 256): visited bits in LDS, the row gathered once per pass
+    for (uint32_t w = lane; w < words; w += 64) vis[w] = 0u;
     wave_sync();
-    cur = pick;
-  }
-  if constexpr (WORDS) {
-    const int nw = (n + 3) >> 2;
-    for (int w = lane; w < nw; w += 64)
-      a.words[(int64_t)w * total_ants + gid] = reinterpret_cast<const uint32_t*>(tbuf)[w];
+    if (lane == 0) atomicOr(&vis[0], 1u);  // depot
+    wave_sync();
+    uint32_t cur = 0;
+    for (int s = 0; s < n; ++s) {
+      const u32x4 r = philox((uint32_t)a.iter, (uint32_t)(a.iter >> 32),
+                             (uint32_t)(colony * a.ants + ant), (uint32_t)s, a.seed_lo, a.seed_hi);
+      const uint32_t* Tr = T + (int64_t)cur * N;
+      const uint32_t* Er = a.eta + (int64_t)cur * N;
+      // pass 1: total weight (integer, so the order of summation is irrelevant)
+      uint64_t tot = 0;
+      int first_free = INT_MAX;
+      for (int j = lane; j < N; j += 64) {
+        if (!((vis[j >> 5] >> (j & 31)) & 1u)) {
+          tot += (uint64_t)(Tr[j] >> 8) * Er[j];
+          first_free = min(first_free, j);
+        }
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        tot += __shfl_xor(tot, off, 64);
+        first_free = min(first_free, __shfl_xor(first_free, off, 64));
+      }
+      uint32_t pick;
+      if (tot == 0) {
+        pick = (uint32_t)first_free;
+      } else {
+        const uint64_t rr = (((uint64_t)r.y << 32) | r.x) % tot;
+        // pass 2: scan chunks of 64 consecutive j; lane-level inclusive prefix
+        uint64_t run = 0;
+        pick = 0xffffffffu;
+        for (int base = 0; base < N && pick == 0xffffffffu; base += 64) {
+          const int j = base + lane;
+          uint64_t w = 0;
+          if (j < N && !((vis[j >> 5] >> (j & 31)) & 1u)) w = (uint64_t)(Tr[j] >> 8) * Er[j];
+          uint64_t inc = w;
+          for (int off = 1; off < 64; off <<= 1) {
+            const uint64_t o = __shfl_up(inc, off, 64);
+            if (lane >= off) inc += o;
+          }
+          const bool hit = w > 0 && run + inc > rr;
+          const uint64_t ball = __ballot(hit);
+          if (ball) pick = (uint32_t)(base + __ffsll((long long)ball) - 1);
+          run += __shfl(inc, 63, 64);
+        }
+        if (pick == 0xffffffffu) pick = (uint32_t)first_free;  // unreachable: tot > rr
+      }
+      if (lane == 0) {
+        out[s] = (uint16_t)pick;
+        if constexpr (WORDS) tbuf[s] = (uint8_t)pick;
+        atomicOr(&vis[pick >> 5], 1u << (pick & 31u));
+      }
+      wave_sync();
+      cur = pick;
+    }
+    if constexpr (WORDS) {
+      const int nw = (n + 3) >> 2;
+      for (int w = lane; w < nw; w += 64)
+        a.words[(int64_t)w * total_ants + gid] = reinterpret_cast<const uint32_t*>(tbuf)[w];
+    }
   }
 }
 
@@ -1886,7 +1952,7 @@ VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, bool symmetr
                               unsigned char* work) {
   const int N = a.N, n = N - 1, r = blockIdx.x;
   const uint32_t npad = ((uint32_t)n + 7u) & ~7u;
-  const int wave = threadIdx.x >> 6, lane = lane_id();
+  const int wave = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
   uint16_t* buf = reinterpret_cast<uint16_t*>(work) + wave * 3 * npad;
   uint64_t* wbest = reinterpret_cast<uint64_t*>(work + 4 * 3 * npad * 2);
   uint16_t* A = buf;
@@ -2274,10 +2340,16 @@ extern "C" int vrpms_aco_iteration(vrpms_ctx* ctx, const vrpms_aco_params* p, ui
   AcoArgs c{p->colonies, p->ants, n, in.N, (uint32_t)p->seed, (uint32_t)(p->seed >> 32), p->iter,
             d_tau, d_eta, d_tours, wbuf};
   const size_t lds = ((4 * (((size_t)in.N + 31) / 32) * 4 + 15) & ~(size_t)15) + (words ? 4 * 256 : 0);
-  if (words)
-    aco_construct_kernel<true><<<(unsigned)((ants + 3) / 4), 256, lds, s>>>(c);
-  else
-    aco_construct_kernel<false><<<(unsigned)((ants + 3) / 4), 256, lds, s>>>(c);
+  const dim3 grid((unsigned)((ants + 3) / 4));
+  auto construct = [&](auto wtag) {
+    constexpr bool WD = decltype(wtag)::value;
+    if (in.N <= 64) aco_construct_kernel<WD, 1><<<grid, 256, lds, s>>>(c);
+    else if (in.N <= 128) aco_construct_kernel<WD, 2><<<grid, 256, lds, s>>>(c);
+    else if (in.N <= 256) aco_construct_kernel<WD, 4><<<grid, 256, lds, s>>>(c);
+    else aco_construct_kernel<WD, 0><<<grid, 256, lds, s>>>(c);
+  };
+  if (words) construct(std::true_type{});
+  else construct(std::false_type{});
   VRPMS_HIP(hipGetLastError());
   if (words) {
     WordsArgs w{f, wbuf, ants, n, d_keys, nullptr, nullptr, nullptr, ants, 1u};
