@@ -1740,6 +1740,70 @@ struct AcoUpdateArgs {
   const uint64_t* ib;            // [colonies][2] iteration-best (key, ant)
 };
 
+// The end of an iteration for small matrices (N <= 256), one workgroup per
+// colony instead of four launches: the colony's iteration-best (key, ant)
+// (lowest ant on ties, as segment_argmin_kernel), its best-so-far when
+// strictly better (aco_track_best_kernel), evaporation of its tau, then the
+// deposit on the iteration-best tour (aco_deposit_kernel) -- colonies share
+// nothing, so the per-colony order is the whole order.
+__global__ __launch_bounds__(1024) void aco_update_fused_kernel(AcoUpdateArgs a, const uint64_t* __restrict__ keys,
+                                                               uint64_t* ib, uint16_t* best_tours,
+                                                               uint64_t* best_keys) {
+  const int c = blockIdx.x;
+  uint64_t k = ~0ull, idx = ~0ull;
+  for (int i = threadIdx.x; i < a.ants; i += blockDim.x) {
+    const uint64_t v = keys[(int64_t)c * a.ants + i];
+    if (v < k || (v == k && (uint64_t)i < idx)) {
+      k = v;
+      idx = (uint64_t)i;
+    }
+  }
+  wave_argmin(k, idx);
+  __shared__ uint64_t wk[16], wi[16];
+  const int w = threadIdx.x >> 6;
+  if (lane_id() == 0) {
+    wk[w] = k;
+    wi[w] = idx;
+  }
+  __syncthreads();
+  k = wk[0];
+  idx = wi[0];
+  for (int x = 1; x < (int)(blockDim.x >> 6); ++x)
+    if (wk[x] < k || (wk[x] == k && wi[x] < idx)) {
+      k = wk[x];
+      idx = wi[x];
+    }
+  const uint16_t* t = a.tours + ((int64_t)c * a.ants + (int64_t)idx) * a.n;
+  if (threadIdx.x == 0) {
+    ib[2 * c] = k;
+    ib[2 * c + 1] = idx;
+  }
+  if (best_tours && best_keys && k < best_keys[c]) {  // block-uniform
+    for (int q = threadIdx.x; q < a.n; q += blockDim.x) best_tours[(int64_t)c * a.n + q] = t[q];
+    __syncthreads();
+    if (threadIdx.x == 0) best_keys[c] = k;
+  }
+  // evaporation: 8 loads in flight per thread before the stores
+  uint32_t* T = a.tau + (int64_t)c * a.N * a.N;
+  const int NN = a.N * a.N, B = (int)blockDim.x;
+  for (int base = (int)threadIdx.x; base < NN; base += 8 * B) {
+    uint32_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = base + u * B < NN ? T[base + u * B] : 0u;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (base + u * B < NN) T[base + u * B] = min(a.tau_max, max(a.tau_min, v[u] - (v[u] >> a.evap_shift)));
+  }
+  __syncthreads();
+  const uint32_t primary = (uint32_t)((k >> 28) & ((1u << 28) - 1u));
+  const uint32_t dep = (uint32_t)((1u << 30) / (1ull + primary));
+  for (int q = threadIdx.x; q <= a.n; q += blockDim.x) {
+    const uint32_t from = q == 0 ? 0u : t[q - 1];
+    const uint32_t to = q == a.n ? 0u : t[q];
+    atomicAdd(&T[(uint64_t)from * a.N + to], dep);
+  }
+}
+
 __global__ void aco_evaporate_kernel(AcoUpdateArgs a) {
   const int64_t total = (int64_t)a.colonies * a.N * a.N;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
@@ -2359,12 +2423,18 @@ extern "C" int vrpms_aco_iteration(vrpms_ctx* ctx, const vrpms_aco_params* p, ui
     int rc = vrpms_eval(ctx, d_tours, 2, ants, n, n, d_keys, nullptr, nullptr, nullptr, stream);
     if (rc) return rc;
   }
+  AcoUpdateArgs u{p->colonies, p->ants, n, in.N, (uint32_t)p->evap_shift, p->tau_min, p->tau_max,
+                  d_tau, d_tours, d_iter_best};
+  if (in.N <= 256) {
+    aco_update_fused_kernel<<<p->colonies, 1024, 0, s>>>(
+        u, d_keys, d_iter_best, d_best_keys ? d_best_tours : nullptr, d_best_tours ? d_best_keys : nullptr);
+    VRPMS_HIP(hipGetLastError());
+    return VRPMS_OK;
+  }
   segment_argmin_kernel<<<p->colonies, 256, 0, s>>>(d_keys, p->ants, p->colonies, d_iter_best);
   if (d_best_tours && d_best_keys)
     aco_track_best_kernel<<<p->colonies, 128, 0, s>>>(d_tours, p->ants, n, d_iter_best,
                                                       d_best_tours, d_best_keys);
-  AcoUpdateArgs u{p->colonies, p->ants, n, in.N, (uint32_t)p->evap_shift, p->tau_min, p->tau_max,
-                  d_tau, d_tours, d_iter_best};
   const int64_t total = (int64_t)p->colonies * in.N * in.N;
   aco_evaporate_kernel<<<(unsigned)std::min<int64_t>((total + 255) / 256, ctx->num_cus * 8), 256, 0,
                          s>>>(u);
