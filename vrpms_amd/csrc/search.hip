@@ -776,6 +776,7 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
         // unrolled tokens carry no loop exits and no copies of the walk state.
         bool stop = false;
         int ev = 0, evq = 0;  // event (1: zone switch, 2: done) and its position
+        uint32_t blk = 0;     // route starts closed in this block, bit i = offset q - zbase + i
 #pragma unroll
         for (int i = 0; i < kBlk; ++i) {
           const int qq = q + i;
@@ -806,14 +807,10 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
             w.ds += rd;
             w.dm = max(w.dm, rd);
             w.cnt += closing ? 1u : 0u;
-            const uint32_t off = (uint32_t)((c == 0 ? qq + 1 : qq) - zbase);
-            zovf = zovf || (closing && off >= 128u);
-            const uint64_t bb = closing && off < 128u ? 1ull << (off & 63u) : 0ull;
-            const uint64_t bl0 = off < 64u ? bb : 0ull, bh0 = off < 64u ? 0ull : bb;
-            zm[0] |= z2 ? 0ull : bl0;
-            zm[1] |= z2 ? 0ull : bh0;
-            zm[2] |= z2 ? bl0 : 0ull;
-            zm[3] |= z2 ? bh0 : 0ull;
+            // the next route starts at block offset i (i + 1 after a
+            // separator); zbase and z2 are fixed inside a block, so the bits
+            // go to the zone's mask once, after the block
+            blk |= closing ? (c == 0 ? 2u << i : 1u << i) : 0u;
             const int t0 = closing ? st0 : w.t, l0 = closing ? 0 : w.load;
             const uint32_t p0 = closing ? 0u : w.prev;
             const bool addf = act && c != 0;
@@ -829,6 +826,19 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
 #ifdef VRPMS_ROUTE_PROF
           if (act) ++wtok;
 #endif
+        }
+        if (blk) {  // as close_rec per bit: offsets >= 128 overflow the zone's mask
+          const uint32_t base = (uint32_t)(q - zbase);
+          zovf = zovf || base + 31u - (uint32_t)__builtin_clz(blk) >= 128u;
+          const uint64_t b = blk;
+          const uint64_t lo = base < 64u ? b << base : 0ull;
+          const uint64_t hi = base == 0u ? 0ull
+                              : base < 64u ? b >> (64u - base)
+                              : base < 128u ? b << (base - 64u) : 0ull;
+          zm[0] |= z2 ? 0ull : lo;
+          zm[1] |= z2 ? 0ull : hi;
+          zm[2] |= z2 ? lo : 0ull;
+          zm[3] |= z2 ? hi : 0ull;
         }
         if (ev == 1) {  // back in step in the middle: the second zone starts fresh at Z2
           if (w.prev != 0) close_rec(w, evq);  // the token opens a route in both tours
