@@ -252,7 +252,10 @@ __global__ __launch_bounds__(256) void sa_kernel(SaArgs a) {
 // move re-walks its zones once, recording their routes, and the per-route
 // tables are rebuilt around them.
 // ===========================================================================
-constexpr int kBlk = 8;         // tokens a pricing walk reads (and gathers edges for) at once
+#ifndef VRPMS_KBLK
+#define VRPMS_KBLK 8
+#endif
+constexpr int kBlk = VRPMS_KBLK;  // tokens a pricing walk reads (and gathers edges for) at once
 constexpr int kTourRegs = 18;   // tour positions per lane held in registers on an accept
 
 __host__ __device__ inline int route_max(int K) { return 2 * K + 2; }  // routes stored
