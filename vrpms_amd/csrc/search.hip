@@ -2024,9 +2024,8 @@ struct TspBatchArgs {
 
 // One request's 4 chains over its LDS-resident matrix D (MatT = uint16_t when
 // every entry fits, int32_t otherwise); `work` is the LDS after the matrix.
-template <typename MatT>
-VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, bool symmetric, bool small,
-                              unsigned char* work) {
+template <typename MatT, bool symmetric, bool small>
+VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, unsigned char* work) {
   const int N = a.N, n = N - 1, r = blockIdx.x;
   const uint32_t npad = ((uint32_t)n + 7u) & ~7u;
   const int wave = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
@@ -2066,11 +2065,13 @@ VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, bool symmetr
     const u32x4 rr = philox((uint32_t)s, 0u, cid, (uint32_t)lane, a.seed_lo, a.seed_hi);
     const Move m = decode_move(rr.x, rr.y, rr.z, n);
     auto tourA = [&](int q) { return (uint32_t)A[q]; };
-    const int nd = dur + (symmetric ? tsp_move_delta_sym(dist, tourA, n, m)
-                                    : tsp_move_delta(dist, tourA, n, m, false));
+    int delta;
+    if constexpr (symmetric) delta = tsp_move_delta_sym(dist, tourA, n, m);
+    else delta = tsp_move_delta(dist, tourA, n, m, false);
+    const int nd = dur + delta;
     uint64_t k;
     int bl;
-    if (small) {  // (duration << 6 | lane): the same order as (key, lane)
+    if constexpr (small) {  // (duration << 6 | lane): the same order as (key, lane)
       const uint32_t v = wave_min_u32_uniform(((uint32_t)nd << 6) | (uint32_t)lane);
       bl = (int)(v & 63u);
       k = pack_key(0, v >> 6, 0);
@@ -2140,16 +2141,27 @@ __global__ __launch_bounds__(256) void tsp_batch_sa_kernel(TspBatchArgs a) {
   const bool small = __syncthreads_or(big) == 0;
   const bool narrow = __syncthreads_or(wide) == 0;
   unsigned char* work = smem + ((NN * 4 + 15u) & ~15u);
+  // block-uniform flags as template arguments: one straight step loop each
+  auto run = [&](auto* D) {
+    using MT = std::remove_pointer_t<decltype(D)>;
+    if (symmetric) {
+      if (small) tsp_batch_body<MT, true, true>(a, D, work);
+      else tsp_batch_body<MT, true, false>(a, D, work);
+    } else {
+      if (small) tsp_batch_body<MT, false, true>(a, D, work);
+      else tsp_batch_body<MT, false, false>(a, D, work);
+    }
+  };
   if (narrow) {
     uint16_t* D = reinterpret_cast<uint16_t*>(smem);
     for (uint32_t i = threadIdx.x; i < NN; i += blockDim.x) D[i] = (uint16_t)src[i];
     __syncthreads();
-    tsp_batch_body<uint16_t>(a, D, symmetric, small, work);
+    run(D);
   } else {
     int32_t* D = reinterpret_cast<int32_t*>(smem);
     for (uint32_t i = threadIdx.x; i < NN; i += blockDim.x) D[i] = src[i];
     __syncthreads();
-    tsp_batch_body<int32_t>(a, D, symmetric, small, work);
+    run(D);
   }
 }
 
