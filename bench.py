@@ -54,8 +54,10 @@ def parse():
                     help="target CPU work for the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-other-configs", action="store_true")
-    ap.add_argument("--island-epochs", type=int, default=20,
+    ap.add_argument("--island-epochs", type=int, default=40,
                     help="cfg 4 island-SA leg (all ranks, RCCL elite all-gather); 0 disables")
+    ap.add_argument("--island-steps", type=int, default=500,
+                    help="SA steps per island epoch (40 x 500 ~ 1 s of wall time)")
     ap.add_argument("--quality-seconds", type=float, default=5.0,
                     help="wall time per side for the best-cost gap (0 disables)")
     return ap.parse_args()
@@ -67,6 +69,19 @@ def make_batch(ctx, C, n, seed, dtype=None):
     Philox-seeded") as uint8 rows, generated on the device."""
     import torch
     return ctx.random_tours(C, n, seed, stream_id=0xBE7C, dtype=dtype or torch.uint8)
+
+
+def cpu_model() -> str:
+    """The host CPU model (lscpu's "Model name", from /proc/cpuinfo)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
 
 
 def cpu_baseline(inst, perms_dev, seconds):
@@ -95,6 +110,7 @@ def cpu_baseline(inst, perms_dev, seconds):
         py_n += 1
     py_dt = time.perf_counter() - t0
     return {"value": S * passes / dt, "unit": "evals/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
             "sample": f"{passes} pass(es) over the first {S} of the same CVRP-100 tours, C "
                       f"restatement oracle/oracle_c.c (OpenMP, {threads} threads), "
                       f"{dt:.2f} s",
@@ -309,28 +325,33 @@ def other_configs(ctx, torch, dev, seed=0):
     return out
 
 
-def island_leg(ctx, torch, dev, world, rank, dist, epochs=20, steps=25, chains=1024, E=8,
+def island_leg(ctx, torch, dev, world, rank, dist, epochs=40, steps=500, chains=1024, E=8,
                every=5, seed=0, window=32):
     """BASELINE.json cfg 4 as a search, not a scoring pass: X-style CVRP-1000
     (u16 matrix L2-resident), `chains` SA chains per GPU, a fixed number of
-    epochs with an elite exchange every `every` epochs -- an RCCL all-gather
-    of every rank's E best (tour + key) over xGMI when N > 1, local
-    re-injection at N = 1.  Tours carry K - 1 A10 separators and the moves
-    are A11-windowed, priced route-locally (sa_route_kernel): every sampled
-    move still gets its exact full-tour key.  Every rank runs the same control flow
-    (islands.run_fixed), and a pre-flight all-reduce makes all ranks skip
-    together if any rank failed to set up.  Reports whole-job full-tour
-    evals/s inside the search (every sampled move is a full re-evaluation of
-    the moved tour: 64 per chain-step), the mean exchange time and the
-    global best."""
+    epochs with an elite exchange every `every` epochs through the library's
+    own communicator: vrpms_island_exchange = device top-E, one RCCL
+    ncclAllGather of every rank's E best (tour + key) over xGMI, device merge
+    and injection (islands.init_comm creates it from the torch.distributed
+    group at N > 1; at N = 1 a world-1 communicator, so the same RCCL call
+    runs).  If the communicator cannot be created on every rank, every rank
+    falls back to torch.distributed's all-gather around the same library
+    pack / merge / inject and says so.  Tours carry K - 1 A10 separators
+    from first-fit ("pack") starts and the moves are A11-windowed 2-opt,
+    priced route-locally by sa_route_kernel (only the span a move changes is
+    walked), so the throughput is reported as route-local move evaluations
+    per second -- not comparable with the headline's full-tour evals.  Every
+    rank runs the same control flow (islands.run_fixed), and a pre-flight
+    all-reduce makes all ranks skip together if any rank failed to set up.
+    ~1 s of wall time by default, so the exchange share means something."""
     from vrpms_amd import islands, runners, synth
     from vrpms_amd.core import CVRP
     ok, err, r = 1, None, None
     try:
         x = synth.x_style(1000, seed=seed)
         ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
-        # the front-end's large-instance SA: K - 1 separators at the greedy
-        # split's route boundaries, A11 windowed moves priced route-locally
+        # the front-end's large-instance SA: K - 1 separators packed first-fit,
+        # A11 windowed 2-opt priced route-locally
         r = runners.SARunner(ctx, x.n, chains=chains, seed=500 + rank,
                              total_steps=epochs * steps, steps_per_epoch=steps,
                              durations=x.durations, n_sep=x.K - 1, window=window,
@@ -345,33 +366,52 @@ def island_leg(ctx, torch, dev, world, rank, dist, epochs=20, steps=25, chains=1
         ok = int(f.item())
     if not ok:
         return {"error": err or "another rank failed to set up"}
+    comm_err = None
+    try:
+        if world > 1:
+            islands.init_comm(ctx, timeout_s=120)   # raises on every rank or on none
+        else:
+            ctx.island_init(ctx.island_unique_id(), 0, 1)
+        path = "vrpms_island_exchange (library RCCL ncclAllGather" + \
+               (" over xGMI)" if world > 1 else ", world-1 communicator)")
+    except Exception:
+        comm_err = traceback.format_exc(limit=2)
+        path = "library pack/merge/inject around torch.distributed all_gather (fallback)"
     # untimed warm epoch + exchange: sort/gather kernels load, communicators form
     islands.run_fixed(r, 1, 1, E)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    step0 = r.step
     t0 = time.perf_counter()
     n_ex, t_ex = islands.run_fixed(r, epochs, every, E,
                                    sync=lambda: torch.cuda.synchronize(dev))
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
+    chain_steps = r.step - step0
     key, tour = r.best()
     if world > 1:
         t = torch.tensor([wall, t_ex], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall, t_ex = float(t[0]), float(t[1])
         key, _ = islands.global_best(r)
-    evals = world * chains * epochs * steps * 64
-    return {"workload": "cfg4 X-style CVRP-1000, island SA", "vehicles": x.K,
-            "separators": x.K - 1, "window": window,
-            "kernel": "sa_route_kernel (route-local pricing of windowed moves)",
-            "chains_per_gpu": chains, "epochs": epochs, "steps_per_epoch": steps,
-            "moves_per_step": 64, "exchange_every": every, "elites": E,
-            "exchange": "RCCL all_gather over xGMI" if world > 1 else "local re-injection",
-            "wall_s": wall, "evals_per_s": evals / wall,
-            "gathers_per_eval": x.n + x.K,
-            "exchanges": n_ex, "exchange_ms_mean": t_ex / max(n_ex, 1) * 1e3,
-            "best": {"unvisited": key >> 56, "duration_sum": (key >> 28) & (2**28 - 1)}}
+    moves = world * chains * chain_steps * 64
+    out = {"workload": "cfg4 X-style CVRP-1000, island SA", "vehicles": x.K,
+           "separators": x.K - 1, "window": window,
+           "kernel": "sa_route_kernel (route-local pricing of windowed moves)",
+           "chains_per_gpu": chains, "epochs": epochs, "steps_per_epoch": steps,
+           "moves_per_step": 64, "exchange_every": every, "elites": E,
+           "exchange": path, "wall_s": wall,
+           "move_evals_per_s": moves / wall,
+           "move_evals_unit": "route-local move pricings (only the span a move changes is "
+                              "walked; not full-tour evals)",
+           "chain_steps_per_s": chain_steps / wall,
+           "exchanges": n_ex, "exchange_ms_mean": t_ex / max(n_ex, 1) * 1e3,
+           "exchange_share_of_wall": t_ex / wall,
+           "best": {"unvisited": key >> 56, "duration_sum": (key >> 28) & (2**28 - 1)}}
+    if comm_err:
+        out["comm_error"] = comm_err
+    return out
 
 
 def search_lines(ctx, torch, dev, r_gather, seed=0):
@@ -576,7 +616,8 @@ def main():
     isl = None
     if args.island_epochs > 0:
         # after every other device use of the matrix instance: it loads its own
-        isl = island_leg(ctx, torch, dev, world, rank, dist, epochs=args.island_epochs)
+        isl = island_leg(ctx, torch, dev, world, rank, dist, epochs=args.island_epochs,
+                         steps=args.island_steps)
 
     if rank == 0:
         cus = torch.cuda.get_device_properties(dev).multi_processor_count

@@ -40,6 +40,7 @@ extern "C" {
 #define VRPMS_ERANGE (-3)   /* A9 overflow guard: clock could exceed int32 */
 #define VRPMS_ESTATE (-4)   /* no instance loaded */
 #define VRPMS_ENOMEM (-5)
+#define VRPMS_ETIMEOUT (-6) /* a collective did not complete within its deadline */
 
 #define VRPMS_TSP 0
 #define VRPMS_CVRP 1
@@ -144,6 +145,11 @@ int vrpms_eval_path(vrpms_ctx* ctx, int32_t perm_bytes, int64_t ld, const void* 
  *   is VALU-issue bound, so a lone wavefront steps up to twice as fast --
  *   and as many as fit for one-wavefront chains; 1 or 2 force). */
 #define VRPMS_OPT_ROUTE_WG_PER_CU 9
+/*   VRPMS_OPT_ISLAND_TIMEOUT_S: deadline in seconds of vrpms_island_init
+ *   (default 120): the RCCL communicator is created non-blocking and aborted
+ *   when not every rank has joined by then, so a rank that never arrives
+ *   yields VRPMS_ETIMEOUT instead of a hang. */
+#define VRPMS_OPT_ISLAND_TIMEOUT_S 10
 int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value);
 
 /* Decode ONE giant tour into the result dict of api/vrp/ga/index.py:49-53
@@ -342,7 +348,10 @@ int vrpms_island_merge(vrpms_ctx* ctx, const void* d_msgs, int32_t world, int32_
 /* RCCL communicator of the island model: rank 0 calls vrpms_island_unique_id
  * (128 opaque bytes), shares them with every rank (the front-end uses its
  * torch.distributed group), and every rank calls vrpms_island_init.  One
- * process per GPU; the communicator runs over xGMI on an MI355X node. */
+ * process per GPU; the communicator runs over xGMI on an MI355X node.  The
+ * communicator is created non-blocking with a deadline
+ * (VRPMS_OPT_ISLAND_TIMEOUT_S): VRPMS_ETIMEOUT, and no communicator, when
+ * the ranks did not all join in time. */
 int vrpms_island_unique_id(void* out128);
 int vrpms_island_init(vrpms_ctx* ctx, const void* unique_id, int32_t rank, int32_t world);
 /* world of the context's communicator, 0 when none was initialised */

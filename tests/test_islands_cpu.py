@@ -169,3 +169,64 @@ def test_philox_tours_are_permutations():
     assert len({tuple(t) for t in rows}) == 20
     assert opool.philox_tour(1, 5, 0) == [1] and opool.philox_tour(0, 5, 0) == []
     assert np.all(np.array(opool.philox_tour(13, 99, 4, 2)) == np.array(rows[4]))
+
+
+class _CommStandIn(StandInContext):
+    """Stand-in with a library communicator that fails on `bad_rank`."""
+
+    def __init__(self, inst, rank, bad_rank):
+        super().__init__(inst)
+        self.rank, self.bad_rank, self._world = rank, bad_rank, 0
+        self.island_comm_group = None
+
+    def set_island_timeout(self, s):
+        self.timeout = s
+
+    def island_unique_id(self):
+        return bytes(128)
+
+    def island_init(self, uid, rank, world):
+        if rank == self.bad_rank:
+            raise RuntimeError("simulated ncclCommInitRank failure")
+        self._world = world
+
+    def island_world(self):
+        return self._world
+
+
+def _agree_worker(rank, world, port, bad_rank, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ctx = _CommStandIn(_inst(), rank, bad_rank)
+        try:
+            islands.init_comm(ctx, timeout_s=5)
+            q.put((rank, ("ok", ctx.island_comm_group, ctx.timeout)))
+        except RuntimeError as e:
+            q.put((rank, ("raised", ctx.island_comm_group, str(e))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bad_rank", [-1, 1])
+def test_init_comm_ranks_agree_on_the_exchange_path(bad_rank):
+    """init_comm sets the communicator on every rank or on none: when one
+    rank's vrpms_island_init fails, every rank raises (no rank is left to
+    call ncclAllGather while another calls torch's all-gather)."""
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = _free_port()
+    procs = [mpc.Process(target=_agree_worker, args=(r, 2, port, bad_rank, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    if bad_rank < 0:
+        assert out[0] == out[1] == ("ok", (None, 2), 5)
+    else:
+        assert out[0][0] == out[1][0] == "raised"
+        assert out[0][1] is None and out[1][1] is None
+        assert "simulated" in out[1][2]

@@ -47,3 +47,52 @@ def test_route_pricing_matches_full_evaluation(nn, slack, obj, sep):
             if ref["unvisited"] == 0 or rng.random() < 0.2:
                 A = mv
     assert checked > 20
+
+
+def _clean_tour(rng, inst, K):
+    """A random clean tour: first-fit routes of a random order, K - 1 separators."""
+    dem = [int(x) for x in inst.demand]
+    return [int(x) for x in spec.pack_separators(rng.permutation(np.arange(1, inst.n + 1)), K - 1,
+                                                 dem, inst.capacities)]
+
+
+@pytest.mark.parametrize("nn,slack,obj,window", [(30, 1.05, 0, 0), (60, 1.2, 1, 0),
+                                                 (120, 1.1, 0, 8), (40, 2.0, 0, 0)])
+def test_clean_pricing_matches_full_evaluation(nn, slack, obj, window):
+    """O(1) pricing of clean tours (route_model.price_clean) == eval_cvrp
+    whenever every route of the moved tour fits; when one does not and the
+    tour has K - 1 separators and ends with a customer, the moved tour
+    leaves a customer unserved (the kernel's largest-key shortcut)."""
+    rng = np.random.default_rng(nn + window)
+    checked = dismissed = 0
+    for trial in range(3):
+        inst = synth.cvrp(nn, max(3, nn // 10), seed=trial + 7 * nn, slack=slack)
+        K, cap = len(inst.capacities), int(inst.capacities[0])
+        dem = [int(x) for x in inst.demand]
+        D = inst.durations[0]
+        A = _clean_tour(rng, inst, K)
+        T = rmod.CleanTables(D, A, dem, cap)
+        if not T.clean(K):
+            continue
+        for _ in range(300):
+            n = len(A)
+            typ = int(rng.integers(0, 3))
+            r = [int(x) for x in rng.integers(0, 2**32, size=3, dtype=np.uint64)]
+            typ_, i, j = spec.decode_move_window(typ, r[1], r[2], n, window, 0)
+            mv = rmod._moved(A, (typ_, i, j))
+            ref = spec.eval_cvrp(inst.durations, mv, inst.demand, inst.capacities,
+                                 inst.start_times, obj)
+            got = rmod.price_clean(T, (typ_, i, j), obj)
+            if got is not None:
+                assert ref["unvisited"] == 0 and got == ref["key"], (trial, typ_, i, j)
+                checked += 1
+            elif T.S == K - 1 and mv[-1] != 0:
+                assert ref["unvisited"] > 0, (trial, typ_, i, j)
+                dismissed += 1
+            if got is not None and rng.random() < 0.5:
+                A = mv
+                T = rmod.CleanTables(D, A, dem, cap)
+                assert T.clean(K)
+    assert checked > 100
+    if slack < 1.5:
+        assert dismissed > 5

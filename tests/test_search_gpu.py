@@ -483,3 +483,90 @@ def test_ga_fused_small_matches_python_oracle(ctx):
     ctx.ga_generation(dpop, keys, generations=6, pmut=0.6, seed=55, gen0=0)
     assert dpop.cpu().numpy().tolist() == rpop
     assert u64(keys) == [k for ks in rkeys for k in ks]
+
+
+# --- round 3: the product shapes the front-end and the bench actually run ---
+
+def test_ga_fused_pop256_cfg2_equals_three_kernel_and_oracle(ctx):
+    """The front-end default population (randomPermutationCount -> 256,
+    solver.py) at CVRP-100 is the largest island the fused kernel keeps in
+    LDS: 4 islands x 3 generations fused == three-launch, and the first 2
+    generations == the Python replay (oracle/search.py ga_generation).
+    Reference slot: api/vrp/ga/index.py:48-53."""
+    torch = torch_()
+    inst = synth.cvrp(100, 8, seed=0)
+    load(ctx, inst)
+    islands, pop, n = 4, 256, inst.n
+    P = synth.random_perms(islands * pop, n, seed=256).astype(np.int16)
+    seed, pmut = 4242, 0.2
+    out = []
+    for mode, gens in ((0, 3), (2, 3), (0, 2)):
+        ctx.set_ga_fused(mode)
+        try:
+            dpop = torch.from_numpy(P.reshape(islands, pop, n).copy()).to(ctx.dev)
+            keys = ctx.eval(dpop.view(islands * pop, n)).view(islands, pop)
+            ctx.ga_generation(dpop, keys, generations=gens, pmut=pmut, seed=seed, gen0=1)
+            out.append((dpop.cpu().numpy(), u64(keys)))
+        finally:
+            ctx.set_ga_fused(0)
+    assert (out[0][0] == out[1][0]).all()
+    assert out[0][1] == out[1][1]
+    sc = scorer(inst)
+    rpop = [[list(r) for r in P.reshape(islands, pop, n)[i]] for i in range(islands)]
+    rkeys = [[sc(t) for t in rpop[i]] for i in range(islands)]
+    pm = min(int(round(pmut * 2**32)), 2**32 - 1)
+    for g in range(2):
+        rpop, rkeys = search.ga_generation(sc, rpop, rkeys, seed, 1 + g, pm)
+    assert out[2][0].tolist() == rpop
+    assert out[2][1] == [k for ks in rkeys for k in ks]
+
+
+@pytest.mark.parametrize("problem", ["cvrp", "tsp"])
+def test_bf_n13_rank_windows_match_c_restatement(ctx, coracle, problem):
+    """The front-end cap (13 customers, 13! = 6.2 G > 2^32 ranks): a window
+    straddling rank 2^32 (64-bit unranking) and the first 10^6 ranks equal
+    the C brute force.  Reference slots: api/{tsp,vrp}/bf/index.py:39-44."""
+    from vrpms_amd.core import CVRP, TSP
+    if problem == "cvrp":
+        inst = synth.cvrp(13, 3, seed=13)
+        ctx.set_instance(CVRP, inst.durations, inst.demand, inst.capacities, inst.start_times)
+        kw = dict(demand=inst.demand, capacities=inst.capacities, start_times=inst.start_times)
+    else:
+        D = synth.tsp20(13).durations[:, :14, :14]
+        inst = synth.Instance("t13", D, None, None, np.array([0]), "tsp")
+        ctx.set_instance(TSP, inst.durations, start_times=inst.start_times)
+        kw = dict(start_times=inst.start_times, problem=0)
+    n = 13
+    for lo, hi in ((2**32 - 5000, 2**32 + 5000), (0, 10**6), (math.factorial(13) - 7777,
+                                                               math.factorial(13))):
+        got = ctx.bf_run(n, lo, hi)
+        ref = coracle.bf(inst.durations, n, lo, hi, **kw)
+        assert got == ref, (lo, hi)
+        assert lo <= got[1] < hi
+        assert scorer(inst)(search.unrank(got[1], n)) == got[0]
+
+
+@pytest.mark.parametrize("lo,hi", [(65_536, 1_000_000), (70_000, 4_000_000)],
+                         ids=["i32_stage_dword_argmin", "i32_stage_u64_argmin"])
+def test_tsp_batch_tsp50_int32_staging_matches_c_restatement(ctx, coracle, lo, hi):
+    """cfg 5 at N = 50 with entries >= 65,536: the matrix cannot be staged as
+    uint16, so the int32 LDS staging runs; the second range also pushes the
+    tour sum past 2^26 (64-bit (key, lane) argmin).  64 requests x 200 steps
+    vs the C restatement.  Reference slot: api/tsp/sa/index.py:40-44."""
+    torch = torch_()
+    rng = np.random.default_rng(lo)
+    R, N = 64, 50
+    mats = []
+    for _ in range(R):
+        m = rng.integers(lo, hi, size=(N, N))
+        m = np.triu(m, 1)
+        m = m + m.T
+        mats.append(m)
+    mats = np.stack(mats)
+    assert mats.max() * N < 2**28
+    M = torch.tensor(mats, dtype=torch.int32, device=ctx.dev)
+    tours, keys = ctx.tsp_batch_sa(M, steps=200, inv_t0=1 / (0.3 * lo), inv_alpha=1 / 0.99,
+                                   seed=77)
+    rt, rk = coracle.tsp_batch_sa(mats, 200, 1 / (0.3 * lo), 1 / 0.99, 77)
+    assert (tours.cpu().numpy().view(np.uint16) == rt).all()
+    assert u64(keys) == [int(k) for k in rk]

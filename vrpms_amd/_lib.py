@@ -21,6 +21,7 @@ VRPMS_EHIP = -2
 VRPMS_ERANGE = -3
 VRPMS_ESTATE = -4
 VRPMS_ENOMEM = -5
+VRPMS_ETIMEOUT = -6
 
 TSP = 0
 CVRP = 1
@@ -33,6 +34,7 @@ OPT_ROWS_CONFIG = 6
 OPT_GA_FUSED = 7
 OPT_SA_ROUTE = 8
 OPT_ROUTE_WG_PER_CU = 9
+OPT_ISLAND_TIMEOUT_S = 10
 OBJ_SUM = 0
 OBJ_MAX = 1
 INJECT_WORST = 0

@@ -55,6 +55,8 @@ class Context:
         self.problem = None
         self.N = self.H = self.K = 0
         self.objective = OBJ_SUM
+        # (group, world) once islands.init_comm agreed on a communicator
+        self.island_comm_group = None
 
     # -- lifetime -----------------------------------------------------------
     def close(self):
@@ -398,6 +400,10 @@ class Context:
 
     def island_world(self) -> int:
         return int(self.lib.vrpms_island_world(self._ctx))
+
+    def set_island_timeout(self, seconds: int):
+        """Deadline of vrpms_island_init (VRPMS_OPT_ISLAND_TIMEOUT_S)."""
+        check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_ISLAND_TIMEOUT_S, int(seconds)))
 
     def island_exchange(self, src, dst, mode: int, E: int, groups: int = 1):
         """vrpms_island_exchange: src/dst are (tours, keys) pairs."""

@@ -264,6 +264,12 @@ int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value) {
     ctx->opt_words_ilp = value;
     return VRPMS_OK;
   }
+  if (option == VRPMS_OPT_ISLAND_TIMEOUT_S) {
+    if (value <= 0)
+      return fail(VRPMS_EINVAL, "vrpms_set_option: island timeout must be > 0 seconds");
+    ctx->opt_island_timeout_s = value;
+    return VRPMS_OK;
+  }
   return fail(VRPMS_EINVAL, "vrpms_set_option: unknown option " + std::to_string(option));
 }
 

@@ -54,8 +54,8 @@ struct vrpms_ctx {
   int opt_words_ilp = 0;        // candidates per lane in eval_cvrp_words2 (0 auto, 1, 2 or 3)
   int opt_words_lookahead = 0;  // VRPMS_OPT_WORDS_LOOKAHEAD (words2 gather lookahead, A/B)
   int opt_words_kernel = 0;     // VRPMS_OPT_WORDS_KERNEL (0 auto = words2/rows2, 1 = first generation)
-  int opt_ga_fused = 0;
-  int opt_sa_route = 0;         // VRPMS_OPT_SA_ROUTE (0 auto, 2 = force full re-evaluation)         // VRPMS_OPT_GA_FUSED (0 auto, 2 = force the three-kernel GA)
+  int opt_ga_fused = 0;          // VRPMS_OPT_GA_FUSED (0 auto, 2 = force the three-kernel GA)
+  int opt_sa_route = 0;         // VRPMS_OPT_SA_ROUTE (0 auto, 2 = force full re-evaluation)
   int opt_rows_config = 0;      // VRPMS_OPT_ROWS_CONFIG (0 auto, 1..5 force eval_cvrp_rows2's (CW, ILP))
   int32_t* d_stats = nullptr;   // scratch for set_instance validation
   uint64_t* d_scratch = nullptr;  // small reduction scratch
@@ -65,6 +65,7 @@ struct vrpms_ctx {
   size_t pool_scratch_bytes = 0;
   void* comm = nullptr;            // ncclComm_t of the island model (vrpms_island_init)
   int comm_rank = 0, comm_world = 1;
+  int opt_island_timeout_s = 120;  // VRPMS_OPT_ISLAND_TIMEOUT_S
 };
 
 namespace vrpms {

@@ -18,8 +18,10 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <string>
+#include <thread>
 
 #include "common.hpp"
 #include "ctx.hpp"
@@ -301,6 +303,26 @@ __global__ void msg_gather_kernel(const unsigned char* msgs, size_t mbytes, int 
   if (threadIdx.x == 0) keys_out[e] = reinterpret_cast<const uint64_t*>(m)[x];
 }
 
+// Poll a non-blocking communicator until its pending operation (creation,
+// or the enqueue of a collective) has completed or failed; ncclInProgress
+// back means the deadline passed first.
+static ncclResult_t wait_comm(ncclComm_t comm, std::chrono::steady_clock::time_point deadline) {
+  ncclResult_t state = ncclInProgress;
+  while (true) {
+    const ncclResult_t r = ncclCommGetAsyncError(comm, &state);
+    if (r != ncclSuccess) return r;
+    if (state != ncclInProgress) return state;
+    if (std::chrono::steady_clock::now() > deadline) return ncclInProgress;
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
+// The pool scratch is grown with a plain hipFree + hipMalloc: hipFree
+// synchronises the device, so work still queued on the caller's stream that
+// reads the old buffer (RCCL receive area, top-E levels) completes first.
+// Every pool / island call enqueues on the one stream it is given and the
+// context is used by one host thread at a time (include/vrpms.h threading
+// rule); a stream-ordered allocator would need hipFreeAsync on that stream.
 static int ensure_pool_scratch(vrpms_ctx* ctx, size_t bytes) {
   if (ctx->pool_scratch_bytes >= bytes) return VRPMS_OK;
   (void)hipFree(ctx->pool_scratch);
@@ -593,10 +615,25 @@ int vrpms_island_init(vrpms_ctx* ctx, const void* unique_id, int32_t rank, int32
   }
   ncclUniqueId id;
   std::memcpy(&id, unique_id, sizeof(id));
-  ncclComm_t comm;
-  const ncclResult_t r = ncclCommInitRank(&comm, world, id, rank);
-  if (r != ncclSuccess)
-    return fail(VRPMS_EHIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  // non-blocking creation + deadline: a rank that never joins (it failed
+  // before reaching this call) turns into VRPMS_ETIMEOUT on the others
+  // instead of a process that hangs in ncclCommInitRank
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  ncclComm_t comm = nullptr;
+  ncclResult_t r = ncclCommInitRankConfig(&comm, world, id, rank, &cfg);
+  if (r != ncclSuccess && r != ncclInProgress)
+    return fail(VRPMS_EHIP, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
+  const auto deadline =
+      std::chrono::steady_clock::now() + std::chrono::seconds(ctx->opt_island_timeout_s);
+  r = wait_comm(comm, deadline);
+  if (r != ncclSuccess) {
+    if (comm) (void)ncclCommAbort(comm);
+    if (r == ncclInProgress)
+      return fail(VRPMS_ETIMEOUT, "vrpms_island_init: not every rank joined within " +
+                                      std::to_string(ctx->opt_island_timeout_s) + " s");
+    return fail(VRPMS_EHIP, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
+  }
   ctx->comm = comm;
   ctx->comm_rank = rank;
   ctx->comm_world = world;
@@ -636,10 +673,15 @@ int vrpms_island_exchange(vrpms_ctx* ctx, const vrpms_pool* src, const vrpms_poo
                      reinterpret_cast<uint64_t*>(send), head, s);
   if (rc) return rc;
   if (ctx->comm) {
-    const ncclResult_t r = ncclAllGather(send, recv, mb, ncclUint8,
-                                         static_cast<ncclComm_t>(ctx->comm), s);
+    // non-blocking communicator: the enqueue may report ncclInProgress
+    ncclComm_t comm = static_cast<ncclComm_t>(ctx->comm);
+    ncclResult_t r = ncclAllGather(send, recv, mb, ncclUint8, comm, s);
+    if (r == ncclInProgress)
+      r = wait_comm(comm, std::chrono::steady_clock::now() +
+                              std::chrono::seconds(ctx->opt_island_timeout_s));
     if (r != ncclSuccess)
-      return fail(VRPMS_EHIP, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+      return fail(r == ncclInProgress ? VRPMS_ETIMEOUT : VRPMS_EHIP,
+                  std::string("ncclAllGather: ") + ncclGetErrorString(r));
   } else {
     VRPMS_HIP(hipMemcpyAsync(recv, send, mb, hipMemcpyDeviceToDevice, s));
   }

@@ -34,15 +34,45 @@ def _dist_world(group=None) -> int:
     return dist.get_world_size(group)
 
 
-def init_comm(ctx, group=None) -> int:
+def _agree(flag: int, group=None, device=None) -> int:
+    """MIN of `flag` over the group (1 on every rank only if 1 on all)."""
+    import torch.distributed as dist
+    torch = _torch()
+    if dist.get_backend(group) == "nccl":
+        device = device if device is not None else torch.device("cuda",
+                                                                torch.cuda.current_device())
+    else:
+        device = "cpu"
+    f = torch.tensor([int(flag)], dtype=torch.int32, device=device)
+    dist.all_reduce(f, op=dist.ReduceOp.MIN, group=group)
+    return int(f.item())
+
+
+def init_comm(ctx, group=None, timeout_s: int | None = None) -> int:
     """Give `ctx` an RCCL communicator spanning the torch.distributed group:
     rank 0 draws the unique id (vrpms_island_unique_id), the group
-    broadcasts it, every rank calls vrpms_island_init.  Returns the world."""
+    broadcasts it, every rank calls vrpms_island_init (non-blocking creation
+    with a deadline, so a rank that never joins is an error, not a hang).
+    The ranks then agree over the torch group: the communicator is used only
+    when every rank has one (ctx.island_comm_group is set on all ranks or on
+    none), otherwise every rank raises.  Returns the world."""
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    obj = [ctx.island_unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(obj, src=0, group=group)
-    ctx.island_init(obj[0], rank, world)
+    if timeout_s is not None:
+        ctx.set_island_timeout(timeout_s)
+    err = None
+    try:
+        obj = [ctx.island_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        ctx.island_init(obj[0], rank, world)
+        ok = int(ctx.island_world() == world)
+    except Exception as e:  # noqa: BLE001 -- reported after the agreement
+        ok, err = 0, e
+    if not _agree(ok, group, getattr(ctx, "dev", None)):
+        ctx.island_comm_group = None
+        raise RuntimeError(f"vrpms_island_init failed on at least one rank "
+                           f"(this rank: {err or 'ok'})")
+    ctx.island_comm_group = (group, world)
     return world
 
 
@@ -65,7 +95,9 @@ def exchange(runner, E: int, group=None):
     runner.dst() by runner.inject_mode.  Returns nothing (device state)."""
     ctx = runner.ctx
     world = _dist_world(group)
-    if world == 1 or ctx.island_world() == world:
+    # the library's communicator only when init_comm agreed on it across the
+    # ranks for this group: every rank takes the same path
+    if world == 1 or getattr(ctx, "island_comm_group", None) == (group, world):
         ctx.island_exchange(runner.src(), runner.dst(), runner.inject_mode, E, runner.groups)
         return
     msg = ctx.island_pack(*runner.src(), E)
