@@ -744,6 +744,248 @@ static uint64_t resync_key(const inst_t* I, const uint16_t* T, int n, const move
   return walk_finish(I, &w);
 }
 
+/* ------------------------------------------------------------------------
+ * Segment pricing (oracle/route_model.py SegTables / price_seg; the device's
+ * sa_seg_kernel): uniform capacity, every demand fits an empty vehicle,
+ * static symmetric matrix, any tour.  With unlimited vehicles the greedy
+ * split is the concatenation over separator-delimited segments of each
+ * segment's own split from an empty vehicle, and a route's duration is a
+ * sum of consecutive edges of the tour (a separator standing for the depot):
+ * prefix sums over the positions price every contiguous run of a moved tour
+ * (forward, or reversed on a symmetric matrix) in O(1), a binary search on
+ * the prefix demands finds a capacity cut, and the fleet limit is one count
+ * (R routes, T separators after the last customer: served iff R - T <= K).
+ * ---------------------------------------------------------------------------- */
+typedef struct {
+  int n, S, R, T, levels;
+  int64_t *PE, *PD;             /* [n + 2], [n + 1] */
+  int *SC, *SP, *PC, *NC, *RB;  /* [n + 1] each (RB: [S + 2]) */
+  int64_t *dur, *dsp, *pmx, *smx, *sp; /* per route [n + 2]; sparse [levels][n + 2] */
+} seg_t;
+
+typedef struct {
+  int64_t dur, load;
+  int prev;
+  int64_t rsum, rmax;
+  int rcnt;
+  int64_t* out; /* route durations (table build) or NULL */
+} sacc_t;
+
+static inline int64_t d0(const inst_t* I, int a, int b) {
+  return (a == 0 && b == 0) ? 0 : (int64_t)I->D[(int64_t)a * I->N + b];
+}
+static inline int sspx(const seg_t* C, int k) { return k < 0 ? -1 : (k >= C->S ? C->n : C->SP[k]); }
+
+static inline void s_close(const inst_t* I, sacc_t* a) {
+  const int64_t d = a->dur + d0(I, a->prev, 0);
+  if (a->out) a->out[a->rcnt] = d;
+  a->rsum += d;
+  if (d > a->rmax) a->rmax = d;
+  ++a->rcnt;
+  a->dur = a->load = 0;
+  a->prev = 0;
+}
+
+/* customers A[a..b] (no separator) joined to the open route in the moved
+ * order (rev: A[b] first), cut wherever the next customer does not fit */
+static void s_run(const inst_t* I, const seg_t* C, const uint16_t* A, int a, int b, int rev,
+                  sacc_t* c) {
+  const int64_t *PE = C->PE, *PD = C->PD, cap = I->cap[0];
+  while (a <= b) {
+    const int64_t room = cap - c->load;
+    if (PD[b + 1] - PD[a] <= room) {
+      c->dur += d0(I, c->prev, rev ? A[b] : A[a]) + PE[b + 1] - PE[a + 1];
+      c->load += PD[b + 1] - PD[a];
+      c->prev = rev ? A[a] : A[b];
+      return;
+    }
+    if (!rev) {
+      int lo = a - 1, hi = b; /* last q in [a - 1, b] with PD[q + 1] - PD[a] <= room */
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (PD[mid + 1] - PD[a] <= room) lo = mid; else hi = mid - 1;
+      }
+      if (lo >= a) {
+        c->dur += d0(I, c->prev, A[a]) + PE[lo + 1] - PE[a + 1];
+        c->load += PD[lo + 1] - PD[a];
+        c->prev = A[lo];
+      }
+      s_close(I, c);
+      a = lo + 1;
+    } else {
+      int lo = a, hi = b + 1; /* first x in [a, b + 1] with PD[b + 1] - PD[x] <= room */
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (PD[b + 1] - PD[mid] <= room) hi = mid; else lo = mid + 1;
+      }
+      if (lo <= b) {
+        c->dur += d0(I, c->prev, A[b]) + PE[b + 1] - PE[lo + 1];
+        c->load += PD[b + 1] - PD[lo];
+        c->prev = A[lo];
+      }
+      s_close(I, c);
+      b = lo - 1;
+    }
+  }
+}
+
+static void seg_build(const inst_t* I, const uint16_t* A, int n, seg_t* C) {
+  C->n = n;
+  C->PE[0] = C->PD[0] = 0;
+  C->SC[0] = 0;
+  int S = 0, last = -1;
+  for (int p = 0; p <= n; ++p) {
+    const int a = p ? A[p - 1] : 0, b = p < n ? A[p] : 0;
+    C->PE[p + 1] = C->PE[p] + d0(I, a, b);
+    if (p < n) {
+      C->PD[p + 1] = C->PD[p] + (b ? I->dem[b] : 0);
+      C->SC[p + 1] = C->SC[p] + (b == 0);
+      if (b == 0) C->SP[S++] = p;
+      if (b) last = p;
+      C->PC[p] = last;
+    }
+  }
+  C->S = S;
+  C->NC[n] = n;
+  for (int q = n - 1; q >= 0; --q) C->NC[q] = A[q] ? q : C->NC[q + 1];
+  sacc_t c = {0, 0, 0, 0, 0, 0, C->dur};
+  for (int g = 0; g <= S; ++g) {
+    C->RB[g] = c.rcnt;
+    s_run(I, C, A, sspx(C, g - 1) + 1, sspx(C, g) - 1, 0, &c);
+    s_close(I, &c);
+  }
+  const int R = c.rcnt;
+  C->R = R;
+  C->RB[S + 1] = R;
+  C->T = n ? n - 1 - C->PC[n - 1] : 0;
+  C->dsp[0] = C->pmx[0] = 0;
+  for (int r = 0; r < R; ++r) {
+    C->dsp[r + 1] = C->dsp[r] + C->dur[r];
+    C->pmx[r + 1] = C->pmx[r] > C->dur[r] ? C->pmx[r] : C->dur[r];
+  }
+  C->smx[R] = 0;
+  for (int r = R - 1; r >= 0; --r) C->smx[r] = C->smx[r + 1] > C->dur[r] ? C->smx[r + 1] : C->dur[r];
+  for (int r = 0; r < R; ++r) C->sp[r] = C->dur[r];
+  for (int l = 1; l < C->levels; ++l) {
+    int64_t* row = C->sp + (int64_t)l * (n + 2);
+    const int64_t* pr = row - (n + 2);
+    for (int r = 0; r + (1 << l) <= R; ++r) {
+      const int64_t x = pr[r], y = pr[r + (1 << (l - 1))];
+      row[r] = x > y ? x : y;
+    }
+  }
+}
+
+static int64_t seg_rmax(const seg_t* C, int a, int b) { /* max dur[a..b] */
+  if (b < a) return 0;
+  const int l = 31 - __builtin_clz((unsigned)(b - a + 1));
+  const int64_t* row = C->sp + (int64_t)l * (C->n + 2);
+  const int64_t x = row[a], y = row[b - (1 << l) + 1];
+  return x > y ? x : y;
+}
+
+typedef struct {
+  sacc_t c;
+  int64_t isum, imax;
+  int icnt, seps, cust;
+} sreg_t;
+
+static inline void g_sep(const inst_t* I, sreg_t* g) {
+  s_close(I, &g->c);
+  ++g->seps;
+}
+static inline void g_run(const inst_t* I, const seg_t* C, const uint16_t* A, int a, int b, int rev,
+                         sreg_t* g) {
+  if (a > b) return;
+  s_run(I, C, A, a, b, rev, &g->c);
+  g->seps = 0;
+  g->cust = 1;
+}
+
+static void g_piece(const inst_t* I, const seg_t* C, const uint16_t* A, int a, int b, int rev,
+                    sreg_t* g) {
+  if (a > b) return;
+  const int* SC = C->SC;
+  if (SC[b + 1] == SC[a]) {
+    g_run(I, C, A, a, b, rev, g);
+    return;
+  }
+  const int smin = sspx(C, SC[a]), smax = sspx(C, SC[b + 1] - 1);
+  if (rev) g_run(I, C, A, smax + 1, b, 1, g);
+  else g_run(I, C, A, a, smin - 1, 0, g);
+  g_sep(I, g);
+  if (smin < smax) { /* whole segments of A between the piece's separators */
+    const int g0 = SC[smin] + 1, g1 = SC[smax];
+    const int r0 = C->RB[g0], r1 = C->RB[g1 + 1];
+    if (rev && r1 - r0 != g1 - g0 + 1) { /* several routes: a reversal splits differently */
+      for (int s = g1; s >= g0; --s) {
+        g_run(I, C, A, sspx(C, s - 1) + 1, sspx(C, s) - 1, 1, g);
+        g_sep(I, g);
+      }
+    } else {
+      g->isum += C->dsp[r1] - C->dsp[r0];
+      const int64_t m = seg_rmax(C, r0, r1 - 1);
+      if (m > g->imax) g->imax = m;
+      g->icnt += r1 - r0;
+      if (rev) {
+        const int c = C->NC[smin];
+        if (c < smax) { g->seps = SC[c] - SC[smin]; g->cust = 1; }
+        else g->seps += SC[smax] - SC[smin];
+      } else {
+        const int c = C->PC[smax];
+        if (c > smin) { g->seps = SC[smax + 1] - SC[c + 1]; g->cust = 1; }
+        else g->seps += SC[smax] - SC[smin];
+      }
+    }
+  }
+  if (rev) g_run(I, C, A, a, smin - 1, 1, g);
+  else g_run(I, C, A, smax + 1, b, 0, g);
+}
+
+/* Key of A moved by m (route_model.price_seg); *unserved = 1 (key 0) when
+ * the moved tour leaves a customer unvisited. */
+static uint64_t seg_key(const inst_t* I, const uint16_t* A, const seg_t* C, const move_t* m,
+                        int* unserved) {
+  const int n = C->n, i = m->i, j = m->j;
+  const int lo = i < j ? i : j, hi = i < j ? j : i;
+  const int* SC = C->SC;
+  const int s0 = SC[lo], st = sspx(C, s0 - 1) + 1, en = sspx(C, SC[hi + 1]);
+  sreg_t g;
+  memset(&g, 0, sizeof(g));
+  g_run(I, C, A, st, lo - 1, 0, &g);
+  if (m->typ == 1) {
+    g_piece(I, C, A, i, j, 1, &g);
+  } else if (m->typ == 0) {
+    g_piece(I, C, A, j, j, 0, &g);
+    g_piece(I, C, A, i + 1, j - 1, 0, &g);
+    g_piece(I, C, A, i, i, 0, &g);
+  } else if (i < j) {
+    g_piece(I, C, A, i + 1, j, 0, &g);
+    g_piece(I, C, A, i, i, 0, &g);
+  } else {
+    g_piece(I, C, A, i, i, 0, &g);
+    g_piece(I, C, A, j, i - 1, 0, &g);
+  }
+  if (en < n) {
+    g_piece(I, C, A, hi + 1, en, 0, &g);
+  } else {
+    g_run(I, C, A, hi + 1, n - 1, 0, &g);
+    s_close(I, &g.c);
+  }
+  const int glast = en < n ? SC[en] : C->S;
+  const int ra = C->RB[s0], rz = C->RB[glast + 1];
+  const int R = C->R - (rz - ra) + g.c.rcnt + g.icnt;
+  int Tb = C->T;
+  if (!(en < n && C->PC[n - 1] > en) && g.cust) Tb = g.seps + (en < n ? n - 1 - en : 0);
+  *unserved = R - Tb > I->K;
+  if (*unserved) return 0;
+  const int64_t dsum = C->dsp[ra] + g.c.rsum + g.isum + C->dsp[C->R] - C->dsp[rz];
+  int64_t dmax = C->pmx[ra] > C->smx[rz] ? C->pmx[ra] : C->smx[rz];
+  if (g.imax > dmax) dmax = g.imax;
+  if (g.c.rmax > dmax) dmax = g.c.rmax;
+  return I->objective ? pack_key(0, dmax, dsum) : pack_key(0, dsum, dmax);
+}
+
 int oracle_sa_run_resync(int problem, const int32_t* D, int H, int N, const int32_t* dem,
                          const int32_t* cap, const int32_t* st, int K, int objective,
                          uint16_t* cur, uint64_t* cur_key, uint16_t* best, uint64_t* best_key,
@@ -760,11 +1002,32 @@ int oracle_sa_run_resync(int problem, const int32_t* D, int H, int N, const int3
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   int levels = 1;
   while ((1 << levels) <= K) ++levels;
+  /* segment pricing: static symmetric matrix, every demand fits a vehicle */
+  int sym = H == 1;
+  for (int a = 0; sym && a < N; ++a)
+    for (int b = a + 1; sym && b < N; ++b) sym = D[(int64_t)a * N + b] == D[(int64_t)b * N + a];
+  for (int c = 1; sym && c < N; ++c) sym = dem[c] <= cap[0];
+  int clevels = 1;
+  while ((1 << clevels) <= n + 2) ++clevels;
 #ifdef _OPENMP
   if (threads > 0) omp_set_num_threads(threads);
 #pragma omp parallel
 #endif
   {
+    seg_t C;
+    C.levels = clevels;
+    C.PE = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n + 2));
+    C.PD = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n + 1));
+    C.SC = (int*)malloc(sizeof(int) * (size_t)(n + 1));
+    C.SP = (int*)malloc(sizeof(int) * (size_t)(n + 1));
+    C.PC = (int*)malloc(sizeof(int) * (size_t)(n + 1));
+    C.NC = (int*)malloc(sizeof(int) * (size_t)(n + 1));
+    C.RB = (int*)malloc(sizeof(int) * (size_t)(n + 2));
+    C.dur = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n + 2));
+    C.dsp = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n + 3));
+    C.pmx = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n + 3));
+    C.smx = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n + 3));
+    C.sp = (int64_t*)malloc(sizeof(int64_t) * (size_t)clevels * (size_t)(n + 2));
     split_t S;
     S.n = n;
     S.K = K;
@@ -790,7 +1053,8 @@ int oracle_sa_run_resync(int problem, const int32_t* D, int H, int N, const int3
         bk = ck;
         memcpy(Bst, A, (size_t)n * 2);
       }
-      split_build(&I, A, &S);
+      if (sym) seg_build(&I, A, n, &C);
+      else split_build(&I, A, &S);
       float invT = inv_t0;
       for (int s = 0; s < steps; ++s) {
         uint64_t step = step0 + (uint64_t)s;
@@ -802,7 +1066,14 @@ int oracle_sa_run_resync(int problem, const int32_t* D, int H, int N, const int3
           u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)c, (uint32_t)lane,
                            k0, k1);
           move_t m = decode_move_window(r.x, r.y, r.z, n, window, window_types);
-          uint64_t kk = S.alive ? resync_key(&I, A, n, &m, &S, hopeless) : tour_key(&I, A, n, &m);
+          uint64_t kk;
+          if (sym) {
+            int unserved = 0;
+            kk = seg_key(&I, A, &C, &m, &unserved);
+            if (unserved) kk = hopeless ? ~0ull : tour_key(&I, A, n, &m);
+          } else {
+            kk = S.alive ? resync_key(&I, A, n, &m, &S, hopeless) : tour_key(&I, A, n, &m);
+          }
           if (kk < kbest) {
             kbest = kk;
             mbest = m;
@@ -819,7 +1090,8 @@ int oracle_sa_run_resync(int problem, const int32_t* D, int H, int N, const int3
           for (int q = 0; q < n; ++q) tmp[q] = A[moved_index(q, &mbest)];
           memcpy(A, tmp, (size_t)n * 2);
           ck = kbest;
-          split_build(&I, A, &S);
+          if (sym) seg_build(&I, A, n, &C);
+          else split_build(&I, A, &S);
           if (ck < bk) {
             bk = ck;
             memcpy(Bst, A, (size_t)n * 2);
@@ -832,6 +1104,8 @@ int oracle_sa_run_resync(int problem, const int32_t* D, int H, int N, const int3
     }
     free(S.load); free(S.t); free(S.prev); free(S.k); free(S.lastcust); free(S.pos_cl);
     free(S.cd); free(S.cs); free(S.sp); free(tmp);
+    free(C.PE); free(C.PD); free(C.SC); free(C.SP); free(C.PC); free(C.NC); free(C.RB);
+    free(C.dur); free(C.dsp); free(C.pmx); free(C.smx); free(C.sp);
   }
   return 0;
 }

@@ -175,77 +175,151 @@ def _moved(A, m):
 
 
 # ---------------------------------------------------------------------------
-# "Clean" tours: O(1) move pricing (sa_route_kernel's fast mode, and
-# oracle_c.c resync_clean).  A tour is clean when its greedy split closes
-# routes only at A10 separators: every separator-delimited segment fits one
-# vehicle and there are at most K - 1 separators.  Then on a static
-# symmetric matrix every route's duration is a sum of consecutive edges of
-# the tour (the separator standing for the depot), so prefix sums over the
-# positions price any route of a moved tour that is a few contiguous pieces
-# of the current one (forward or reversed) in O(1), whatever the move's span.
+# Segment pricing (sa_seg_kernel, oracle_c.c seg_key): uniform capacity,
+# static symmetric matrix, any tour.  The greedy split with unlimited
+# vehicles is the concatenation, over the separator-delimited segments, of
+# each segment's own greedy split from an empty vehicle (every separator
+# closes a route, an empty one lasting 0).  A route's duration is a sum of
+# consecutive edges of the tour (a separator standing for the depot), so
+# with prefix sums over the positions any run of a moved tour that reads the
+# current tour contiguously (forward, or reversed on a symmetric matrix) is
+# priced in O(1), and a capacity cut inside a run is found by a binary search
+# on the prefix demands.  The fleet limit is one count: with R routes (empty
+# segments included) and T separators after the last customer, the split
+# serves everyone iff R - T <= K (R - 1 - T closures precede the last
+# customer).  Start times do not enter a static route's duration.
 # ---------------------------------------------------------------------------
-class CleanTables:
-    """Position prefix tables of tour A (uniform capacity `cap`).
+class SegTables:
+    """Tables of tour A (uniform capacity `cap`, every demand <= cap).
 
     e(p), p in [0, n]: edge into position p from the token before it (A[-1] =
-    A[n] = 0, the depot), 0 between two depots (an empty route lasts 0).
-    PE[q] = sum e(p < q) (q <= n + 1); PD[q] = demand of A[0..q-1];
-    SC[q] = separators in A[0..q-1]; SP[k] = position of separator k,
-    SPx(-1) = -1, SPx(S) = n.  Route r = segment SPx(r-1)+1 .. SPx(r)-1."""
+    A[n] = 0), 0 between two depots.  PE[q] = sum e(p < q) (q <= n + 1);
+    PD[q] = demand of A[0..q-1]; SC[q] = separators in A[0..q-1]; SP[k] =
+    position of separator k (spx(-1) = -1, spx(S) = n); PC[q] / NC[q]: last /
+    first customer position <= q / >= q (-1 / n: none).  Routes (unlimited
+    vehicles): RB[s] = first route of segment s (RB[S + 1] = R), dur[r]; T =
+    separators after the last customer."""
 
     def __init__(self, D, A, dem, cap):
         self.D, self.dem, self.cap = D, dem, cap
         self.A = list(A)
         n = self.n = len(A)
         ext = [0] + self.A + [0]
-        self.e = [0 if ext[p] == 0 and ext[p + 1] == 0 else int(D[ext[p], ext[p + 1]])
-                  for p in range(n + 1)]
+        e = [0 if ext[p] == 0 and ext[p + 1] == 0 else int(D[ext[p], ext[p + 1]])
+             for p in range(n + 1)]
         self.PE = [0]
-        for x in self.e:
+        for x in e:
             self.PE.append(self.PE[-1] + x)
-        self.PD = [0]
-        self.SC = [0]
+        self.PD, self.SC = [0], [0]
         for c in self.A:
             self.PD.append(self.PD[-1] + (dem[c] if c else 0))
             self.SC.append(self.SC[-1] + (c == 0))
         self.SP = [q for q, c in enumerate(self.A) if c == 0]
         self.S = len(self.SP)
-        R = self.S + 1
-        self.dur = [self.PE[self.spx(r) + 1] - self.PE[self.spx(r - 1) + 1] for r in range(R)]
-        self.load = [self.PD[self.spx(r)] - self.PD[self.spx(r - 1) + 1] for r in range(R)]
+        self.PC, last = [], -1
+        for q, c in enumerate(self.A):
+            last = q if c else last
+            self.PC.append(last)
+        self.NC, nxt = [n] * (n + 1), n
+        for q in range(n - 1, -1, -1):
+            nxt = q if self.A[q] else nxt
+            self.NC[q] = nxt
+        self.dur, self.RB = [], []
+        for s in range(self.S + 1):
+            self.RB.append(len(self.dur))
+            acc = Acc()
+            run(self, acc, self.spx(s - 1) + 1, self.spx(s) - 1, False)
+            close_route(self, acc)
+            self.dur += acc.routes
+        self.R = len(self.dur)
+        self.RB.append(self.R)
+        self.T = n - 1 - self.PC[n - 1] if n else 0
         self.dsp = [0]
         for d in self.dur:
             self.dsp.append(self.dsp[-1] + d)
         self.pmx = [0]
         for d in self.dur:
             self.pmx.append(max(self.pmx[-1], d))
-        self.smx = [0] * (R + 1)
-        for r in range(R - 1, -1, -1):
+        self.smx = [0] * (self.R + 1)
+        for r in range(self.R - 1, -1, -1):
             self.smx[r] = max(self.smx[r + 1], self.dur[r])
 
     def spx(self, k):
         return -1 if k < 0 else (self.n if k >= self.S else self.SP[k])
 
-    def clean(self, K):
-        return self.S <= K - 1 and all(x <= self.cap for x in self.load)
-
     def d0(self, a, b):
         return 0 if a == 0 and b == 0 else int(self.D[a, b])
 
 
-def price_clean(T: CleanTables, m, objective: int = 0):
-    """Key of T.A moved by m on a clean tour and a static symmetric matrix,
-    or None when a route of the moved tour exceeds the capacity (the kernel
-    then gives the largest key when that provably leaves a customer
-    unserved, else prices the move by a walk)."""
+class Acc:
+    """The open route of a pricing walk and what the walk has closed."""
+
+    def __init__(self, dur=0, load=0, prev=0):
+        self.dur, self.load, self.prev = dur, load, prev
+        self.routes = []
+
+
+def close_route(T, acc):
+    acc.routes.append(acc.dur + T.d0(acc.prev, 0))
+    acc.dur = acc.load = acc.prev = 0
+
+
+def run(T, acc, a, b, rev):
+    """Customers A[a..b] (no separator among them) joined to the open route
+    in the moved order (reversed: A[b] first), cutting the route wherever
+    the greedy split's next customer does not fit."""
+    PE, PD, A = T.PE, T.PD, T.A
+    while a <= b:
+        room = T.cap - acc.load
+        if PD[b + 1] - PD[a] <= room:
+            acc.dur += T.d0(acc.prev, A[b] if rev else A[a]) + PE[b + 1] - PE[a + 1]
+            acc.load += PD[b + 1] - PD[a]
+            acc.prev = A[a] if rev else A[b]
+            return
+        if not rev:
+            # last q in [a - 1, b] with PD[q + 1] - PD[a] <= room
+            lo_, hi_ = a - 1, b
+            while lo_ < hi_:
+                mid = (lo_ + hi_ + 1) // 2
+                if PD[mid + 1] - PD[a] <= room:
+                    lo_ = mid
+                else:
+                    hi_ = mid - 1
+            q = lo_
+            if q >= a:
+                acc.dur += T.d0(acc.prev, A[a]) + PE[q + 1] - PE[a + 1]
+                acc.load += PD[q + 1] - PD[a]
+                acc.prev = A[q]
+            close_route(T, acc)
+            a = q + 1
+        else:
+            # first x in [a, b + 1] with PD[b + 1] - PD[x] <= room
+            lo_, hi_ = a, b + 1
+            while lo_ < hi_:
+                mid = (lo_ + hi_) // 2
+                if PD[b + 1] - PD[mid] <= room:
+                    hi_ = mid
+                else:
+                    lo_ = mid + 1
+            x = lo_
+            if x <= b:
+                acc.dur += T.d0(acc.prev, A[b]) + PE[b + 1] - PE[x + 1]
+                acc.load += PD[b + 1] - PD[x]
+                acc.prev = A[x]
+            close_route(T, acc)
+            b = x - 1
+
+
+def price_seg(T: SegTables, m, K: int, objective: int = 0):
+    """Key of T.A moved by m, or None when the moved tour leaves a customer
+    unserved (R - T > K)."""
     typ, i, j = m
-    A, PE, PD, SC = T.A, T.PE, T.PD, T.SC
+    A, SC = T.A, T.SC
     n = T.n
     lo, hi = min(i, j), max(i, j)
-    ra = SC[lo]                      # first changed route (B's routes before it are A's)
-    st = T.spx(ra - 1) + 1           # its first position
-    en = T.spx(SC[hi + 1])           # first separator at or after hi + 1 (n: none)
-    # pieces of the moved tour between lo and hi, A positions (a, b, reversed)
+    s0 = SC[lo]                         # first changed segment
+    st = T.spx(s0 - 1) + 1              # its first position
+    en = T.spx(SC[hi + 1])              # separator closing the last changed one (n: the end)
     if typ == spec.MOVE_2OPT:
         mid = [(i, j, True)]
     elif typ == spec.MOVE_SWAP:
@@ -254,65 +328,81 @@ def price_clean(T: CleanTables, m, objective: int = 0):
         mid = [(i + 1, j, False), (i, i, False)]
     else:
         mid = [(i, i, False), (j, i - 1, False)]
-    st_ = {"load": PD[lo] - PD[st], "dur": PE[lo] - PE[st], "prev": A[lo - 1] if st < lo else 0}
-    routes = []          # (dur, load) of the changed routes, in order
-    inner = [0, 0]       # sum and max of the whole current-tour routes inside pieces
+    acc = Acc()
+    inner = {"sum": 0, "max": 0, "cnt": 0}
+    tr = {"seps": 0, "cust": False}      # separators since the last customer of the region
 
-    def close():
-        routes.append((st_["dur"], st_["load"]))
+    def sep():
+        close_route(T, acc)
+        tr["seps"] += 1
+
+    def crun(a, b, rev):
+        if a <= b:
+            run(T, acc, a, b, rev)
+            tr["seps"], tr["cust"] = 0, True
 
     def piece(a, b, rev):
         if a > b:
             return
-        F, L = (A[b], A[a]) if rev else (A[a], A[b])
-        ns = SC[b + 1] - SC[a]
-        if ns == 0:
-            st_["dur"] += T.d0(st_["prev"], F) + PE[b + 1] - PE[a + 1]
-            st_["load"] += PD[b + 1] - PD[a]
-            st_["prev"] = L
+        if SC[b + 1] == SC[a]:
+            crun(a, b, rev)
             return
         smin, smax = T.spx(SC[a]), T.spx(SC[b + 1] - 1)
-        sf, sl = (smax, smin) if rev else (smin, smax)
-        # the part before the first separator (in the moved order) ends the open route
-        if not rev and sf > a:
-            st_["dur"] += T.d0(st_["prev"], A[a]) + PE[sf + 1] - PE[a + 1]
-            st_["load"] += PD[sf] - PD[a]
-        elif rev and sf < b:
-            st_["dur"] += T.d0(st_["prev"], A[b]) + PE[b + 1] - PE[sf + 1]
-            st_["load"] += PD[b + 1] - PD[sf + 1]
+        if rev:
+            crun(smax + 1, b, True)
         else:
-            st_["dur"] += T.d0(st_["prev"], 0)
-        close()
-        # whole routes between the piece's first and last separator
-        r0, r1 = SC[smin] + 1, SC[smax]
-        if r0 <= r1:
-            inner[0] += T.dsp[r1 + 1] - T.dsp[r0]
-            inner[1] = max(inner[1], max(T.dur[r0:r1 + 1]))
-        # the part after the last separator opens the next route
-        if not rev:
-            if sl < b:
-                st_.update(dur=PE[b + 1] - PE[sl + 1], load=PD[b + 1] - PD[sl + 1], prev=A[b])
+            crun(a, smin - 1, False)
+        sep()
+        if smin < smax:                  # whole segments of A between the piece's separators
+            g0, g1 = SC[smin] + 1, SC[smax]
+            r0, r1 = T.RB[g0], T.RB[g1 + 1]
+            if rev and r1 - r0 != g1 - g0 + 1:
+                # a reversed segment of several routes splits differently: walk them
+                for g in range(g1, g0 - 1, -1):
+                    crun(T.spx(g - 1) + 1, T.spx(g) - 1, True)
+                    sep()
             else:
-                st_.update(dur=0, load=0, prev=0)
+                inner["sum"] += T.dsp[r1] - T.dsp[r0]
+                inner["max"] = max([inner["max"]] + T.dur[r0:r1])
+                inner["cnt"] += r1 - r0
+                if rev:
+                    c = T.NC[smin]       # the interior's last customer in the moved order
+                    if c < smax:
+                        tr["seps"], tr["cust"] = SC[c] - SC[smin], True
+                    else:
+                        tr["seps"] += SC[smax] - SC[smin]
+                else:
+                    c = T.PC[smax]
+                    if c > smin:
+                        tr["seps"], tr["cust"] = SC[smax + 1] - SC[c + 1], True
+                    else:
+                        tr["seps"] += SC[smax] - SC[smin]
+        if rev:
+            crun(a, smin - 1, True)
         else:
-            if sl > a:
-                st_.update(dur=PE[sl + 1] - PE[a + 1], load=PD[sl] - PD[a], prev=A[a])
-            else:
-                st_.update(dur=0, load=0, prev=0)
+            crun(smax + 1, b, False)
 
+    crun(st, lo - 1, False)
     for a, b, rev in mid:
         piece(a, b, rev)
     if en < n:
-        piece(hi + 1, en, False)         # closes the last changed route at A's separator en
+        piece(hi + 1, en, False)
     else:
-        piece(hi + 1, n - 1, False)
-        st_["dur"] += T.d0(st_["prev"], 0)
-        close()
-    if any(ld > T.cap for _, ld in routes):
+        crun(hi + 1, n - 1, False)
+        close_route(T, acc)
+    g_last = SC[en] if en < n else T.S   # last segment of the region
+    ra, rz = T.RB[s0], T.RB[g_last + 1]  # current routes the region replaces
+    R = T.R - (rz - ra) + len(acc.routes) + inner["cnt"]
+    if en < n and T.PC[n - 1] > en:     # the tail after the region keeps the last customer
+        Tb = T.T
+    elif tr["cust"]:
+        Tb = tr["seps"] + (n - 1 - en if en < n else 0)
+    else:
+        Tb = T.T
+    if R - Tb > K:
         return None
-    after = SC[en] + 1
-    dsum = T.dsp[ra] + sum(d for d, _ in routes) + inner[0] + T.dsp[T.S + 1] - T.dsp[after]
-    dmax = max([T.pmx[ra], T.smx[after], inner[1]] + [d for d, _ in routes])
+    dsum = T.dsp[ra] + sum(acc.routes) + inner["sum"] + T.dsp[T.R] - T.dsp[rz]
+    dmax = max([T.pmx[ra], T.smx[rz], inner["max"]] + acc.routes)
     if objective == spec.OBJ_SUM:
         return spec.pack_key(0, dsum, dmax)
     return spec.pack_key(0, dmax, dsum)

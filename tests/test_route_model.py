@@ -49,50 +49,45 @@ def test_route_pricing_matches_full_evaluation(nn, slack, obj, sep):
     assert checked > 20
 
 
-def _clean_tour(rng, inst, K):
-    """A random clean tour: first-fit routes of a random order, K - 1 separators."""
-    dem = [int(x) for x in inst.demand]
-    return [int(x) for x in spec.pack_separators(rng.permutation(np.arange(1, inst.n + 1)), K - 1,
-                                                 dem, inst.capacities)]
-
-
-@pytest.mark.parametrize("nn,slack,obj,window", [(30, 1.05, 0, 0), (60, 1.2, 1, 0),
-                                                 (120, 1.1, 0, 8), (40, 2.0, 0, 0)])
-def test_clean_pricing_matches_full_evaluation(nn, slack, obj, window):
-    """O(1) pricing of clean tours (route_model.price_clean) == eval_cvrp
-    whenever every route of the moved tour fits; when one does not and the
-    tour has K - 1 separators and ends with a customer, the moved tour
-    leaves a customer unserved (the kernel's largest-key shortcut)."""
+@pytest.mark.parametrize("nn,slack,obj,window,sep", [
+    (30, 1.05, 0, 0, "K-1"), (60, 1.2, 1, 0, "K-1"), (120, 1.1, 0, 8, "K-1"),
+    (40, 2.0, 0, 0, "K-1"), (50, 1.0, 0, 0, "K-2"), (70, 1.3, 1, 6, "K+2"), (45, 1.02, 0, 0, "0")])
+def test_segment_pricing_matches_full_evaluation(nn, slack, obj, window, sep):
+    """O(1) segment pricing (route_model.price_seg: prefix sums, binary-searched
+    capacity cuts, the R - T <= K fleet count) == eval_cvrp on random moves of
+    random tours -- first-fit (trailing separators) and random separators,
+    feasible and infeasible, tight and loose fleets -- and None exactly when
+    the moved tour leaves a customer unserved."""
     rng = np.random.default_rng(nn + window)
-    checked = dismissed = 0
+    checked = none = 0
     for trial in range(3):
         inst = synth.cvrp(nn, max(3, nn // 10), seed=trial + 7 * nn, slack=slack)
         K, cap = len(inst.capacities), int(inst.capacities[0])
         dem = [int(x) for x in inst.demand]
         D = inst.durations[0]
-        A = _clean_tour(rng, inst, K)
-        T = rmod.CleanTables(D, A, dem, cap)
-        if not T.clean(K):
-            continue
+        S = max(0, {"K-1": K - 1, "K-2": K - 2, "0": 0, "K+2": K + 2}[sep])
+        perm = rng.permutation(np.arange(1, nn + 1))
+        if trial == 0:
+            A = [int(x) for x in spec.pack_separators(perm, S, dem, inst.capacities)]
+        else:
+            A = [int(x) for x in perm] + [0] * S
+            rng.shuffle(A)
+        T = rmod.SegTables(D, A, dem, cap)
         for _ in range(300):
             n = len(A)
-            typ = int(rng.integers(0, 3))
             r = [int(x) for x in rng.integers(0, 2**32, size=3, dtype=np.uint64)]
-            typ_, i, j = spec.decode_move_window(typ, r[1], r[2], n, window, 0)
-            mv = rmod._moved(A, (typ_, i, j))
+            typ, i, j = spec.decode_move_window(r[0], r[1], r[2], n, window, 0)
+            mv = rmod._moved(A, (typ, i, j))
             ref = spec.eval_cvrp(inst.durations, mv, inst.demand, inst.capacities,
                                  inst.start_times, obj)
-            got = rmod.price_clean(T, (typ_, i, j), obj)
-            if got is not None:
-                assert ref["unvisited"] == 0 and got == ref["key"], (trial, typ_, i, j)
+            got = rmod.price_seg(T, (typ, i, j), K, obj)
+            if ref["unvisited"] == 0:
+                assert got == ref["key"], (trial, typ, i, j)
                 checked += 1
-            elif T.S == K - 1 and mv[-1] != 0:
-                assert ref["unvisited"] > 0, (trial, typ_, i, j)
-                dismissed += 1
-            if got is not None and rng.random() < 0.5:
+            else:
+                assert got is None, (trial, typ, i, j)
+                none += 1
+            if rng.random() < 0.4 and (ref["unvisited"] == 0 or rng.random() < 0.3):
                 A = mv
-                T = rmod.CleanTables(D, A, dem, cap)
-                assert T.clean(K)
-    assert checked > 100
-    if slack < 1.5:
-        assert dismissed > 5
+                T = rmod.SegTables(D, A, dem, cap)
+    assert checked > 5 and checked + none == 900

@@ -240,12 +240,14 @@ def test_route_local_sa_matches_c_restatement(ctx, coracle, name, maker, start, 
     assert (got[0].view(np.uint16) == ccur).all()
     assert got[1] == [int(x) for x in cck] and got[3] == [int(x) for x in cbk]
     assert (got[2].view(np.uint16) == cbest).all()
-    ctx.set_sa_route(2)
-    try:
-        full = _run_sa(ctx, P, steps, inv_t0, 1 / 0.99, 21, 7, window, types)
-    finally:
-        ctx.set_sa_route(0)
-    assert (full[0] == got[0]).all() and full[1] == got[1] and full[3] == got[3]
+    # the same chains through the route-local walks (3) and full re-evaluation (2)
+    for mode in (3, 2):
+        ctx.set_sa_route(mode)
+        try:
+            other = _run_sa(ctx, P, steps, inv_t0, 1 / 0.99, 21, 7, window, types)
+        finally:
+            ctx.set_sa_route(0)
+        assert (other[0] == got[0]).all() and other[1] == got[1] and other[3] == got[3]
 
 
 MULTIWAVE_CASES = [
@@ -308,6 +310,8 @@ def test_sa_moves_validation(ctx):
         ctx.sa_run(cur, ck, cur.clone(), bk, 2, 0.01, 1.0, 1, 0, window=4, moves=100)
     with pytest.raises(RuntimeError):   # more than 8 wavefronts
         ctx.sa_run(cur, ck, cur.clone(), bk, 2, 0.01, 1.0, 1, 0, window=4, moves=576)
+    td = synth.td_cvrp(30, 4, seed=1)    # hour-indexed: no segment pricing
+    load(ctx, td)
     with pytest.raises(RuntimeError):   # window 0: not the route-local kernel
         ctx.sa_run(cur, ck, cur.clone(), bk, 2, 0.01, 1.0, 1, 0, window=0, moves=128)
 
@@ -359,3 +363,58 @@ def test_pack_separators_matches_spec(ctx):
         dev = ctx.pack_separators(torch.from_numpy(P0.astype(np.int16)).to(ctx.dev), S)
         want = [spec.pack_separators(p, S, het.demand, het.capacities) for p in P0]
         assert dev.cpu().numpy().tolist() == want
+
+
+SEG_CASES = [
+    # (case, instance, start, chains, steps, inv_t0, window, types, moves): the
+    # segment-priced kernel on the fleets / move mixes the walk kernel cannot take
+    ("x1000_full_range_m256", lambda: synth.x_style(1000, seed=6), "pack", 8, 120, 1 / 300.0, 0,
+     0, 256),
+    ("x1000_staggered_starts", lambda: _starts(synth.x_style(1000, seed=7)), "pack", 8, 150,
+     1 / 300.0, 32, 2, 64),
+    ("cvrp300_hot_m128", lambda: synth.cvrp(300, 24, seed=9, slack=1.05), "random", 8, 60, 1e-7, 0,
+     0, 128),
+    ("cvrp1200_long_tours", lambda: synth.cvrp(1200, 60, seed=10), "pack", 4, 60, 1 / 300.0, 32, 2,
+     64),
+]
+
+
+def _starts(inst):
+    import dataclasses
+    st = np.arange(inst.K, dtype=np.int64) * 37 % 240
+    return dataclasses.replace(inst, start_times=st)
+
+
+@pytest.mark.parametrize("name,maker,start,chains,steps,inv_t0,window,types,moves", SEG_CASES,
+                         ids=[c[0] for c in SEG_CASES])
+def test_segment_sa_matches_c_restatement(ctx, coracle, name, maker, start, chains, steps, inv_t0,
+                                          window, types, moves):
+    """sa_seg_kernel (O(1) segment pricing) on full-range moves, several
+    moves per lane, staggered vehicle start times (static matrix: a route's
+    duration does not depend on its start) and tours longer than 1,100
+    tokens, against the C restatement (full walks and segment pricing)."""
+    inst = maker()
+    load(ctx, inst)
+    S = inst.K - 1
+    if start == "pack":
+        P0 = synth.random_perms(chains, inst.n, seed=9, dtype=np.uint16)
+        P = np.array([spec.pack_separators(p, S, inst.demand, inst.capacities) for p in P0])
+    else:
+        P = sep_tours(chains, inst.n, S, seed=9, dtype=np.uint16)
+    P = P.astype(np.int16)
+    torch = torch_()
+    cur = torch.from_numpy(P).to(ctx.dev)
+    best = cur.clone()
+    ck = torch.empty(chains, dtype=torch.int64, device=ctx.dev)
+    bk = torch.full((chains,), -1, dtype=torch.int64, device=ctx.dev)
+    ctx.sa_run(cur, ck, best, bk, steps=steps, inv_t0=inv_t0, inv_alpha=1 / 0.99, seed=33,
+               step0=5, window=window, window_types=types, moves=moves)
+    for resync in (False, True):
+        ccur, cbest = P.view(np.uint16).copy(), P.view(np.uint16).copy()
+        cbk = np.full(chains, 2**64 - 1, dtype=np.uint64)
+        cck = coracle.sa_run(inst.durations, ccur, cbest, cbk, steps, inv_t0, 1 / 0.99, 33, 5,
+                             inst.demand, inst.capacities, inst.start_times, window=window,
+                             window_types=types, resync=resync, moves=moves)
+        assert (cur.cpu().numpy().view(np.uint16) == ccur).all()
+        assert u64(ck) == [int(x) for x in cck] and u64(bk) == [int(x) for x in cbk]
+        assert (best.cpu().numpy().view(np.uint16) == cbest).all()

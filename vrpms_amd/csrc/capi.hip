@@ -229,8 +229,9 @@ int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value) {
     return VRPMS_OK;
   }
   if (option == VRPMS_OPT_SA_ROUTE) {
-    if (value != 0 && value != 2)
-      return fail(VRPMS_EINVAL, "vrpms_set_option: SA route must be 0 (auto) or 2 (full walks)");
+    if (value != 0 && value != 2 && value != 3)
+      return fail(VRPMS_EINVAL,
+                  "vrpms_set_option: SA route must be 0 (auto), 2 (full walks) or 3 (route walks)");
     ctx->opt_sa_route = value;
     return VRPMS_OK;
   }

@@ -28,86 +28,11 @@
 #include "common.hpp"
 #include "ctx.hpp"
 #include "split.hpp"
+#include "staging.hpp"
 #include "tour.hpp"
 #include "words.hpp"
 
 namespace vrpms {
-
-VRPMS_DEV int lane_id() { return (int)(threadIdx.x & 63u); }
-
-// Instance staged for a search kernel: matrix in LDS when it fits, else L2.
-struct SearchInst {
-  const void* mat;   // u16 or i32 [H][N][N] (global)
-  int N, H, K, problem, objective;
-  const int32_t* dem;
-  const int32_t* cap;
-  const int32_t* start;
-  int mat_lds;       // 1: stage the matrix into LDS (only when mat_bytes <= 64 KB)
-  uint64_t mat_bytes; // H*N*N*elem: 64-bit, an int32 matrix can exceed 4 GB
-  int symmetric;     // hour slice 0 symmetric (O(1) 2-opt delta)
-};
-
-static SearchInst search_inst(const vrpms_ctx* ctx) {
-  const Instance& in = ctx->inst;
-  SearchInst s;
-  s.mat = in.use16 ? static_cast<const void*>(in.mat16) : static_cast<const void*>(in.mat32);
-  s.N = in.N;
-  s.H = in.H;
-  s.K = in.K;
-  s.problem = in.problem;
-  s.objective = in.objective;
-  s.dem = in.dem;
-  s.cap = in.cap;
-  s.start = in.start;
-  s.mat_bytes = (uint64_t)in.H * (uint64_t)in.N * (uint64_t)in.N * (in.use16 ? 2u : 4u);
-  s.mat_lds = s.mat_bytes <= 64u * 1024u ? 1 : 0;
-  s.symmetric = in.symmetric ? 1 : 0;
-  return s;
-}
-
-// LDS carve for the instance part: [matrix][dem N][cap K][start K], 16-B aligned.
-VRPMS_DEV uint32_t inst_lds_bytes(const SearchInst& si) {
-  const uint32_t m = si.mat_lds ? (((uint32_t)si.mat_bytes + 15u) & ~15u) : 0u;
-  return m + (((uint32_t)(si.N + 2 * si.K) * 4u + 15u) & ~15u);
-}
-
-static size_t inst_lds_bytes_host(const SearchInst& si) {
-  const size_t m = si.mat_lds ? (((size_t)si.mat_bytes + 15u) & ~(size_t)15u) : 0u;
-  return m + ((((size_t)si.N + 2 * si.K) * 4u + 15u) & ~(size_t)15u);
-}
-
-template <typename MatT, int HM>
-struct StagedInst {
-  MatView<MatT, HM> D;
-  SplitParams sp;
-};
-
-template <typename MatT, int HM>
-VRPMS_DEV StagedInst<MatT, HM> stage_inst(const SearchInst& si, unsigned char* smem) {
-  const uint32_t NN = (uint32_t)si.N * si.N;
-  const MatT* M = static_cast<const MatT*>(si.mat);
-  uint32_t off = 0;
-  if (si.mat_lds) {
-    const uint32_t mb = (uint32_t)si.mat_bytes;  // <= 64 KB when staged
-    const uint32_t* s = static_cast<const uint32_t*>(si.mat);
-    uint32_t* d = reinterpret_cast<uint32_t*>(smem);
-    for (uint32_t i = threadIdx.x; i < mb / 4; i += blockDim.x) d[i] = s[i];
-    if ((mb & 2u) && threadIdx.x == 0)
-      reinterpret_cast<uint16_t*>(smem)[mb / 2 - 1] = static_cast<const uint16_t*>(si.mat)[mb / 2 - 1];
-    M = reinterpret_cast<const MatT*>(smem);
-    off = (mb + 15u) & ~15u;
-  }
-  int32_t* dem = reinterpret_cast<int32_t*>(smem + off);
-  int32_t* cap = dem + si.N;
-  int32_t* st = cap + si.K;
-  for (int i = threadIdx.x; i < si.N; i += blockDim.x) dem[i] = si.dem[i];
-  for (int i = threadIdx.x; i < si.K; i += blockDim.x) {
-    cap[i] = si.cap[i];
-    st[i] = si.start[i];
-  }
-  __syncthreads();
-  return {{M, (uint32_t)si.N, NN, si.H}, {dem, cap, st, si.K, si.objective}};
-}
 
 // ===========================================================================
 // Simulated annealing: one wavefront per chain.
@@ -2212,6 +2137,9 @@ struct BfK {
 
 int launch_ga_fused(const vrpms_ctx* ctx, const vrpms_ga_params* p, uint16_t* d_pop,
                     uint64_t* d_keys, int n, hipStream_t s);  // ga_fused.hip
+int launch_sa_seg(const vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* d_cur,
+                  uint64_t* d_cur_key, uint16_t* d_best, uint64_t* d_best_key, int n,
+                  uint32_t wtypes, int moves, hipStream_t s);  // sa_seg.hip
 
 static void ensure_scratch(vrpms_ctx* ctx, size_t bytes, int* err) {
   if (ctx->search_scratch_bytes >= bytes) return;
@@ -2268,6 +2196,13 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
       return VRPMS_OK;
     }
   }
+  // segment pricing (sa_seg_kernel, sa_seg.hip): static symmetric matrix,
+  // one capacity, every demand fits a vehicle -- any move span, any start times
+  if (ctx->opt_sa_route == 0) {
+    const int rc = launch_sa_seg(ctx, p, d_cur, d_cur_key, d_best, d_best_key, n, wtypes, moves,
+                                 (hipStream_t)stream);
+    if (rc <= 0) return rc;
+  }
   SaArgs a{search_inst(ctx), p->chains, n, p->steps, p->window, wtypes, p->inv_t0, p->inv_alpha,
            (uint32_t)p->seed, (uint32_t)(p->seed >> 32), p->step0, d_cur, d_cur_key, d_best,
            d_best_key, wpc};
@@ -2277,7 +2212,7 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
   if (p->window > 0 && in.problem == VRPMS_CVRP && in.uniform_cap &&
       in.min_start == in.max_start && in.max_dem <= in.cap0 && in.max_dem <= 65535 &&
       route_max(in.K) <= 255 &&
-      n <= 65535 && ctx->opt_sa_route != 2) {
+      n <= 65535 && ctx->opt_sa_route != 2) {  // (0 auto, 3 force this kernel)
     const size_t npad = ((size_t)n + 7) & ~(size_t)7;
     const size_t wbytes = ((size_t)route_wave_bytes((int)npad, in.K) + 15) & ~(size_t)15;
     const int elem = in.use16 ? 2 : 4;
