@@ -231,7 +231,10 @@ int vrpms_ga_generation(vrpms_ctx* ctx, const vrpms_ga_params* p, uint16_t* d_po
 /* Ant colony (api/{tsp,vrp}/aco/index.py), integer pheromone so every
  * update is exact and order-independent: w_ij = (tau_ij >> 8) * eta_ij,
  * eta_ij = floor(2^24 / (1 + D_ij)^2); tau <- clamp(tau - tau >> evap_shift);
- * the iteration-best ant deposits floor(2^30 / (1 + primary)) per edge. */
+ * the iteration-best ant deposits floor(2^30 / (1 + primary)) per edge --
+ * or, every bsf_period-th iteration ((iter + 1) % bsf_period == 0, best-so-far
+ * buffers given), the colony's best-so-far does (max-min global-best update:
+ * an island migrant injected into the best-so-far then shapes tau). */
 typedef struct {
   int32_t colonies;
   int32_t ants;        /* per colony, one wavefront each */
@@ -239,6 +242,7 @@ typedef struct {
   uint32_t tau_min, tau_max;  /* tau_max <= 2^31 */
   uint64_t seed;
   uint64_t iter;       /* global iteration index (Philox counter) */
+  uint32_t bsf_period; /* 0: the iteration best always deposits */
 } vrpms_aco_params;
 
 /* d_tau [colonies][N][N] <- tau0, d_eta [N][N] <- floor(2^24 / (1 + D)^2). */

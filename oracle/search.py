@@ -233,9 +233,16 @@ def aco_eta(D0) -> np.ndarray:
 
 
 def aco_iteration(score: Scorer, tau, eta, ants: int, n: int, seed: int, it: int,
-                  evap_shift: int, tau_min: int, tau_max: int):
+                  evap_shift: int, tau_min: int, tau_max: int, best=None, bsf_period: int = 0):
     """tau: list (per colony) of int64 [N][N] arrays, updated in place.
-    Returns (tours[colony][ant], keys[colony][ant], iter_best[(key, ant)])."""
+    Returns (tours[colony][ant], keys[colony][ant], iter_best[(key, ant)]).
+
+    best: optional (tours[colony], keys[colony]) best-so-far, updated in
+    place when the iteration best is strictly better.  bsf_period > 0: on
+    iterations with (it + 1) % bsf_period == 0 the colony's best-so-far
+    (after that update) deposits instead of the iteration best (max-min ant
+    system's global-best update; migrants injected into the best-so-far
+    then shape the pheromone).  Anchor: api/vrp/aco/index.py:40-45."""
     skey = spec.seed_key(seed)
     N = eta.shape[0]
     all_tours, all_keys, ib = [], [], []
@@ -262,10 +269,16 @@ def aco_iteration(score: Scorer, tau, eta, ants: int, n: int, seed: int, it: int
         keys = [score(t) for t in tours]
         b = min(range(ants), key=lambda a: (keys[a], a))
         ib.append((keys[b], b))
+        dkey, t = keys[b], tours[b]
+        if best is not None:
+            if keys[b] < best[1][colony]:
+                best[0][colony] = list(tours[b])
+                best[1][colony] = keys[b]
+            if bsf_period > 0 and (it + 1) % bsf_period == 0:
+                dkey, t = best[1][colony], best[0][colony]
         T[:] = np.minimum(tau_max, np.maximum(tau_min, T - (T >> evap_shift)))
-        primary = (keys[b] >> 28) & ((1 << 28) - 1)
+        primary = (dkey >> 28) & ((1 << 28) - 1)
         dep = (1 << 30) // (1 + primary)
-        t = tours[b]
         for q in range(n + 1):
             fr = 0 if q == 0 else t[q - 1]
             to = 0 if q == n else t[q]

@@ -570,3 +570,43 @@ def test_tsp_batch_tsp50_int32_staging_matches_c_restatement(ctx, coracle, lo, h
     rt, rk = coracle.tsp_batch_sa(mats, 200, 1 / (0.3 * lo), 1 / 0.99, 77)
     assert (tours.cpu().numpy().view(np.uint16) == rt).all()
     assert u64(keys) == [int(k) for k in rk]
+
+
+@pytest.mark.parametrize("name,maker", [ACO_SIZES[1], ACO_SIZES[3]], ids=["cvrp100", "cvrp300"])
+def test_aco_best_so_far_deposit_matches_oracle(ctx, name, maker):
+    """Max-min global-best deposits (bsf_period): every 2nd iteration the
+    colony's best-so-far -- here seeded with a migrant-like tour that beats
+    the first ants -- deposits instead of the iteration best; tau, tours,
+    keys and the best-so-far equal the oracle on the fused (N <= 256) and
+    the multi-launch (N > 256) update paths."""
+    torch = torch_()
+    inst = maker()
+    load(ctx, inst)
+    colonies, ants, tau0, n = 2, 8, 1 << 20, inst.n
+    tau, eta = ctx.aco_init(colonies, tau0)
+    ref_eta = search.aco_eta(inst.durations[0])
+    rtau = [np.full((inst.N, inst.N), tau0, dtype=np.int64) for _ in range(colonies)]
+    sc = scorer(inst)
+    # colony 0 starts from a good injected tour (a greedy nearest-neighbour order), colony 1 empty
+    D0 = inst.durations[0]
+    cur, left, nn = 0, set(range(1, n + 1)), []
+    while left:
+        cur = min(left, key=lambda c: (D0[cur, c], c))
+        nn.append(cur)
+        left.remove(cur)
+    rbest = [[list(nn), [0] * n], [sc(nn), 2**64 - 1]]
+    bt = torch.tensor([nn, [0] * n], dtype=torch.int16, device=ctx.dev)
+    bk = torch.tensor([sc(nn) - (1 << 64) if sc(nn) >= 1 << 63 else sc(nn), -1], dtype=torch.int64,
+                      device=ctx.dev)
+    for it in range(4):
+        tours, keys, ib = ctx.aco_iteration(tau, eta, ants, seed=5, it=it, evap_shift=3,
+                                            tau_min=1 << 10, tau_max=1 << 30, best_tours=bt,
+                                            best_keys=bk, bsf_period=2)
+        rt, rk, rib = search.aco_iteration(sc, rtau, ref_eta, ants, n, 5, it, 3, 1 << 10, 1 << 30,
+                                           best=rbest, bsf_period=2)
+        assert tours.cpu().numpy().tolist() == rt
+        assert u64(keys) == [k for ks in rk for k in ks]
+        assert [(a & (2**64 - 1), b) for a, b in ib.cpu().tolist()] == rib
+        got_tau = tau.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+        assert all((got_tau[c] == rtau[c]).all() for c in range(colonies)), it
+        assert bt.cpu().numpy().tolist() == rbest[0] and u64(bk) == rbest[1]

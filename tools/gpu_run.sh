@@ -67,6 +67,15 @@ for step in "$@"; do
           --output-format csv -d "$OUT/pmc_l2_sq" -o run -- $S
       run pmc_l2_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/pmc_l2_stats" -o run -- $S
       cd "$ROOT" ;;
+    pmc_seg)
+      cd /tmp
+      S="python3 $ROOT/tools/seg_run.py 256 128 1000"
+      run pmc_seg_a 300 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS \
+          --output-format csv -d "$OUT/pmc_seg_a" -o run -- $S
+      run pmc_seg_b 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_SCA \
+          --output-format csv -d "$OUT/pmc_seg_b" -o run -- $S
+      run pmc_seg_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/pmc_seg_stats" -o run -- $S
+      cd "$ROOT" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -37,8 +37,10 @@ def main():
                          "cvrp100, pack otherwise)")
     ap.add_argument("--window", type=int, default=None,
                     help="A11 move window (default: 0 for cvrp100, 32 otherwise)")
-    ap.add_argument("--instance", default="cvrp100", choices=["cvrp100", "cvrp200", "x1000"],
-                    help="cfg 2 CVRP-100 K=8, CVRP-200 K=16, or cfg 4 X-style CVRP-1000")
+    ap.add_argument("--instance", default="cvrp100",
+                    choices=["cvrp100", "cvrp200", "x1000", "tdvrp200"],
+                    help="cfg 2 CVRP-100 K=8, CVRP-200 K=16, cfg 4 X-style CVRP-1000, or cfg 3 "
+                         "time-dependent VRP-200 x 24 hourly matrices (K=16, start 480)")
     ap.add_argument("--sep", type=int, default=None,
                     help="A10 route separators per tour (default K - 1; 0 = plain giant tours)")
     ap.add_argument("--moves", type=int, default=64,
@@ -65,7 +67,8 @@ def main():
     t_start = time.time()
     make = {"cvrp100": lambda s: synth.cvrp(100, 8, seed=s),
             "cvrp200": lambda s: synth.cvrp(200, 16, seed=s),
-            "x1000": lambda s: synth.x_style(1000, seed=s)}[args.instance]
+            "x1000": lambda s: synth.x_style(1000, seed=s),
+            "tdvrp200": lambda s: synth.td_cvrp(200, 16, seed=s)}[args.instance]
     for seed in args.seeds:
         inst = make(seed)
         ctx.set_instance(CVRP, inst.durations, inst.demand, inst.capacities, inst.start_times)

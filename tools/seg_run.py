@@ -1,0 +1,26 @@
+#!/usr/bin/env python3
+"""sa_seg_kernel alone on cfg 4 (X-1000, K - 1 separators, first-fit
+starts, windowed 2-opt + swap / relocate anywhere) -- a short target for
+rocprofv3 --pmc / --stats passes.  usage: seg_run.py [chains] [moves] [steps]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from vrpms_amd import runners, synth  # noqa: E402
+from vrpms_amd.core import CVRP, Context  # noqa: E402
+
+chains = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+moves = int(sys.argv[2]) if len(sys.argv) > 2 else 128
+steps = int(sys.argv[3]) if len(sys.argv) > 3 else 1000
+ctx = Context(0)
+x = synth.x_style(1000, seed=0)
+ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
+r = runners.SARunner(ctx, x.n, chains=chains, total_steps=2 * steps, durations=x.durations,
+                     n_sep=x.K - 1, window=32, window_types=2, start="pack", moves=moves)
+r.epoch(steps)
+r.epoch(steps)
+torch.cuda.synchronize()
+print("done", r.best()[0] >> 28 & (2 ** 28 - 1))

@@ -61,7 +61,7 @@ class GaParams(ctypes.Structure):
 class AcoParams(ctypes.Structure):
     _fields_ = [("colonies", _i32), ("ants", _i32), ("evap_shift", _i32),
                 ("tau_min", ctypes.c_uint32), ("tau_max", ctypes.c_uint32), ("seed", _u64),
-                ("iter", _u64)]
+                ("iter", _u64), ("bsf_period", ctypes.c_uint32)]
 
 
 class Pool(ctypes.Structure):

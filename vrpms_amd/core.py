@@ -262,10 +262,11 @@ class Context:
 
     def aco_iteration(self, tau, eta, ants: int, seed: int, it: int, evap_shift: int = 3,
                       tau_min: int = 1 << 10, tau_max: int = 1 << 30, best_tours=None,
-                      best_keys=None):
+                      best_keys=None, bsf_period: int = 0):
         """One ACO iteration -> (tours, keys, iteration-best (key, ant) per
         colony); `best_tours`/`best_keys` (per colony) are updated in place
-        on the device when given."""
+        on the device when given; with `bsf_period` > 0 the best-so-far
+        deposits on every bsf_period-th iteration."""
         torch = _torch()
         colonies = tau.shape[0]
         n = self.N - 1
@@ -273,7 +274,7 @@ class Context:
         keys = torch.empty((colonies, ants), dtype=torch.int64, device=self.dev)
         ib = torch.empty((colonies, 2), dtype=torch.int64, device=self.dev)
         p = _lib.AcoParams(colonies, ants, evap_shift, tau_min, tau_max,
-                           int(seed) & (2**64 - 1), int(it))
+                           int(seed) & (2**64 - 1), int(it), int(bsf_period))
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
         check(self.lib.vrpms_aco_iteration(self._ctx, ctypes.byref(p), tau.data_ptr(),
                                            eta.data_ptr(), tours.data_ptr(), keys.data_ptr(),

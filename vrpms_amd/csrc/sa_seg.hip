@@ -39,7 +39,7 @@
 
 namespace vrpms {
 
-constexpr int kSegRegs = 20;      // positions per lane in registers on a rebuild: n < 64 * 20
+constexpr int kSegRegs = 20;      // positions per lane in registers on an accept: n < 64 * 20
 constexpr int kSegMaxMoves = 8;   // moves per lane per step (64 M per step)
 
 struct SegArgs {
@@ -60,8 +60,8 @@ struct SegArgs {
   uint32_t chain_bytes;
 };
 
-// per-chain LDS: u32 [PE n+2 | PD n+2 | dur, dsp, pmx, smx rm+1 each | sparse
-// (lv-1) x rm], then u16 [tok n+2 | SC n+2 | SP, RB, FNE, LNE1 segs+2 each]
+// per-chain LDS: u32 [PE n+2 | PD n+2 | dur rm+1 | dsp, pmx, smx rm+1 each |
+// sparse (lv-1) x rm], then u16 [tok n+2 | SC n+2 | SP, RB, FNE, LNE1 segs+2]
 __host__ __device__ inline uint32_t seg_chain_bytes(int n, int segs, int rm, int lv) {
   const uint32_t np2 = ((uint32_t)n + 2u + 1u) & ~1u;
   const uint32_t u32s = 2u * np2 + 4u * (uint32_t)(rm + 1) + (uint32_t)(lv - 1) * (uint32_t)rm;
@@ -75,42 +75,49 @@ __host__ __device__ inline int seg_levels(int rm) {
   return lv;
 }
 
-// Inclusive scans over the 64 lanes (shuffles): add, max, and min from the top lane down.
-VRPMS_DEV uint32_t seg_scan_add(uint32_t v) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t o = (uint32_t)__shfl_up((int)v, off, 64);
-    if (lane >= off) v += o;
-  }
-  return v;
+// Wave64 inclusive scans in VALU (every lane active): Hillis-Steele inside
+// each 16-lane row by DPP row_shr 1, 2, 4, 8 (a lane shifted in from outside
+// the row reads 0), then the row totals (v_readlane) folded into the rows
+// above.  MAX needs values >= 0 (0 is its identity).  `total` = the wave's.
+template <bool MAX>
+VRPMS_DEV uint32_t dpp_scan(uint32_t v, uint32_t& total) {
+  auto op = [](uint32_t x, uint32_t y) { return MAX ? (x > y ? x : y) : x + y; };
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true));
+  const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+  const uint32_t s1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+  const uint32_t s2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 47);
+  const uint32_t s3 = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+  const int row = lane_id() >> 4;
+  uint32_t add = 0;
+  add = row >= 1 ? op(add, s0) : add;
+  add = row >= 2 ? op(add, s1) : add;
+  add = row >= 3 ? op(add, s2) : add;
+  total = op(op(s0, s1), op(s2, s3));
+  return op(v, add);
 }
-VRPMS_DEV int seg_scan_max(int v) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int o = __shfl_up(v, off, 64);
-    if (lane >= off) v = max(v, o);
-  }
-  return v;
-}
-VRPMS_DEV int seg_rscan_min(int v) {  // min over lanes >= this one
-  const int lane = lane_id();
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int o = __shfl_down(v, off, 64);
-    if (lane + off < 64) v = min(v, o);
-  }
-  return v;
-}
-VRPMS_DEV uint32_t seg_rscan_max(uint32_t v) {  // max over lanes >= this one
-  const int lane = lane_id();
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t o = (uint32_t)__shfl_down((int)v, off, 64);
-    if (lane + off < 64) v = max(v, o);
-  }
-  return v;
+
+// Suffix max (over this lane and the lanes above it), values >= 0: DPP
+// row_shl 1, 2, 4, 8, then the row heads of the rows above.
+VRPMS_DEV uint32_t dpp_rscan_max(uint32_t v, uint32_t& total) {
+  auto mx = [](uint32_t x, uint32_t y) { return x > y ? x : y; };
+  v = mx(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x101, 0xF, 0xF, true));
+  v = mx(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x102, 0xF, 0xF, true));
+  v = mx(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xF, 0xF, true));
+  v = mx(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x108, 0xF, 0xF, true));
+  const uint32_t h1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+  const uint32_t h2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 32);
+  const uint32_t h3 = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+  const uint32_t h0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+  const int row = lane_id() >> 4;
+  uint32_t add = 0;
+  add = row <= 2 ? mx(add, h3) : add;
+  add = row <= 1 ? mx(add, h2) : add;
+  add = row <= 0 ? mx(add, h1) : add;
+  total = mx(mx(h0, h1), mx(h2, h3));
+  return mx(v, add);
 }
 
 struct SegTabs {
@@ -118,16 +125,19 @@ struct SegTabs {
   uint16_t *tok, *SC, *SP, *RB, *FNE, *LNE1;
 };
 
-// The open route of a pricing walk and the routes it has closed.
-struct SegAcc {
-  uint32_t dur, load, prev;
-  uint32_t rsum, rmax;
-  int rcnt;
-};
+#ifdef VRPMS_SEG_PROF
+// per-chain counters (A/B builds only: tools/seg_prof.py): pricing ticks,
+// rebuild ticks, steps, accepts, lanes re-evaluated in full, setup ticks,
+// kernel ticks, rebuilds (wall_clock64, 100 MHz)
+__device__ unsigned long long g_seg_prof[8 * 8192];
+#endif
 
 template <typename MatT>
 __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+#ifdef VRPMS_SEG_PROF
+  const unsigned long long pk0 = wall_clock64();
+#endif
   // instance: demand / capacities / start times in LDS (matrix in L2), then
   // the depot legs leg[c] = D(0, c) = D(c, 0) (symmetric matrix)
   const StagedInst<MatT, 1> I = stage_inst<MatT, 1>(a.si, smem);
@@ -163,42 +173,43 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
     T.FNE = T.RB + (SEGS + 2);
     T.LNE1 = T.FNE + (SEGS + 2);
   }
-  auto d0 = [&](uint32_t x, uint32_t y) __attribute__((always_inline)) -> uint32_t {  // edge x -> y, 0 between two depots
-    if ((x | y) == 0u) return 0u;
+  auto d0 = [&](uint32_t x, uint32_t y) __attribute__((always_inline)) -> uint32_t {
+    if ((x | y) == 0u) return 0u;  // two depots: an empty route lasts 0
     if (x == 0u) return leg[y];
     if (y == 0u) return leg[x];
     return (uint32_t)M0[__umul24(x, N) + y];
   };
-  auto SPX = [&](int k, int S) __attribute__((always_inline)) -> int { return k < 0 ? -1 : (k >= S ? n : (int)T.SP[k]); };
-  auto SPv = [&](int l) __attribute__((always_inline)) { return l ? T.sp + (l - 1) * RM : T.dur; };
-
-  // ---- tables of the current tour from its tokens and edges (registers:
-  // position q = lane + 64 i; v_e[i] = edge into q, q <= n) -----------------
   int S = 0, R = 0, Tt = 0;
-  bool seg_ok = true;  // the tables hold the tour (else: full re-evaluation of every move)
-  uint32_t v_tok[kSegRegs], v_e[kSegRegs];  // the tour being (re)built, position lane + 64 i
+  bool seg_ok = false;  // the tables hold the tour (else: full re-evaluation of every move)
+  auto SPX = [&](int k) __attribute__((always_inline)) -> int {
+    return k < 0 ? -1 : (k >= S ? n : (int)T.SP[k]);
+  };
+  auto SPv = [&](int l) __attribute__((always_inline)) { return l ? T.sp + (l - 1) * RM : T.dur; };
+  auto tourA = [&](int q) __attribute__((always_inline)) { return (uint32_t)T.tok[q]; };
+
+  // ---- tables from the tokens in T.tok and the edges in T.PE[q + 1] -------
   auto rebuild = [&]() __attribute__((always_inline)) {
-    // positions: PE / PD prefix sums in one 64-bit DPP scan, SC in another
-    uint64_t carry = 0, scarry = 0;
     wave_sync();
-#pragma unroll
-    for (int i = 0; i < kSegRegs; ++i) {
-      if (64 * i > n) continue;  // wave-uniform; no break, so the loop unrolls
-      const int q = lane + 64 * i;
+    // positions: PE (edges) and PD (demands) prefix sums in one 64-bit DPP
+    // scan, the separator count SC in a 32-bit one, separator positions SP
+    uint64_t carry = 0;
+    uint32_t scarry = 0;
+#pragma unroll 1
+    for (int base = 0; base <= n; base += 64) {
+      const int q = base + lane;
       const bool in = q < n;
-      const uint32_t c = in ? v_tok[i] : 1u;
-      uint64_t v = q <= n ? ((uint64_t)(in && c ? (uint32_t)dem[c] : 0u) << 32) | v_e[i] : 0ull;
-      uint64_t sv = (in && c == 0u) ? 1ull : 0ull;
+      const uint32_t c = in ? (uint32_t)T.tok[q] : 1u;
+      uint64_t v = q <= n ? ((uint64_t)(in && c ? (uint32_t)dem[c] : 0u) << 32) | T.PE[q + 1] : 0ull;
       const uint64_t tot = wave_scan_add_u64(v);
-      const uint64_t stot = wave_scan_add_u64(sv);
+      uint32_t stot;
+      const uint32_t sv = dpp_scan<false>(in && c == 0u ? 1u : 0u, stot);
       if (q <= n) {
         T.PE[q + 1] = (uint32_t)(carry + v);
         T.PD[q + 1] = (uint32_t)((carry + v) >> 32);
       }
       if (in) {
-        T.tok[q] = (uint16_t)c;
         T.SC[q + 1] = (uint16_t)(scarry + sv);
-        if (c == 0u && scarry + sv <= (uint64_t)SEGS) T.SP[scarry + sv - 1] = (uint16_t)q;
+        if (c == 0u && scarry + sv <= (uint32_t)SEGS) T.SP[scarry + sv - 1] = (uint16_t)q;
       }
       carry += tot;
       scarry += stot;
@@ -210,128 +221,112 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
     }
     S = (int)scarry;
     wave_sync();
-    if (S > SEGS) {
-      seg_ok = false;
-      return;
-    }
-    // segments: routes of each (one lane per segment), first route RB, the
-    // nearest non-empty segments FNE / LNE1
-    uint32_t rcarry = 0;
-    int lcarry = 0;
+    seg_ok = S <= SEGS;
+    if (!seg_ok) return;
+    // segments, one lane each: how many routes the greedy split makes of it
+    // (binary-searched capacity cuts), the first route RB, the nearest
+    // non-empty segments at or before (LNE1, +1) / at or after (FNE)
+    uint32_t rcarry = 0, lcarry = 0;
+#pragma unroll 1
     for (int base = 0; base <= S; base += 64) {
       const int g = base + lane;
-      uint32_t cnt = 0;
-      int ne = 0;
+      uint32_t cnt = 0, ne = 0;
       if (g <= S) {
-        const int s0 = SPX(g - 1, S) + 1, s1 = SPX(g, S) - 1;
-        ne = s1 >= s0 ? 1 : 0;
-        const uint32_t load = ne ? T.PD[s1 + 1] - T.PD[s0] : 0u;
-        if (load <= cap) {
-          cnt = 1;
-        } else {  // greedy cuts, binary-searched on PD
-          uint32_t ld = 0;
-          int x = s0;
-          cnt = 1;
-          while (x <= s1) {
-            const uint32_t room = cap - ld;
-            if (T.PD[s1 + 1] - T.PD[x] <= room) break;
-            int lo = x - 1, hi = s1;
-            while (lo < hi) {
-              const int mid = (lo + hi + 1) >> 1;
-              if (T.PD[mid + 1] - T.PD[x] <= room) lo = mid; else hi = mid - 1;
-            }
-            ++cnt;
-            ld = 0;
-            x = lo + 1;
+        const int s0 = SPX(g - 1) + 1, s1 = SPX(g) - 1;
+        ne = s1 >= s0 ? 1u : 0u;
+        cnt = 1;
+        int x = s0;
+        while (x <= s1 && T.PD[s1 + 1] - T.PD[x] > cap) {  // cut: last q fitting from x
+          const uint32_t thr = T.PD[x] + cap;
+          int l = x, h = s1;  // first q in [x, s1] with PD[q + 1] > thr (exists)
+          while (l < h) {
+            const int md = (l + h) >> 1;
+            if (T.PD[md + 1] > thr) h = md; else l = md + 1;
           }
+          ++cnt;
+          x = l;
         }
       }
-      const uint32_t inc = seg_scan_add(cnt);
-      const int lne = seg_scan_max(ne ? g + 1 : 0);
+      uint32_t tc, tl;
+      const uint32_t inc = dpp_scan<false>(cnt, tc);
+      const uint32_t lne = dpp_scan<true>(ne ? (uint32_t)g + 1u : 0u, tl);
       if (g <= S) {
         T.RB[g] = (uint16_t)(rcarry + inc - cnt);
         T.LNE1[g] = (uint16_t)max(lcarry, lne);
       }
-      rcarry += (uint32_t)__shfl((int)inc, 63, 64);
-      lcarry = max(lcarry, __shfl(lne, 63, 64));
+      rcarry += tc;
+      lcarry = max(lcarry, tl);
     }
     R = (int)rcarry;
-    if (R > RM) {
-      seg_ok = false;
-      return;
-    }
-    int fcarry = S + 1;
-    for (int top = ((S) / 64) * 64; top >= 0; top -= 64) {
+    seg_ok = R <= RM;
+    if (!seg_ok) return;
+    uint32_t fcarry = 0;  // FNE[g] = S + 1 - (suffix max of S + 1 - g over non-empty g)
+#pragma unroll 1
+    for (int top = (S / 64) * 64; top >= 0; top -= 64) {
       const int g = top + lane;
-      int f = S + 1;
+      uint32_t f = 0;
       if (g <= S) {
-        const int s0 = SPX(g - 1, S) + 1, s1 = SPX(g, S) - 1;
-        f = s1 >= s0 ? g : S + 1;
+        const int s0 = SPX(g - 1) + 1, s1 = SPX(g) - 1;
+        f = s1 >= s0 ? (uint32_t)(S + 1 - g) : 0u;
       }
-      f = min(seg_rscan_min(f), fcarry);
-      if (g <= S) T.FNE[g] = (uint16_t)f;
-      fcarry = min(fcarry, __shfl(f, 0, 64));
+      uint32_t tf;
+      f = max(dpp_rscan_max(f, tf), fcarry);
+      if (g <= S) T.FNE[g] = (uint16_t)(S + 1 - (int)f);
+      fcarry = max(fcarry, tf);
     }
     if (lane == 0) T.RB[S + 1] = (uint16_t)R;
     wave_sync();
-    // route durations: one lane per segment
+    // route durations, one lane per segment
+#pragma unroll 1
     for (int g = lane; g <= S; g += 64) {
-      const int s0 = SPX(g - 1, S) + 1, s1 = SPX(g, S) - 1;
-      int r = T.RB[g];
-      const uint32_t load = s1 >= s0 ? T.PD[s1 + 1] - T.PD[s0] : 0u;
-      if (load <= cap) {
-        T.dur[r] = T.PE[s1 + 2] - T.PE[s0];
-      } else {
-        uint32_t ld = 0, du = 0, prev = 0;
-        int x = s0;
-        while (x <= s1) {
-          const uint32_t room = cap - ld;
-          const uint32_t F = T.tok[x];
-          const uint32_t ein = prev ? 0u : leg[F];  // a segment's routes start at the depot
-          if (T.PD[s1 + 1] - T.PD[x] <= room) {
-            du += ein + T.PE[s1 + 1] - T.PE[x + 1];
-            prev = T.tok[s1];
-            break;
-          }
-          int lo = x - 1, hi = s1;
-          while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (T.PD[mid + 1] - T.PD[x] <= room) lo = mid; else hi = mid - 1;
-          }
-          du += ein + T.PE[lo + 1] - T.PE[x + 1];
-          T.dur[r++] = du + leg[T.tok[lo]];
-          du = ld = 0;
-          prev = 0;
-          x = lo + 1;
+      const int s0 = SPX(g - 1) + 1, s1 = SPX(g) - 1;
+      int r = T.RB[g], x = s0;
+      while (x <= s1 && T.PD[s1 + 1] - T.PD[x] > cap) {
+        const uint32_t thr = T.PD[x] + cap;
+        int l = x, h = s1;
+        while (l < h) {
+          const int md = (l + h) >> 1;
+          if (T.PD[md + 1] > thr) h = md; else l = md + 1;
         }
-        T.dur[r] = du + (prev ? leg[prev] : 0u);
+        // route: depot -> A[x..l-1] -> depot
+        T.dur[r++] = leg[T.tok[x]] + T.PE[l] - T.PE[x + 1] + leg[T.tok[l - 1]];
+        x = l;
       }
+      // the last (or only) route: A[x..s1], closed by the separator (or the end)
+      T.dur[r] = x <= s1 ? leg[T.tok[x]] + T.PE[s1 + 2] - T.PE[x + 1] : T.PE[s1 + 2] - T.PE[x];
     }
     wave_sync();
-    // per-route prefix sums / maxima, suffix maxima, sparse table
+    // per-route prefix sums / maxima (dsp / pmx [r] over routes < r), suffix
+    // maxima (smx [r] over routes >= r), sparse table of maxima
     uint32_t cds = 0, cmx = 0;
-    for (int base = 0; base <= R; base += 64) {
+#pragma unroll 1
+    for (int base = 0; base < R; base += 64) {
       const int r = base + lane;
       const uint32_t d = r < R ? T.dur[r] : 0u;
-      const uint32_t ids = seg_scan_add(d);
-      const uint32_t imx = (uint32_t)seg_scan_max((int)d);  // durations < 2^31
-      const uint32_t ex_mx = (uint32_t)__shfl_up((int)imx, 1, 64);
-      if (r <= R) {
-        T.dsp[r] = cds + ids - d;
-        T.pmx[r] = max(cmx, lane ? ex_mx : 0u);
+      uint32_t ts, tm;
+      const uint32_t ids = dpp_scan<false>(d, ts), imx = dpp_scan<true>(d, tm);
+      if (r < R) {
+        T.dsp[r + 1] = cds + ids;
+        T.pmx[r + 1] = max(cmx, imx);
       }
-      cds += (uint32_t)__shfl((int)ids, 63, 64);
-      cmx = max(cmx, (uint32_t)__shfl((int)imx, 63, 64));
+      cds += ts;
+      cmx = max(cmx, tm);
     }
     uint32_t smx = 0;
+#pragma unroll 1
     for (int top = (R / 64) * 64; top >= 0; top -= 64) {
       const int r = top + lane;
-      const uint32_t d = r < R ? T.dur[r] : 0u;
-      const uint32_t s = max(seg_rscan_max(d), smx);
-      if (r <= R) T.smx[r] = s;
-      smx = max(smx, (uint32_t)__shfl((int)s, 0, 64));
+      uint32_t tm;
+      const uint32_t sm = max(dpp_rscan_max(r < R ? T.dur[r] : 0u, tm), smx);
+      if (r <= R) T.smx[r] = sm;
+      smx = max(smx, tm);
+    }
+    if (lane == 0) {
+      T.dsp[0] = 0u;
+      T.pmx[0] = 0u;
     }
     wave_sync();
+#pragma unroll 1
     for (int l = 1; l < LV; ++l) {
       const int w = 1 << (l - 1);
       const uint32_t* src = SPv(l - 1);
@@ -341,43 +336,62 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
     }
     const int l1 = T.LNE1[S];
     Tt = l1 ? S - (l1 - 1) : S;
-    seg_ok = true;
   };
-  auto rmaxq = [&](int r0, int r1) __attribute__((always_inline)) -> uint32_t {  // max dur over routes r0..r1
+  auto rmaxq = [&](int r0, int r1) __attribute__((always_inline)) -> uint32_t {  // routes r0..r1
     if (r0 > r1) return 0u;
     const int l = 31 - __builtin_clz((uint32_t)(r1 - r0 + 1));
     const uint32_t* t = SPv(l);
     return max(t[r0], t[r1 - (1 << l) + 1]);
   };
 
-  // ---- the current tour ------------------------------------------------------
+  // ---- the current tour: tokens and edges into LDS ----------------------------
   {
     const uint16_t* gcur = a.cur + (int64_t)chain * n;
-#pragma unroll
-    for (int i = 0; i < kSegRegs; ++i) {
-      const int q = lane + 64 * i;
-      v_tok[i] = q < n ? min((uint32_t)gcur[q], Nm1) : 0u;
-      const uint32_t p = q >= 1 && q - 1 < n ? min((uint32_t)gcur[q - 1], Nm1) : 0u;
-      v_e[i] = q <= n ? d0(p, v_tok[i]) : 0u;
+    for (int q = lane; q <= n; q += 64) {
+      const uint32_t c = q < n ? min((uint32_t)gcur[q], Nm1) : 0u;
+      const uint32_t p = q >= 1 ? min((uint32_t)gcur[q - 1], Nm1) : 0u;
+      if (q < n) T.tok[q] = (uint16_t)c;
+      T.PE[q + 1] = d0(p, c);
     }
-    rebuild();
-  }
-  auto tourA = [&](int q) { return (uint32_t)T.tok[q]; };
-  uint64_t ck;
-  if (seg_ok && R - Tt <= K) {
-    ck = cvrp_key(0, T.dsp[R], T.smx[0], I.sp.objective);
-  } else {
-    ck = eval_tour<true>(I.D, I.sp, tourA, n).key;
   }
   uint16_t* gbest = a.best + (int64_t)chain * n;
   uint64_t bk = a.best_key[chain];
-  if (ck < bk) {
-    bk = ck;
-    for (int q = lane; q < n; q += 64) gbest[q] = T.tok[q];
-  }
-
+  uint64_t ck = 0;
+  bool need_build = true, first = true;
   float invT = a.inv_t0;
-  for (int st = 0; st < a.steps && n >= 2; ++st) {
+#ifdef VRPMS_SEG_PROF
+  unsigned long long pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+#pragma unroll 1
+  for (int st = 0;; ++st) {
+    if (need_build) {
+#ifdef VRPMS_SEG_PROF
+      const unsigned long long pb0 = wall_clock64();
+#endif
+      rebuild();
+      need_build = false;
+#ifdef VRPMS_SEG_PROF
+      pf[1] += wall_clock64() - pb0;
+      pf[7] += 1;
+#endif
+      if (first) {  // the start tour's key: from the tables when it serves everyone
+        first = false;
+        if (seg_ok && R - Tt <= K) ck = cvrp_key(0, T.dsp[R], T.smx[0], I.sp.objective);
+        else ck = eval_tour<true>(I.D, I.sp, tourA, n).key;
+#ifdef VRPMS_SEG_PROF
+        pf[5] = wall_clock64() - pk0;
+#endif
+      }
+      if (ck < bk) {
+        bk = ck;
+        for (int q = lane; q < n; q += 64) gbest[q] = T.tok[q];
+      }
+    }
+    if (st >= a.steps || n < 2) break;
+#ifdef VRPMS_SEG_PROF
+    const unsigned long long pt0 = wall_clock64();
+    int nfull = 0;
+#endif
     const uint64_t step = a.step0 + (uint64_t)st;
     // an unserved customer cannot be accepted from a tour serving everyone
     // when 2^28 * invT puts the acceptance threshold at 0 (sa_route_kernel)
@@ -385,202 +399,189 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
     uint64_t bkey = ~0ull;
     uint32_t bidx = 0xffffffffu, bw = 0;
     Move bmv{0, 0, 0};
-    uint32_t bj[4] = {0, 0, 0, 0};
-    for (int mm_ = 0; mm_ < a.M; ++mm_) {
-      const uint32_t idx = (uint32_t)(lane + 64 * mm_);
+    uint32_t bj0 = 0, bj1 = 0, bj2 = 0, bj3 = 0;
+#pragma unroll 1
+    for (int mi = 0; mi < a.M; ++mi) {
+      const uint32_t idx = (uint32_t)(lane + 64 * mi);
       const u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)chain, idx,
                              a.seed_lo, a.seed_hi);
       const Move m = decode_move_window(r.x, r.y, r.z, n, a.window, a.window_types);
       const MoveMap mmap = move_map(m);
-      auto B = [&](int p) -> uint32_t {  // token of the moved tour (0 outside the tour)
+      auto B = [&](int p) __attribute__((always_inline)) -> uint32_t {  // moved tour, 0 outside
         return (uint32_t)p < (uint32_t)n ? tourA(map_src(mmap, p)) : 0u;
       };
       const int lo = min(m.i, m.j), hi = max(m.i, m.j);
-      // junction edges of the moved tour at positions lo, lo + 1, hi, hi + 1
+      // the junction edges of the moved tour at positions lo, lo + 1, hi, hi + 1
       const uint32_t b0 = B(lo - 1), b1 = B(lo), b2 = B(lo + 1), b3 = B(hi - 1), b4 = B(hi),
                      b5 = B(hi + 1);
       const uint32_t jx0 = d0(b0, b1), jx1 = d0(b1, b2), jx2 = d0(b3, b4), jx3 = d0(b4, b5);
-      uint64_t k;
+      uint64_t k = ~0ull;
+      bool full = !seg_ok;
       if (seg_ok) {
-        SegAcc c{0u, 0u, 0u, 0u, 0u, 0};
+        // the open route and what the walk has closed
+        uint32_t c_dur = 0, c_load = 0, c_prev = 0, c_sum = 0, c_max = 0;
+        int c_cnt = 0;
         uint32_t isum = 0, imax = 0;
         int icnt = 0, seps = 0;
         bool cust = false;
         auto close = [&]() __attribute__((always_inline)) {
-          const uint32_t d = c.dur + (c.prev ? leg[c.prev] : 0u);
-          c.rsum += d;
-          c.rmax = max(c.rmax, d);
-          ++c.rcnt;
-          c.dur = c.load = c.prev = 0u;
+          const uint32_t d = c_dur + (c_prev ? leg[c_prev] : 0u);
+          c_sum += d;
+          c_max = max(c_max, d);
+          ++c_cnt;
+          c_dur = c_load = c_prev = 0u;
         };
-        // customers A[x..y] joined in the moved order (rev: A[y] first); jv =
-        // the junction edge into the first one when the open route has a customer
+        // customers A[x..y] joined to the open route in the moved order (rev:
+        // A[y] first), cut where the greedy split's next customer does not
+        // fit; jv = the junction edge into the first one when the open route
+        // holds a customer
         auto run = [&](int x, int y, bool rev, uint32_t jv) __attribute__((always_inline)) {
           if (x > y) return;
           seps = 0;
           cust = true;
-          while (x <= y) {
-            const uint32_t room = cap - c.load;
-            const uint32_t F = rev ? T.tok[y] : T.tok[x];
-            const uint32_t ein = c.prev ? jv : leg[F];
-            if (T.PD[y + 1] - T.PD[x] <= room) {
-              c.dur += ein + T.PE[y + 1] - T.PE[x + 1];
-              c.load += T.PD[y + 1] - T.PD[x];
-              c.prev = rev ? T.tok[x] : T.tok[y];
-              return;
-            }
-            if (!rev) {
-              int l = x - 1, h = y;  // last q with PD[q + 1] - PD[x] <= room
-              while (l < h) {
-                const int md = (l + h + 1) >> 1;
-                if (T.PD[md + 1] - T.PD[x] <= room) l = md; else h = md - 1;
-              }
-              if (l >= x) {
-                c.dur += ein + T.PE[l + 1] - T.PE[x + 1];
-                c.load += T.PD[l + 1] - T.PD[x];
-                c.prev = T.tok[l];
-              }
-              close();
-              x = l + 1;
-            } else {
-              int l = x, h = y + 1;  // first z with PD[y + 1] - PD[z] <= room
+          while (true) {
+            const uint32_t room = cap - c_load;
+            const bool fits = T.PD[y + 1] - T.PD[x] <= room;
+            int pa = x, pb = y;
+            if (!fits) {
+              // first q in [x - 1, y + 1] with PD[q + 1] > thr, on the monotone PD
+              const int thr = rev ? (int)(T.PD[y + 1] - room) - 1 : (int)(T.PD[x] + room);
+              int l = x - 1, h = y + 1;
               while (l < h) {
                 const int md = (l + h) >> 1;
-                if (T.PD[y + 1] - T.PD[md] <= room) h = md; else l = md + 1;
+                if ((int)T.PD[md + 1] > thr) h = md; else l = md + 1;
               }
-              if (l <= y) {
-                c.dur += ein + T.PE[y + 1] - T.PE[l + 1];
-                c.load += T.PD[y + 1] - T.PD[l];
-                c.prev = T.tok[l];
-              }
-              close();
-              y = l - 1;
+              if (rev) pa = l + 1; else pb = l - 1;
             }
-          }
-        };
-        auto sep = [&]() __attribute__((always_inline)) {
-          close();
-          ++seps;
-        };
-        // A[x..y] in the moved order; jv = the junction edge into it
-        auto piece = [&](int x, int y, bool rev, uint32_t jv) __attribute__((always_inline)) {
-          if (x > y) return;
-          const int sa = T.SC[x], sb = T.SC[y + 1];
-          if (sa == sb) {
-            run(x, y, rev, jv);
-            return;
-          }
-          const int smin = T.SP[sa], smax = T.SP[sb - 1];
-          if (rev) run(smax + 1, y, true, jv);
-          else run(x, smin - 1, false, jv);
-          sep();
-          if (smin < smax) {  // whole segments of the current tour between the separators
-            const int g0 = T.SC[smin] + 1, g1 = T.SC[smax];
-            const int r0 = T.RB[g0], r1 = T.RB[g1 + 1];
-            if (rev && r1 - r0 != g1 - g0 + 1) {
-              // a segment of several routes splits differently reversed
-              for (int g = g1; g >= g0; --g) {
-                run(SPX(g - 1, S) + 1, SPX(g, S) - 1, true, 0u);
-                sep();
-              }
-            } else {
-              isum += T.dsp[r1] - T.dsp[r0];
-              imax = max(imax, rmaxq(r0, r1 - 1));
-              icnt += r1 - r0;
-              if (rev) {
-                const int gf = T.FNE[g0];
-                if (gf <= g1) {
-                  seps = gf - g0 + 1;
-                  cust = true;
-                } else {
-                  seps += g1 - g0 + 1;
-                }
-              } else {
-                const int gl = (int)T.LNE1[g1] - 1;
-                if (gl >= g0) {
-                  seps = g1 + 1 - gl;
-                  cust = true;
-                } else {
-                  seps += g1 - g0 + 1;
-                }
-              }
+            if (pa <= pb) {
+              const uint32_t F = rev ? T.tok[pb] : T.tok[pa];
+              c_dur += (c_prev ? jv : leg[F]) + T.PE[pb + 1] - T.PE[pa + 1];
+              c_load += T.PD[pb + 1] - T.PD[pa];
+              c_prev = rev ? T.tok[pa] : T.tok[pb];
             }
+            if (fits) break;
+            close();
+            if (rev) y = pa - 1; else x = pb + 1;
           }
-          if (rev) run(x, smin - 1, true, 0u);
-          else run(smax + 1, y, false, 0u);
         };
         const int s0 = T.SC[lo];
-        const int stp = SPX(s0 - 1, S) + 1;
-        const int en = SPX(T.SC[hi + 1], S);
+        const int stp = SPX(s0 - 1) + 1;
+        const int en = SPX(T.SC[hi + 1]);
+        const bool opt = m.typ == kMove2Opt, swp = m.typ == kMoveSwap, fwd = m.i < m.j;
+        // the start of the first changed segment, up to lo
         run(stp, lo - 1, false, 0u);
-        // the moved span as pieces of the current tour (moved_index, tour.hpp),
-        // then the rest of the last changed segment: four slots, one code path
-        int px[4], py[4];
-        uint32_t pj[4];  // junction edge into the slot (moved positions lo, lo + 1 / hi, hi, hi + 1)
-        bool pr[4];
-        {
-          const bool opt = m.typ == kMove2Opt, swp = m.typ == kMoveSwap, fwd = m.i < m.j;
-          // slot 0: 2-opt A[i..j] reversed | swap A[j] | relocate A[i+1..j] or A[i]
-          px[0] = opt ? m.i : swp ? m.j : fwd ? m.i + 1 : m.i;
-          py[0] = opt ? m.j : swp ? m.j : fwd ? m.j : m.i;
-          pr[0] = opt;
-          pj[0] = jx0;
-          // slot 1: swap A[i+1..j-1] | relocate A[i] or A[j..i-1]
-          px[1] = opt ? 1 : swp ? m.i + 1 : fwd ? m.i : m.j;
-          py[1] = opt ? 0 : swp ? m.j - 1 : fwd ? m.i : m.i - 1;
-          pr[1] = false;
-          pj[1] = fwd && !swp ? jx2 : jx1;
-          // slot 2: swap A[i]
-          px[2] = swp ? m.i : 1;
-          py[2] = swp ? m.i : 0;
-          pr[2] = false;
-          pj[2] = jx2;
-          // slot 3: the rest of the last changed segment, to its separator
-          px[3] = hi + 1;
-          py[3] = en < n ? en : n - 1;
-          pr[3] = false;
-          pj[3] = jx3;
+        // The moved span as pieces of the current tour (moved_index,
+        // tour.hpp) in four slots -- 2-opt [A[i..j] reversed] | swap [A[j]]
+        // [A[i+1..j-1]] [A[i]] | relocate i<j [A[i+1..j]] [A[i]] | relocate
+        // i>j [A[i]] [A[j..i-1]] -- then slot 3, the rest of the last changed
+        // segment A[hi+1 .. en] (its closing separator included).  Every lane
+        // runs the same four predicated steps per slot, so the wave's control
+        // flow stays uniform: the part before the piece's first separator (in
+        // the moved order) joins the open route, the separator closes it,
+        // whole segments between its separators come from the route tables,
+        // the part after its last separator opens the next route.
+#pragma unroll 1
+        for (int sl = 0; sl < 4; ++sl) {
+          int x, y;
+          uint32_t jv;
+          if (sl == 0) {
+            x = opt ? m.i : swp ? m.j : fwd ? m.i + 1 : m.i;
+            y = opt ? m.j : swp ? m.j : fwd ? m.j : m.i;
+            jv = jx0;
+          } else if (sl == 1) {
+            x = opt ? 1 : swp ? m.i + 1 : fwd ? m.i : m.j;
+            y = opt ? 0 : swp ? m.j - 1 : fwd ? m.i : m.i - 1;
+            jv = fwd && !swp ? jx2 : jx1;
+          } else if (sl == 2) {
+            x = swp ? m.i : 1;
+            y = swp ? m.i : 0;
+            jv = jx2;
+          } else {
+            x = hi + 1;
+            y = en < n ? en : n - 1;
+            jv = jx3;
+          }
+          const bool rev = opt && sl == 0;
+          const bool live = x <= y;
+          const int sa = live ? (int)T.SC[x] : 0, sb = live ? (int)T.SC[y + 1] : 0;
+          const bool hs = sa != sb;  // the piece holds a separator
+          const int smin = hs ? (int)T.SP[sa] : 0, smax = hs ? (int)T.SP[sb - 1] : 0;
+          // (A) up to the first separator in the moved order
+          run(!hs ? x : rev ? smax + 1 : x, !hs ? (live ? y : x - 1) : rev ? y : smin - 1, rev, jv);
+          if (hs) {
+            // (B) the separator closes the open route
+            close();
+            ++seps;
+            // (C) whole segments between the piece's separators
+            if (smin < smax) {
+              const int g0 = T.SC[smin] + 1, g1 = T.SC[smax];
+              const int r0 = T.RB[g0], r1 = T.RB[g1 + 1];
+              if (rev && r1 - r0 != g1 - g0 + 1) {
+                // reversed and split by capacity: a reversal splits differently, walk them
+                for (int g = g1; g >= g0; --g) {
+                  run(SPX(g - 1) + 1, SPX(g) - 1, true, 0u);
+                  close();
+                  ++seps;
+                }
+              } else {
+                isum += T.dsp[r1] - T.dsp[r0];
+                imax = max(imax, rmaxq(r0, r1 - 1));
+                icnt += r1 - r0;
+                // the last customer in the moved order and the separators after it
+                const int gf = rev ? (int)T.FNE[g0] : (int)T.LNE1[g1] - 1;
+                const bool has = rev ? gf <= g1 : gf >= g0;
+                if (has) {
+                  seps = rev ? gf - g0 + 1 : g1 + 1 - gf;
+                  cust = true;
+                } else {
+                  seps += g1 - g0 + 1;
+                }
+              }
+            }
+          }
+          // (D) the part after the last separator opens the next route
+          run(hs ? (rev ? x : smax + 1) : 1, hs ? (rev ? smin - 1 : y) : 0, rev, 0u);
         }
-#pragma unroll
-        for (int sl = 0; sl < 4; ++sl) piece(px[sl], py[sl], pr[sl], pj[sl]);
         if (en >= n) close();  // the tour's end closes the last route
         const int glast = en < n ? (int)T.SC[en] : S;
         const int ra = T.RB[s0], rz = T.RB[glast + 1];
-        const int RBn = R - (rz - ra) + c.rcnt + icnt;
+        const int Rb = R - (rz - ra) + c_cnt + icnt;
         int Tb = Tt;
         const bool tail_kept = en < n && (int)T.LNE1[S] - 1 > glast;
         if (!tail_kept && cust) Tb = seps + (en < n ? n - 1 - en : 0);
-        if (RBn - Tb <= K) {
-          const uint32_t dsum = T.dsp[ra] + c.rsum + isum + T.dsp[R] - T.dsp[rz];
-          const uint32_t dmax = max(max(T.pmx[ra], T.smx[rz]), max(imax, c.rmax));
+        if (Rb - Tb <= K) {
+          const uint32_t dsum = T.dsp[ra] + c_sum + isum + T.dsp[R] - T.dsp[rz];
+          const uint32_t dmax = max(max(T.pmx[ra], T.smx[rz]), max(imax, c_max));
           k = cvrp_key(0, dsum, dmax, I.sp.objective);
         } else if (shortcut) {
           k = ~0ull;
         } else {
-          auto moved = [&](int q) { return tourA(map_src(mmap, q)); };
-          k = eval_tour<true>(I.D, I.sp, moved, n).key;
+          full = true;
         }
-      } else {
+      }
+      if (full) {
         auto moved = [&](int q) { return tourA(map_src(mmap, q)); };
         k = eval_tour<true>(I.D, I.sp, moved, n).key;
+#ifdef VRPMS_SEG_PROF
+        ++nfull;
+#endif
       }
       if (k < bkey) {  // ties keep the earlier (smaller) move index
         bkey = k;
         bidx = idx;
         bw = r.w;
         bmv = m;
-        bj[0] = jx0;
-        bj[1] = jx1;
-        bj[2] = jx2;
-        bj[3] = jx3;
+        bj0 = jx0;
+        bj1 = jx1;
+        bj2 = jx2;
+        bj3 = jx3;
       }
     }
     // the chain's (key, move index) minimum
     int wl;
-    const uint64_t kmin = wave_argmin_lane(bkey, wl);
-    const uint32_t imin = wave_min_u32_uniform(bkey == kmin ? bidx : 0xffffffffu);
+    const uint64_t k = wave_argmin_lane(bkey, wl);
+    const uint32_t imin = wave_min_u32_uniform(bkey == k ? bidx : 0xffffffffu);
     const int bl = (int)(imin & 63u);
-    const uint64_t k = kmin;
     const uint32_t uw = (uint32_t)wave_bcast((int)bw, bl);
     bool accept = k <= ck;
     if (!accept) {
@@ -588,47 +589,57 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
       const uint32_t dp = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
       accept = (uw >> 8) < accept_threshold(dp, invT);
     }
+#ifdef VRPMS_SEG_PROF
+    pf[0] += wall_clock64() - pt0;
+    pf[2] += 1;
+    pf[3] += accept ? 1 : 0;
+    pf[4] += (unsigned long long)__popcll(__ballot(nfull > 0));
+#endif
     if (accept) {
       Move mb;
       mb.typ = (uint32_t)wave_bcast((int)bmv.typ, bl);
       mb.i = wave_bcast(bmv.i, bl);
       mb.j = wave_bcast(bmv.j, bl);
-      const MoveMap mmb = move_map(mb);
       const int blo = min(mb.i, mb.j), bhi = max(mb.i, mb.j);
-      uint32_t wj[4];
+      // a move among separators only (e.g. two separators swapped) leaves the
+      // tour as it is: no rebuild
+      const bool same = (mb.typ == kMoveSwap && T.tok[blo] == T.tok[bhi]) ||
+                        (mb.typ != kMoveSwap && T.SC[bhi + 1] - T.SC[blo] == bhi - blo + 1);
+      ck = k;
+      if (!same) {
+        const MoveMap mmb = move_map(mb);
+        const uint32_t w0 = (uint32_t)wave_bcast((int)bj0, bl), w1 = (uint32_t)wave_bcast((int)bj1, bl);
+        const uint32_t w2 = (uint32_t)wave_bcast((int)bj2, bl), w3 = (uint32_t)wave_bcast((int)bj3, bl);
+        // the new tour's tokens and edges: a kept adjacency's edge is a
+        // difference of PE (forward, or reversed on the symmetric matrix; PE
+        // is complete even when the segment tables are not), the four
+        // junctions are the winner's gathers
+        uint32_t v_tok[kSegRegs], v_e[kSegRegs];
 #pragma unroll
-      for (int x = 0; x < 4; ++x) wj[x] = (uint32_t)wave_bcast((int)bj[x], bl);
-      // the new tour's tokens and edges: a kept adjacency's edge is a
-      // difference of PE (forward, or reversed on the symmetric matrix), the
-      // four junctions come from the winner's gathers
-#pragma unroll
-      for (int i = 0; i < kSegRegs; ++i) {
-        const int q = lane + 64 * i;
-        v_tok[i] = 0u;
-        v_e[i] = 0u;
-        if (q > n) continue;
-        const int sq = map_src(mmb, q), sp = map_src(mmb, q - 1);
-        if (q < n) v_tok[i] = T.tok[sq];
-        if (q == blo) v_e[i] = wj[0];
-        else if (q == blo + 1) v_e[i] = wj[1];
-        else if (q == bhi) v_e[i] = wj[2];
-        else if (q == bhi + 1) v_e[i] = wj[3];
-        else if (sp + 1 == sq) v_e[i] = T.PE[sq + 1] - T.PE[sq];
-        else v_e[i] = T.PE[sp + 1] - T.PE[sp];  // reversed: the edge between A[sq] and A[sp]
-      }
-      if (!seg_ok) {
-        // tables not held (too many separators / routes): edges from L2
+        for (int i = 0; i < kSegRegs; ++i) {
+          const int q = lane + 64 * i;
+          v_tok[i] = 0u;
+          v_e[i] = 0u;
+          if (q > n) continue;
+          const int sq = map_src(mmb, q), sp = map_src(mmb, q - 1);
+          if (q < n) v_tok[i] = T.tok[sq];
+          if (q == blo) v_e[i] = w0;
+          else if (q == blo + 1) v_e[i] = w1;
+          else if (q == bhi) v_e[i] = w2;
+          else if (q == bhi + 1) v_e[i] = w3;
+          else if (sp + 1 == sq) v_e[i] = T.PE[sq + 1] - T.PE[sq];
+          else v_e[i] = T.PE[sp + 1] - T.PE[sp];  // reversed: the edge between A[sq] and A[sp]
+        }
+        wave_sync();
 #pragma unroll
         for (int i = 0; i < kSegRegs; ++i) {
           const int q = lane + 64 * i;
           if (q > n) continue;
-          const uint32_t p = q >= 1 ? tourA(map_src(mmb, q - 1)) : 0u;
-          v_e[i] = d0(p, v_tok[i]);
+          if (q < n) T.tok[q] = (uint16_t)v_tok[i];
+          T.PE[q + 1] = v_e[i];
         }
-      }
-      rebuild();
-      ck = k;
-      if (ck < bk) {
+        need_build = true;
+      } else if (ck < bk) {
         bk = ck;
         for (int q = lane; q < n; q += 64) gbest[q] = T.tok[q];
       }
@@ -640,6 +651,11 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
   if (lane == 0) {
     a.cur_key[chain] = ck;
     a.best_key[chain] = bk;
+#ifdef VRPMS_SEG_PROF
+    pf[6] = wall_clock64() - pk0;
+    if (chain < 8192)
+      for (int i = 0; i < 8; ++i) g_seg_prof[8 * chain + i] += pf[i];
+#endif
   }
 }
 
@@ -683,3 +699,16 @@ int launch_sa_seg(const vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* d_cu
 }
 
 }  // namespace vrpms
+
+#ifdef VRPMS_SEG_PROF
+extern "C" int vrpms_debug_seg_prof(unsigned long long* out, int count, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vrpms::g_seg_prof), sizeof(unsigned long long) * count) !=
+      hipSuccess)
+    return -2;
+  if (reset) {
+    static unsigned long long zero[8 * 8192];
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(vrpms::g_seg_prof), zero, sizeof(zero));
+  }
+  return 0;
+}
+#endif

@@ -1676,14 +1676,16 @@ struct AcoUpdateArgs {
   uint32_t* tau;                 // [colonies][N][N]
   const uint16_t* tours;         // [colonies][ants][n]
   const uint64_t* ib;            // [colonies][2] iteration-best (key, ant)
+  int bsf;                       // this iteration the best-so-far deposits
 };
 
 // The end of an iteration for small matrices (N <= 256), one workgroup per
 // colony instead of four launches: the colony's iteration-best (key, ant)
 // (lowest ant on ties, as segment_argmin_kernel), its best-so-far when
 // strictly better (aco_track_best_kernel), evaporation of its tau, then the
-// deposit on the iteration-best tour (aco_deposit_kernel) -- colonies share
-// nothing, so the per-colony order is the whole order.
+// deposit on the iteration-best tour, or on a best-so-far iteration the
+// best-so-far's (aco_deposit_kernel) -- colonies share nothing, so the
+// per-colony order is the whole order.
 __global__ __launch_bounds__(1024) void aco_update_fused_kernel(AcoUpdateArgs a, const uint64_t* __restrict__ keys,
                                                                uint64_t* ib, uint16_t* best_tours,
                                                                uint64_t* best_keys) {
@@ -1716,10 +1718,16 @@ __global__ __launch_bounds__(1024) void aco_update_fused_kernel(AcoUpdateArgs a,
     ib[2 * c] = k;
     ib[2 * c + 1] = idx;
   }
-  if (best_tours && best_keys && k < best_keys[c]) {  // block-uniform
+  const bool tracked = best_tours && best_keys;
+  const uint64_t bsf_key = tracked ? best_keys[c] : ~0ull;  // block-uniform
+  __syncthreads();
+  if (tracked && k < bsf_key) {
     for (int q = threadIdx.x; q < a.n; q += blockDim.x) best_tours[(int64_t)c * a.n + q] = t[q];
     __syncthreads();
     if (threadIdx.x == 0) best_keys[c] = k;
+  } else if (tracked && a.bsf) {  // the (unchanged) best-so-far deposits
+    t = best_tours + (int64_t)c * a.n;
+    k = bsf_key;
   }
   // evaporation: 8 loads in flight per thread before the stores
   uint32_t* T = a.tau + (int64_t)c * a.N * a.N;
@@ -1751,14 +1759,19 @@ __global__ void aco_evaporate_kernel(AcoUpdateArgs a) {
   }
 }
 
-// deposit floor(2^30 / (1 + primary)) on every edge of the iteration-best tour
-__global__ void aco_deposit_kernel(AcoUpdateArgs a) {
+// deposit floor(2^30 / (1 + primary)) on every edge of the iteration-best
+// tour, or on a best-so-far iteration (a.bsf) of the colony's best-so-far
+// (already updated by aco_track_best_kernel)
+__global__ void aco_deposit_kernel(AcoUpdateArgs a, const uint16_t* best_tours,
+                                   const uint64_t* best_keys) {
   const int colony = blockIdx.x;
-  const uint64_t key = a.ib[2 * colony];
+  const bool bsf = a.bsf && best_tours && best_keys;
+  const uint64_t key = bsf ? best_keys[colony] : a.ib[2 * colony];
   const int ant = (int)a.ib[2 * colony + 1];
   const uint32_t primary = (uint32_t)((key >> 28) & ((1u << 28) - 1u));
   const uint32_t dep = (uint32_t)((1u << 30) / (1ull + primary));
-  const uint16_t* t = a.tours + ((int64_t)colony * a.ants + ant) * a.n;
+  const uint16_t* t = bsf ? best_tours + (int64_t)colony * a.n
+                          : a.tours + ((int64_t)colony * a.ants + ant) * a.n;
   uint32_t* T = a.tau + (int64_t)colony * a.N * a.N;
   for (int q = threadIdx.x; q <= a.n; q += blockDim.x) {
     const uint32_t from = q == 0 ? 0u : t[q - 1];
@@ -2383,8 +2396,9 @@ extern "C" int vrpms_aco_iteration(vrpms_ctx* ctx, const vrpms_aco_params* p, ui
     int rc = vrpms_eval(ctx, d_tours, 2, ants, n, n, d_keys, nullptr, nullptr, nullptr, stream);
     if (rc) return rc;
   }
+  const int bsf = p->bsf_period > 0 && (p->iter + 1) % p->bsf_period == 0 ? 1 : 0;
   AcoUpdateArgs u{p->colonies, p->ants, n, in.N, (uint32_t)p->evap_shift, p->tau_min, p->tau_max,
-                  d_tau, d_tours, d_iter_best};
+                  d_tau, d_tours, d_iter_best, bsf};
   if (in.N <= 256) {
     aco_update_fused_kernel<<<p->colonies, 1024, 0, s>>>(
         u, d_keys, d_iter_best, d_best_keys ? d_best_tours : nullptr, d_best_tours ? d_best_keys : nullptr);
@@ -2398,7 +2412,8 @@ extern "C" int vrpms_aco_iteration(vrpms_ctx* ctx, const vrpms_aco_params* p, ui
   const int64_t total = (int64_t)p->colonies * in.N * in.N;
   aco_evaporate_kernel<<<(unsigned)std::min<int64_t>((total + 255) / 256, ctx->num_cus * 8), 256, 0,
                          s>>>(u);
-  aco_deposit_kernel<<<p->colonies, 256, 0, s>>>(u);
+  aco_deposit_kernel<<<p->colonies, 256, 0, s>>>(u, d_best_keys ? d_best_tours : nullptr,
+                                                 d_best_tours ? d_best_keys : nullptr);
   VRPMS_HIP(hipGetLastError());
   return VRPMS_OK;
 }

@@ -150,18 +150,21 @@ class GARunner(_Base):
 
 class ACORunner(_Base):
     """Integer max-min ant colonies (one pheromone matrix per colony); each
-    colony's best-so-far is tracked on the device."""
+    colony's best-so-far is tracked on the device and deposits on every
+    `bsf_period`-th iteration (the iteration best on the others), so a
+    migrant injected into a colony's best-so-far shapes its pheromone."""
 
     inject_mode = INJECT_BETTER
 
     def __init__(self, ctx: Context, n: int, colonies: int = 4, ants: int = 64, seed: int = 0,
-                 iters_per_epoch: int = 5, evap_shift: int = 3):
+                 iters_per_epoch: int = 5, evap_shift: int = 3, bsf_period: int = 5):
         torch = _torch()
         if n != ctx.N - 1:
             raise ValueError("ACO builds complete giant tours: n must be N - 1")
         self.ctx, self.n, self.seed = ctx, n, seed
         self.colonies, self.ants = colonies, ants
         self.iters_per_epoch, self.evap_shift = iters_per_epoch, evap_shift
+        self.bsf_period = bsf_period
         self.tau_max, self.tau_min = 1 << 30, 1 << 12
         self.tau, self.eta = ctx.aco_init(colonies, 1 << 24)
         self.it = 0
@@ -172,7 +175,8 @@ class ACORunner(_Base):
         for _ in range(self.iters_per_epoch if iters is None else iters):
             self.ctx.aco_iteration(self.tau, self.eta, self.ants, self.seed, self.it,
                                    self.evap_shift, self.tau_min, self.tau_max,
-                                   best_tours=self.best_t, best_keys=self.best_key)
+                                   best_tours=self.best_t, best_keys=self.best_key,
+                                   bsf_period=self.bsf_period)
             self.it += 1
 
     # migrant e replaces colony e's best-so-far when better

@@ -69,6 +69,10 @@ def _matrix(durations) -> np.ndarray:
         raise ValueError("duration matrix must be [N][N] or [24][N][N]")
     if D.shape[0] not in (1, 24):
         raise ValueError("hour-indexed duration matrix must have 24 slices")
+    if np.issubdtype(D.dtype, np.integer):       # the DB's JSON integers: one check
+        if D.size and D.min() < 0:
+            raise ValueError("durations must be non-negative integers (minutes)")
+        return D.astype(np.int64, copy=False)
     if not np.issubdtype(D.dtype, np.number) or not np.all(np.isfinite(D)):
         raise ValueError("durations must be numbers")
     if np.any(D != np.floor(D)) or np.any(D < 0):
@@ -90,7 +94,8 @@ def compact_tsp(durations, customers, start_node, start_time=0) -> CompactInstan
             raise ValueError(f"customer {c} outside the {N}-node matrix")
         if c not in nodes:
             nodes.append(c)
-    sub = D[:, nodes][:, :, nodes]
+    # every node in matrix order (the common request): no copy
+    sub = D if nodes == list(range(N)) else D[:, nodes][:, :, nodes]
     return CompactInstance(TSP, sub, nodes, None, None, np.array([int(start_time or 0)]))
 
 
