@@ -234,3 +234,47 @@ def test_tsp_batcher_coalesces_and_groups_by_node_count():
     # other algorithms never ride the batcher
     status, body = app.post("tsp", "ga", json.dumps(bodies[0]).encode())
     assert status == 200 and app.batcher.launches == 2
+
+
+def test_remote_front_end_over_http(monkeypatch):
+    """A host without a GPU (VRPMS_REMOTE set) sends solve_tsp / solve_vrp /
+    solve_vrp_problem to the GPU box's HTTP host (POST /solve/...) with the
+    instance inline; here the box's solver slot is a stand-in that records
+    the compact request, so the wire path is checked on CPU."""
+    import threading
+
+    from vrpms_amd import remote, solver
+
+    seen = []
+
+    def fake_solve(problem, algorithm, params, knobs, locations, durations):
+        seen.append((problem, algorithm, params, knobs, locations, durations))
+        if problem == "tsp":
+            return {"duration": 24, "vehicle": [0, 1, 2, 3, 0]}
+        return {"durationMax": 21, "durationSum": 21,
+                "vehicles": [{"tour": [0, 1, 3, 0], "duration": 21}, {"tour": [0, 0], "duration": 0}]}
+
+    srv = service.serve(service.App(store(), solve=fake_solve), "127.0.0.1", 0)
+    th = threading.Thread(target=srv.serve_forever, daemon=True)
+    th.start()
+    try:
+        monkeypatch.setenv("VRPMS_REMOTE", f"http://127.0.0.1:{srv.server_address[1]}")
+        r = solver.solve_tsp("sa", MATRIX, [1, 2, 3], 0, 0)
+        assert r == {"duration": 24, "vehicle": [0, 1, 2, 3, 0]}
+        assert seen[-1][:3] == ("tsp", "sa", {"customers": [1, 2, 3], "start_node": 0,
+                                              "start_time": 0})
+        assert seen[-1][5] == MATRIX
+        locs = [{"id": i} for i in range(4)]
+        v = solver.solve_vrp("ga", MATRIX, locs, [5, 5], [0, 30], [2], [],
+                             random_permutation_count=10, iteration_count=5)
+        assert v["durationSum"] == 21
+        assert seen[-1][3] == {"random_permutationCount": 10, "iteration_count": 5}
+        assert seen[-1][2]["ignored_customers"] == [2]
+        p = solver.solve_vrp_problem(MATRIX, locs, [5, 5], [0, 30], [2], [])
+        assert p["tour"] == [0, 1, 3, 0] and p["total_time"] == 21 and p["unvisited"] == []
+        with pytest.raises(ValueError, match="Invalid request"):
+            remote._post(f"http://127.0.0.1:{srv.server_address[1]}", "tsp", "tabu", {},
+                                10)
+    finally:
+        srv.shutdown()
+        srv.server_close()

@@ -98,6 +98,11 @@ def test_solve_vrp_problem_default_and_bf_errors():
     assert bf["duration"] <= sa["duration"]
     with pytest.raises(ValueError, match="unknown algorithm"):
         solver.solve_tsp("tabu", tsp_matrix().tolist(), [1, 2], 0)
+    # an hour-indexed matrix keeps the lower cap (every edge priced at its hour)
+    import numpy as np
+    td = np.stack([tsp_matrix(13)] * 24)
+    with pytest.raises(ValueError, match=f"at most {solver.BF_MAX_CUSTOMERS_TD}"):
+        solver.solve_tsp("bf", td.tolist(), list(range(1, 13)), 0)
 
 
 def test_tiny_instances():

@@ -15,13 +15,15 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-LIB = os.path.join(ROOT, "build_ab", "segprof", "libvrpms.so")
+VARIANT = os.environ.get("SEG_PROF_VARIANT", "")  # e.g. NOCUT (A/B: no capacity cuts)
+LIB = os.path.join(ROOT, "build_ab", "segprof" + VARIANT.lower(), "libvrpms.so")
 
 
 def build():
     from vrpms_amd import build as b
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    cmd = [b.HIPCC, *b.FLAGS, "-shared", "-DVRPMS_SEG_PROF", "-o", LIB, *b.sources(),
+    extra = [f"-DVRPMS_SEG_{VARIANT}"] if VARIANT else []
+    cmd = [b.HIPCC, *b.FLAGS, "-shared", "-DVRPMS_SEG_PROF", *extra, "-o", LIB, *b.sources(),
            "-L/opt/rocm/lib", "-lrccl"]
     subprocess.run(cmd, check=True)
 

@@ -352,6 +352,50 @@ class App:
         return 200, {"success": True, "message": result}
 
 
+    def solve_inline(self, problem: str, algorithm: str, raw: bytes):
+        """POST /solve/{tsp,vrp}/<algo>: the instance inline (no DB) -- what a
+        host without a GPU sends to the GPU box (vrpms_amd.remote).  Body: the
+        solve_tsp / solve_vrp arguments in the request's camelCase names
+        ("durations" is the DB's `matrix` payload); response as the
+        handlers': {"success": true, "message": result} or a 400 error list."""
+        try:
+            content = json.loads(raw.decode("utf-8")) if raw else {}
+            if not isinstance(content, dict):
+                raise ValueError("the body must be a JSON object")
+        except ValueError as e:
+            return 400, {"success": False,
+                         "errors": [{"what": "Invalid request", "reason": str(e)}]}
+        if problem not in ("tsp", "vrp") or algorithm not in TITLES:
+            return 400, {"success": False, "errors": [
+                {"what": "Invalid request", "reason": f"no solver /solve/{problem}/{algorithm}"}]}
+        names = (["durations", "customers", "startNode", "startTime"] if problem == "tsp" else
+                 ["durations", "locations", "capacities", "startTimes", "ignoredCustomers",
+                  "completedCustomers"])
+        errors = []
+        vals = {name: get_parameter(name, content, errors) for name in names}
+        if errors:
+            return 400, {"success": False, "errors": errors}
+        if problem == "tsp":
+            params = {"customers": vals["customers"], "start_node": vals["startNode"],
+                      "start_time": vals["startTime"]}
+            knobs, locations = {}, None
+        else:
+            params = {"capacities": vals["capacities"], "start_times": vals["startTimes"],
+                      "ignored_customers": vals["ignoredCustomers"] or [],
+                      "completed_customers": vals["completedCustomers"] or []}
+            knobs = {"random_permutationCount": content.get("randomPermutationCount"),
+                     "iteration_count": content.get("iterationCount")}
+            locations = vals["locations"]
+        try:
+            with self.gpu_lock:
+                result = self._solve(problem, algorithm, params, knobs, locations,
+                                     vals["durations"])
+        except Exception as e:
+            return 400, {"success": False,
+                         "errors": [{"what": "Solver error", "reason": str(e)}]}
+        return 200, {"success": True, "message": result}
+
+
 def endpoint_handler(app: App, problem: str, algorithm: str):
     """A BaseHTTPRequestHandler class for one endpoint, with the reference's
     GET banner, POST contract and (VRP GA only) preflight response."""
@@ -404,6 +448,15 @@ def router(app: App):
                 self.send_header("Content-type", "text/plain")
                 self.end_headers()
                 self.wfile.write(b"Hello!")
+                return
+            if path.startswith("/solve/") and method == "POST":   # vrpms_amd.remote
+                _, _, problem, algorithm = (path.split("/") + ["", ""])[:4]
+                n = int(self.headers.get("Content-Length", 0))
+                status, body = app.solve_inline(problem, algorithm, self.rfile.read(n))
+                self.send_response(status)
+                self.send_header("Content-type", "application/json")
+                self.end_headers()
+                self.wfile.write(json.dumps(body).encode("utf-8"))
                 return
             cls = routes.get(path)
             fn = getattr(cls, "do_" + method, None) if cls else None

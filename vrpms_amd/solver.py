@@ -32,9 +32,12 @@ from .core import CVRP, OBJ_MAX, OBJ_SUM, TSP, Context
 
 ALGORITHMS = ("bf", "ga", "sa", "aco")
 # exhaustive search over n! giant tours: 13! = 6.2 G tours is ~0.1 s at the
-# measured ~64 G evals/s of bf_kernel on one MI355X (bench "search.bf");
+# measured ~64 G evals/s of bf_kernel on one MI355X (bench "search.bf") on a
+# static matrix; an hour-indexed one prices every edge at its departure
+# hour (several times slower), so it keeps 11 (39.9 M tours).
 # vrpms_bf_run itself accepts n <= 15 (nibble-packed tours)
 BF_MAX_CUSTOMERS = 13
+BF_MAX_CUSTOMERS_TD = 11
 # SA on tours of more than SA_WINDOW_MIN_N customers samples A11 windowed
 # moves (second position within SA_WINDOW of the first)
 SA_WINDOW, SA_WINDOW_MIN_N = 32, 150
@@ -166,8 +169,9 @@ def search(ctx: Context, ci: CompactInstance, algorithm: str, seed: int = 0,
     if n == 1:
         return None, [1]
     if algorithm == "bf":
-        if n > BF_MAX_CUSTOMERS:
-            raise ValueError(f"brute force supports at most {BF_MAX_CUSTOMERS} customers "
+        cap = BF_MAX_CUSTOMERS if ci.durations.shape[0] == 1 else BF_MAX_CUSTOMERS_TD
+        if n > cap:
+            raise ValueError(f"brute force supports at most {cap} customers "
                              f"({n} given)")
         return runners.brute_force(ctx, n)
     iters = knobs.get("iteration_count")
@@ -177,12 +181,14 @@ def search(ctx: Context, ci: CompactInstance, algorithm: str, seed: int = 0,
         # boundaries instead of leaving them to the greedy split alone
         n_sep = int(knobs.get("separators", len(ci.capacities) - 1 if ci.problem == CVRP else 0))
         # large tours: A11/A12 windowed 2-opt, swap / relocate anywhere
-        # (priced route-locally on an exchangeable fleet), from first-fit routes
+        # (priced in O(1) / route-locally); separators start where first-fit
+        # routes end (a feasible start on a tight fleet, where random
+        # separator positions would leave customers unserved)
         window = int(knobs.get("window", SA_WINDOW if n > SA_WINDOW_MIN_N else 0))
         r = runners.SARunner(ctx, n, chains=int(knobs.get("chains", 1024)), seed=seed,
                              total_steps=steps, durations=ci.durations, n_sep=n_sep,
                              window=window, window_types=int(knobs.get("window_types", 2)),
-                             start="pack" if window > 0 and n_sep > 0 else "random")
+                             start="pack" if n_sep > 0 else "random")
         epochs = max(1, steps // r.steps_per_epoch)
     elif algorithm == "ga":
         pop = int(knobs.get("random_permutation_count") or knobs.get("pop", 256))
@@ -217,9 +223,21 @@ def _decode(ctx: Context, tour):
     return ctx.decode(t, len(tour))
 
 
+def _remote():
+    """VRPMS_REMOTE set and no local GPU: the GPU box's URL (vrpms_amd.remote)."""
+    from . import remote
+    if remote.url() is None:
+        return None
+    import torch
+    return None if torch.cuda.is_available() else remote
+
+
 def solve_tsp(algorithm: str, durations, customers, start_node, start_time=0, *, seed: int = 0,
               time_limit: float | None = None, device: int = 0, **knobs) -> dict:
     """Result dict of the TSP TODO slot (api/tsp/ga/index.py:40-44)."""
+    rem = _remote()
+    if rem is not None:
+        return rem.solve_tsp(algorithm, durations, customers, start_node, start_time)
     ci = compact_tsp(durations, customers, start_node, start_time)
     ctx = context(device)
     load(ctx, ci)
@@ -234,6 +252,16 @@ def solve_vrp(algorithm: str, durations, locations, capacities, start_times,
               objective: str = "sum", time_limit: float | None = None, device: int = 0,
               with_unvisited: bool = False, **knobs) -> dict:
     """Result dict of the VRP TODO slot (api/vrp/ga/index.py:48-53); A7 shapes."""
+    rem = _remote()
+    if rem is not None:
+        out = rem.solve_vrp(algorithm, durations, locations, capacities, start_times,
+                            ignored_customers, completed_customers, **knobs)
+        if with_unvisited:   # the served customers' complement (the remote answers the slot dict)
+            served = {c for v in out["vehicles"] for c in v["tour"][1:-1]}
+            nodes = [0] + active_customers(list(locations or []), ignored_customers,
+                                           completed_customers)
+            out["unvisited"] = [c for c in nodes[1:] if c not in served]
+        return out
     ci = compact_vrp(durations, locations, capacities, start_times, ignored_customers,
                      completed_customers)
     ctx = context(device)
