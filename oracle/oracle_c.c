@@ -769,9 +769,6 @@ typedef struct {
   int64_t rsum, rmax;
   int rcnt;
   int64_t* out; /* route durations (table build) or NULL */
-  int nocut;    /* price every route as one (over / lbcut below) */
-  int over;     /* (nocut) a route exceeds the capacity */
-  int64_t ncus, lbcut; /* customers in the open route; sum of (customers - 1) of over routes */
 } sacc_t;
 
 static inline int64_t d0(const inst_t* I, int a, int b) {
@@ -785,12 +782,7 @@ static inline void s_close(const inst_t* I, sacc_t* a) {
   a->rsum += d;
   if (d > a->rmax) a->rmax = d;
   ++a->rcnt;
-  if (a->load > I->cap[0]) {
-    a->over = 1;
-    a->lbcut += a->ncus - 1;
-  }
   a->dur = a->load = 0;
-  a->ncus = 0;
   a->prev = 0;
 }
 
@@ -801,10 +793,9 @@ static void s_run(const inst_t* I, const seg_t* C, const uint16_t* A, int a, int
   const int64_t *PE = C->PE, *PD = C->PD, cap = I->cap[0];
   while (a <= b) {
     const int64_t room = cap - c->load;
-    if (c->nocut || PD[b + 1] - PD[a] <= room) {
+    if (PD[b + 1] - PD[a] <= room) {
       c->dur += d0(I, c->prev, rev ? A[b] : A[a]) + PE[b + 1] - PE[a + 1];
       c->load += PD[b + 1] - PD[a];
-      c->ncus += b - a + 1;
       c->prev = rev ? A[a] : A[b];
       return;
     }
@@ -817,7 +808,6 @@ static void s_run(const inst_t* I, const seg_t* C, const uint16_t* A, int a, int
       if (lo >= a) {
         c->dur += d0(I, c->prev, A[a]) + PE[lo + 1] - PE[a + 1];
         c->load += PD[lo + 1] - PD[a];
-        c->ncus += lo - a + 1;
         c->prev = A[lo];
       }
       s_close(I, c);
@@ -831,7 +821,6 @@ static void s_run(const inst_t* I, const seg_t* C, const uint16_t* A, int a, int
       if (lo <= b) {
         c->dur += d0(I, c->prev, A[b]) + PE[b + 1] - PE[lo + 1];
         c->load += PD[b + 1] - PD[lo];
-        c->ncus += b - lo + 1;
         c->prev = A[lo];
       }
       s_close(I, c);
@@ -859,7 +848,7 @@ static void seg_build(const inst_t* I, const uint16_t* A, int n, seg_t* C) {
   C->S = S;
   C->NC[n] = n;
   for (int q = n - 1; q >= 0; --q) C->NC[q] = A[q] ? q : C->NC[q + 1];
-  sacc_t c = {0, 0, 0, 0, 0, 0, C->dur, 0, 0, 0, 0};
+  sacc_t c = {0, 0, 0, 0, 0, 0, C->dur};
   for (int g = 0; g <= S; ++g) {
     C->RB[g] = c.rcnt;
     s_run(I, C, A, sspx(C, g - 1) + 1, sspx(C, g) - 1, 0, &c);
@@ -954,19 +943,15 @@ static void g_piece(const inst_t* I, const seg_t* C, const uint16_t* A, int a, i
 }
 
 /* Key of A moved by m (route_model.price_seg); *unserved = 1 (key 0) when
- * the moved tour leaves a customer unvisited.  nocut (the device's first
- * pass): every changed route priced as one route; when one exceeds the
- * capacity *over = 1 and the key is a lower bound on the durationSum
- * instead (a cut a -> depot -> b is shorter than a -> b by at most dx). */
+ * the moved tour leaves a customer unvisited. */
 static uint64_t seg_key(const inst_t* I, const uint16_t* A, const seg_t* C, const move_t* m,
-                        int* unserved, int nocut, int64_t dx, int* over) {
+                        int* unserved) {
   const int n = C->n, i = m->i, j = m->j;
   const int lo = i < j ? i : j, hi = i < j ? j : i;
   const int* SC = C->SC;
   const int s0 = SC[lo], st = sspx(C, s0 - 1) + 1, en = sspx(C, SC[hi + 1]);
   sreg_t g;
   memset(&g, 0, sizeof(g));
-  g.c.nocut = nocut;
   g_run(I, C, A, st, lo - 1, 0, &g);
   if (m->typ == 1) {
     g_piece(I, C, A, i, j, 1, &g);
@@ -989,13 +974,6 @@ static uint64_t seg_key(const inst_t* I, const uint16_t* A, const seg_t* C, cons
   }
   const int glast = en < n ? SC[en] : C->S;
   const int ra = C->RB[s0], rz = C->RB[glast + 1];
-  *over = g.c.over;
-  *unserved = 0;
-  if (g.c.over) {
-    const int64_t ds = C->dsp[ra] + g.c.rsum + g.isum + C->dsp[C->R] - C->dsp[rz];
-    const int64_t lb = ds - g.c.lbcut * dx;
-    return (uint64_t)(lb > 0 ? lb : 0);
-  }
   const int R = C->R - (rz - ra) + g.c.rcnt + g.icnt;
   int Tb = C->T;
   if (!(en < n && C->PC[n - 1] > en) && g.cust) Tb = g.seps + (en < n ? n - 1 - en : 0);
@@ -1031,12 +1009,6 @@ int oracle_sa_run_resync(int problem, const int32_t* D, int H, int N, const int3
   for (int c = 1; sym && c < N; ++c) sym = dem[c] <= cap[0];
   int clevels = 1;
   while ((1 << clevels) <= n + 2) ++clevels;
-  int64_t dx = 0; /* depot-detour excess: max(0, D(a,b) - D(a,0) - D(0,b)) */
-  for (int a = 1; sym && a < N; ++a)
-    for (int b = 1; b < N; ++b) {
-      const int64_t e = (int64_t)D[(int64_t)a * N + b] - D[(int64_t)a * N] - D[b];
-      if (e > dx) dx = e;
-    }
 #ifdef _OPENMP
   if (threads > 0) omp_set_num_threads(threads);
 #pragma omp parallel
@@ -1090,17 +1062,14 @@ int oracle_sa_run_resync(int problem, const int32_t* D, int H, int N, const int3
         move_t mbest = {0, 0, 0};
         uint32_t wbest = 0;
         const int hopeless = (ck >> 56) == 0 && accept_threshold(1u << 28, invT) == 0;
-        /* (the device prices without capacity cuts first and re-prices only the
-         * overflowing moves whose bound can still win, seg_key's nocut mode; on
-         * the host one exact pass is faster, with the same keys) */
         for (int lane = 0; lane < moves; ++lane) {
           u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)c, (uint32_t)lane,
                            k0, k1);
           move_t m = decode_move_window(r.x, r.y, r.z, n, window, window_types);
           uint64_t kk;
           if (sym) {
-            int unserved = 0, over = 0;
-            kk = seg_key(&I, A, &C, &m, &unserved, 0, dx, &over);
+            int unserved = 0;
+            kk = seg_key(&I, A, &C, &m, &unserved);
             if (unserved) kk = hopeless ? ~0ull : tour_key(&I, A, n, &m);
           } else {
             kk = S.alive ? resync_key(&I, A, n, &m, &S, hopeless) : tour_key(&I, A, n, &m);

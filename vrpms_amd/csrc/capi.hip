@@ -28,31 +28,21 @@ int hip_fail(hipError_t e, const char* what) {
 
 // stats layout: 0 min_dur 1 max_dur 2 min_dem 3 max_dem 4 min_cap 5 max_cap
 //               6 min_start 7 max_start 8 asymmetric (slice 0)
-//               9 depot-detour excess (slice 0)
 __global__ void stats_init_kernel(int32_t* s) {
   if (threadIdx.x < 8) s[threadIdx.x] = (threadIdx.x & 1) ? INT_MIN : INT_MAX;
-  if (threadIdx.x == 8 || threadIdx.x == 9) s[threadIdx.x] = 0;
+  if (threadIdx.x == 8) s[8] = 0;
 }
 
-// s[8] |= any D[a][b] != D[b][a] in hour slice 0 (selects the O(1) 2-opt
-// delta); s[9] = max(0, D[a][b] - D[a][0] - D[0][b]) over customers a, b: how
-// much a route can shorten by returning to the depot between a and b (0 under
-// the triangle inequality; the segment SA's lower bound on a capacity cut).
+// s[8] |= any D[a][b] != D[b][a] in hour slice 0 (selects the O(1) 2-opt delta).
 __global__ void asym_kernel(const int32_t* __restrict__ D, int N, int32_t* s) {
   const int64_t total = (int64_t)N * N;
   int asym = 0;
-  int64_t ex = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t a = i / N, b = i - a * N;
     asym |= D[i] != D[b * N + a];
-    if (a > 0 && b > 0) ex = max(ex, (int64_t)D[i] - D[a * N] - D[b]);
   }
   if (__any(asym) && (threadIdx.x & 63) == 0) atomicOr(s + 8, 1);
-  int e = (int)min(ex, (int64_t)INT_MAX);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) e = max(e, __shfl_xor(e, off, kWave));
-  if ((threadIdx.x & 63) == 0 && e > 0) atomicMax(s + 9, e);
 }
 
 __device__ __forceinline__ void block_minmax_commit(int vmin, int vmax, int32_t* smin,
@@ -336,7 +326,7 @@ int vrpms_set_instance(vrpms_ctx* ctx, int32_t problem, const int32_t* d_dur, in
   VRPMS_HIP(hipGetLastError());
   asym_kernel<<<grid, 256, 0, s>>>(in.mat32, N, ctx->d_stats);
   VRPMS_HIP(hipGetLastError());
-  int32_t st[10];
+  int32_t st[9];
   std::vector<int32_t> caps(K);
   VRPMS_HIP(hipMemcpyAsync(st, ctx->d_stats, sizeof(st), hipMemcpyDeviceToHost, s));
   VRPMS_HIP(hipMemcpyAsync(caps.data(), in.cap, (size_t)K * 4, hipMemcpyDeviceToHost, s));
@@ -354,7 +344,6 @@ int vrpms_set_instance(vrpms_ctx* ctx, int32_t problem, const int32_t* d_dur, in
   in.max_start = st[7];
   in.min_start = st[6];
   in.symmetric = st[8] == 0;
-  in.depot_excess = st[9];
   in.cap0 = caps[0];
   in.uniform_cap = std::all_of(caps.begin(), caps.end(), [&](int32_t c) { return c == caps[0]; });
   const long double bound = (long double)in.max_start + (long double)(N + K + 1) * in.max_dur;

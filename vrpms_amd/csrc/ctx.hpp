@@ -21,7 +21,6 @@ struct Instance {
   int max_dur = 0, max_dem = 0, max_start = 0, min_start = 0, min_cap = 0, max_cap = 0;
   bool uniform_cap = true;
   bool symmetric = false;      // hour slice 0 is symmetric (O(1) 2-opt delta for static TSP)
-  int depot_excess = 0;        // max(0, D(a,b) - D(a,0) - D(0,b)) over customers, slice 0
   int cap0 = 0;
   // device copies owned by the context
   int32_t* mat32 = nullptr;    // [H][N][N]

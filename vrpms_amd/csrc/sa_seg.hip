@@ -58,16 +58,13 @@ struct SegArgs {
   int segs;     // separator slots per chain
   int rm, lv;   // route slots, sparse-table levels
   uint32_t chain_bytes;
-  uint32_t dx;  // depot-detour excess max(0, D(a,b) - D(a,0) - D(0,b)) (the bound's slack per cut)
 };
 
 // per-chain LDS: u32 [PE n+2 | PD n+2 | dur rm+1 | dsp, pmx, smx rm+1 each |
-// sparse (lv-1) x rm | lbv 64 x kSegMaxMoves], then u16 [tok n+2 | SC n+2 |
-// SP, RB, FNE, LNE1 segs+2]
+// sparse (lv-1) x rm], then u16 [tok n+2 | SC n+2 | SP, RB, FNE, LNE1 segs+2]
 __host__ __device__ inline uint32_t seg_chain_bytes(int n, int segs, int rm, int lv) {
   const uint32_t np2 = ((uint32_t)n + 2u + 1u) & ~1u;
-  const uint32_t u32s = 2u * np2 + 4u * (uint32_t)(rm + 1) + (uint32_t)(lv - 1) * (uint32_t)rm +
-                        64u * (uint32_t)kSegMaxMoves;
+  const uint32_t u32s = 2u * np2 + 4u * (uint32_t)(rm + 1) + (uint32_t)(lv - 1) * (uint32_t)rm;
   const uint32_t u16s = 2u * np2 + 4u * (uint32_t)(segs + 2);
   return (4u * u32s + 2u * u16s + 15u) & ~15u;
 }
@@ -124,7 +121,7 @@ VRPMS_DEV uint32_t dpp_rscan_max(uint32_t v, uint32_t& total) {
 }
 
 struct SegTabs {
-  uint32_t *PE, *PD, *dur, *dsp, *pmx, *smx, *sp, *lbv;
+  uint32_t *PE, *PD, *dur, *dsp, *pmx, *smx, *sp;
   uint16_t *tok, *SC, *SP, *RB, *FNE, *LNE1;
 };
 
@@ -168,8 +165,7 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
     T.pmx = T.dsp + (RM + 1);
     T.smx = T.pmx + (RM + 1);
     T.sp = T.smx + (RM + 1);
-    T.lbv = T.sp + (LV - 1) * RM;
-    uint16_t* h = reinterpret_cast<uint16_t*>(T.lbv + 64 * kSegMaxMoves);
+    uint16_t* h = reinterpret_cast<uint16_t*>(T.sp + (LV - 1) * RM);
     T.tok = h;
     T.SC = h + np2;
     T.SP = T.SC + np2;
@@ -404,13 +400,8 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
     uint32_t bidx = 0xffffffffu, bw = 0;
     Move bmv{0, 0, 0};
     uint32_t bj0 = 0, bj1 = 0, bj2 = 0, bj3 = 0;
-    // Price this lane's move mi (index lane + 64 mi).  cuts = false prices
-    // every changed route as one route: exact when none exceeds the
-    // capacity; else `over` is set and `lbp` bounds the durationSum from
-    // below (a capacity cut turns an edge a -> b into a -> depot -> b, which
-    // is shorter by at most the instance's depot-detour excess dx).  cuts =
-    // true applies the greedy split's cuts (binary-searched on PD): exact.
-    auto price = [&](int mi, bool cuts, bool& over, uint32_t& lbp) __attribute__((always_inline)) {
+#pragma unroll 1
+    for (int mi = 0; mi < a.M; ++mi) {
       const uint32_t idx = (uint32_t)(lane + 64 * mi);
       const u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)chain, idx,
                              a.seed_lo, a.seed_hi);
@@ -426,11 +417,9 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
       const uint32_t jx0 = d0(b0, b1), jx1 = d0(b1, b2), jx2 = d0(b3, b4), jx3 = d0(b4, b5);
       uint64_t k = ~0ull;
       bool full = !seg_ok;
-      over = false;
-      lbp = 0xffffffffu;
       if (seg_ok) {
         // the open route and what the walk has closed
-        uint32_t c_dur = 0, c_load = 0, c_prev = 0, c_sum = 0, c_max = 0, c_ncus = 0, lbcut = 0;
+        uint32_t c_dur = 0, c_load = 0, c_prev = 0, c_sum = 0, c_max = 0;
         int c_cnt = 0;
         uint32_t isum = 0, imax = 0;
         int icnt = 0, seps = 0;
@@ -440,27 +429,19 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
           c_sum += d;
           c_max = max(c_max, d);
           ++c_cnt;
-          if (c_load > cap) {  // (cuts = false only) the greedy split cuts this route
-            over = true;
-            lbcut += c_ncus - 1u;
-          }
-          c_dur = c_load = c_prev = c_ncus = 0u;
+          c_dur = c_load = c_prev = 0u;
         };
         // customers A[x..y] joined to the open route in the moved order (rev:
-        // A[y] first), with cuts where the greedy split's next customer does
-        // not fit; jv = the junction edge into the first one when the open
-        // route holds a customer
+        // A[y] first), cut where the greedy split's next customer does not
+        // fit; jv = the junction edge into the first one when the open route
+        // holds a customer
         auto run = [&](int x, int y, bool rev, uint32_t jv) __attribute__((always_inline)) {
           if (x > y) return;
           seps = 0;
           cust = true;
           while (true) {
             const uint32_t room = cap - c_load;
-#ifdef VRPMS_SEG_NOCUT
-            const bool fits = true || room;  // A/B only: wrong keys, the price of capacity cuts
-#else
-            const bool fits = !cuts || T.PD[y + 1] - T.PD[x] <= room;
-#endif
+            const bool fits = T.PD[y + 1] - T.PD[x] <= room;
             int pa = x, pb = y;
             if (!fits) {
               // first q in [x - 1, y + 1] with PD[q + 1] > thr, on the monotone PD
@@ -477,7 +458,6 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
               c_dur += (c_prev ? jv : leg[F]) + T.PE[pb + 1] - T.PE[pa + 1];
               c_load += T.PD[pb + 1] - T.PD[pa];
               c_prev = rev ? T.tok[pa] : T.tok[pb];
-              c_ncus += (uint32_t)(pb - pa + 1);
             }
             if (fits) break;
             close();
@@ -565,22 +545,18 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
         if (en >= n) close();  // the tour's end closes the last route
         const int glast = en < n ? (int)T.SC[en] : S;
         const int ra = T.RB[s0], rz = T.RB[glast + 1];
-        const uint32_t dsum = T.dsp[ra] + c_sum + isum + T.dsp[R] - T.dsp[rz];
-        if (over) {
-          lbp = dsum - (uint32_t)min((uint64_t)dsum, (uint64_t)lbcut * a.dx);
+        const int Rb = R - (rz - ra) + c_cnt + icnt;
+        int Tb = Tt;
+        const bool tail_kept = en < n && (int)T.LNE1[S] - 1 > glast;
+        if (!tail_kept && cust) Tb = seps + (en < n ? n - 1 - en : 0);
+        if (Rb - Tb <= K) {
+          const uint32_t dsum = T.dsp[ra] + c_sum + isum + T.dsp[R] - T.dsp[rz];
+          const uint32_t dmax = max(max(T.pmx[ra], T.smx[rz]), max(imax, c_max));
+          k = cvrp_key(0, dsum, dmax, I.sp.objective);
+        } else if (shortcut) {
+          k = ~0ull;
         } else {
-          const int Rb = R - (rz - ra) + c_cnt + icnt;
-          int Tb = Tt;
-          const bool tail_kept = en < n && (int)T.LNE1[S] - 1 > glast;
-          if (!tail_kept && cust) Tb = seps + (en < n ? n - 1 - en : 0);
-          if (Rb - Tb <= K) {
-            const uint32_t dmax = max(max(T.pmx[ra], T.smx[rz]), max(imax, c_max));
-            k = cvrp_key(0, dsum, dmax, I.sp.objective);
-          } else if (shortcut) {
-            k = ~0ull;
-          } else {
-            full = true;
-          }
+          full = true;
         }
       }
       if (full) {
@@ -590,7 +566,7 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
         ++nfull;
 #endif
       }
-      if (!over && (k < bkey || (k == bkey && idx < bidx))) {  // (key, index) order
+      if (k < bkey) {  // ties keep the earlier (smaller) move index
         bkey = k;
         bidx = idx;
         bw = r.w;
@@ -599,33 +575,6 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
         bj1 = jx1;
         bj2 = jx2;
         bj3 = jx3;
-      }
-    };
-    // (1) every move without capacity cuts; an overflowing one leaves its bound
-#pragma unroll 1
-    for (int mi = 0; mi < a.M; ++mi) {
-      bool over;
-      uint32_t lbp;
-      price(mi, false, over, lbp);
-      T.lbv[64 * mi + lane] = over ? lbp : 0xffffffffu;
-    }
-    // (2) the overflowing moves that can still win priced with their cuts:
-    // a bound above the best exact durationSum cannot (objective "sum",
-    // best served and unclamped); otherwise every overflowing move is
-    {
-      const uint64_t kstar = wave_min_u64(bkey);
-      const uint32_t pk = (uint32_t)(kstar >> 28) & kKeyClamp;
-      const uint32_t thr = I.sp.objective == VRPMS_OBJ_SUM && (kstar >> 56) == 0 && pk < kKeyClamp
-                               ? pk : 0xfffffffeu;
-#pragma unroll 1
-      for (int mi = 0; mi < a.M; ++mi) {
-        const bool need = T.lbv[64 * mi + lane] <= thr;
-        if (__ballot(need) == 0) continue;
-        if (need) {
-          bool over;
-          uint32_t lbp;
-          price(mi, true, over, lbp);
-        }
       }
     }
     // the chain's (key, move index) minimum
@@ -736,7 +685,7 @@ int launch_sa_seg(const vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* d_cu
   if (lds > ctx->max_lds) return 1;
   SegArgs a{si, p->chains, n, p->steps, p->window, wtypes, p->inv_t0, p->inv_alpha,
             (uint32_t)p->seed, (uint32_t)(p->seed >> 32), p->step0, d_cur, d_cur_key, d_best,
-            d_best_key, moves / 64, cpw, segs, rm, lv, cb, (uint32_t)in.depot_excess};
+            d_best_key, moves / 64, cpw, segs, rm, lv, cb};
   auto go = [&](auto kern) {
     if (lds > 65536)
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
