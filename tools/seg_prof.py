@@ -2,7 +2,7 @@
 """Where sa_seg_kernel's time goes (built with -DVRPMS_SEG_PROF into
 build_ab/segprof/libvrpms.so): per SA step the pricing and accept (table
 rebuild) time (wall_clock64 ticks of lane 0, 100 MHz), the accept rate and
-the lanes re-evaluated in full -- on X-1000 first-fit start tours at a hot
+the cross-wavefront exchange (W > 1, VRPMS_SEG_WAVES) -- on X-1000 first-fit start tours at a hot
 and a cold fixed temperature.
 
 usage: tools/seg_prof.py build   (CPU: compile the variant)
@@ -59,7 +59,7 @@ def run(chains, moves):
         print(f"{tag}: {steps / dt:,.0f} steps/s/chain | per step: pricing {a[0] / st * 10:.0f} ns, "
               f"rebuild {a[1] / max(a[7], 1) * 10:.0f} ns x {a[7] / st:.3f}/step, "
               f"accept rate {a[3] / st:.3f}, "
-              f"full-eval lanes/step {a[4] / st:.3f}, setup {a[5] / chains * 10 / 1e3:.1f} us, "
+              f"exchange {a[4] / st * 10:.0f} ns, setup {a[5] / chains * 10 / 1e3:.1f} us, "
               f"kernel {a[6] / chains * 10 / 1e3:.1f} us/chain | best "
               f"{r.best()[0] >> 28 & (2**28 - 1)}", flush=True)
 

@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.hpp"
 #include "ctx.hpp"
@@ -58,7 +59,21 @@ struct SegArgs {
   int segs;     // separator slots per chain
   int rm, lv;   // route slots, sparse-table levels
   uint32_t chain_bytes;
+  int W;        // wavefronts per chain (W > 1: one chain per workgroup, cpw = 1)
 };
+
+// The cross-wavefront exchange of a multi-wavefront chain: each wavefront's
+// best (key, move index) with what applying it needs, two buffers by step
+// parity, then the table scalars wavefront 0 publishes after a rebuild.
+struct SegXSlot {
+  uint64_t key;
+  uint32_t idx, w, typ;
+  int32_t i, j;
+  uint32_t jx[4];
+  uint32_t pad;
+};
+constexpr int kSegMaxWaves = 4;
+constexpr uint32_t kSegXBytes = 2 * kSegMaxWaves * sizeof(SegXSlot) + 32;
 
 // per-chain LDS: u32 [PE n+2 | PD n+2 | dur rm+1 | dsp, pmx, smx rm+1 each |
 // sparse (lv-1) x rm], then u16 [tok n+2 | SC n+2 | SP, RB, FNE, LNE1 segs+2]
@@ -66,7 +81,7 @@ __host__ __device__ inline uint32_t seg_chain_bytes(int n, int segs, int rm, int
   const uint32_t np2 = ((uint32_t)n + 2u + 1u) & ~1u;
   const uint32_t u32s = 2u * np2 + 4u * (uint32_t)(rm + 1) + (uint32_t)(lv - 1) * (uint32_t)rm;
   const uint32_t u16s = 2u * np2 + 4u * (uint32_t)(segs + 2);
-  return (4u * u32s + 2u * u16s + 15u) & ~15u;
+  return ((4u * u32s + 2u * u16s + 15u) & ~15u) + kSegXBytes;
 }
 
 __host__ __device__ inline int seg_levels(int rm) {
@@ -127,13 +142,13 @@ struct SegTabs {
 
 #ifdef VRPMS_SEG_PROF
 // per-chain counters (A/B builds only: tools/seg_prof.py): pricing ticks,
-// rebuild ticks, steps, accepts, lanes re-evaluated in full, setup ticks,
+// rebuild ticks, steps, accepts, cross-wavefront exchange ticks, setup ticks,
 // kernel ticks, rebuilds (wall_clock64, 100 MHz)
 __device__ unsigned long long g_seg_prof[8 * 8192];
 #endif
 
 template <typename MatT>
-__global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
+__global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 #ifdef VRPMS_SEG_PROF
   const unsigned long long pk0 = wall_clock64();
@@ -147,8 +162,15 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
   for (uint32_t c = threadIdx.x; c < N; c += blockDim.x) leg[c] = (uint32_t)M0[c];
   __syncthreads();
   const int wave = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
-  const int chain = (int)blockIdx.x * a.cpw + wave;
-  if (chain >= a.chains) return;  // no block-wide barrier after this point
+  // W = 1: cpw chains per workgroup, one wavefront each.  W > 1: one chain
+  // per workgroup; its W wavefronts price 64 W M moves per step (move index
+  // lane + 64 (cw + W mi)), the (key, index) minimum meets in LDS, and
+  // wavefront 0 applies an accepted move and rebuilds the tables.
+  const int W = a.W;
+  const int cw = W > 1 ? wave : 0;
+  const int slot = W > 1 ? 0 : wave;
+  const int chain = W > 1 ? (int)blockIdx.x : (int)blockIdx.x * a.cpw + wave;
+  if (chain >= a.chains) return;  // (W = 1) no block-wide barrier after this point
   const int n = a.n, K = a.si.K, RM = a.rm, LV = a.lv, SEGS = a.segs;
   const uint32_t cap = (uint32_t)I.sp.cap[0];
   const int32_t* dem = I.sp.dem;
@@ -157,7 +179,7 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
   {
     const uint32_t np2 = ((uint32_t)n + 2u + 1u) & ~1u;
     uint32_t* u = reinterpret_cast<uint32_t*>(smem + inst_lds_bytes(a.si) + ((N * 4u + 15u) & ~15u) +
-                                              (uint32_t)wave * a.chain_bytes);
+                                              (uint32_t)slot * a.chain_bytes);
     T.PE = u;
     T.PD = u + np2;
     T.dur = u + 2 * np2;
@@ -173,6 +195,10 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
     T.FNE = T.RB + (SEGS + 2);
     T.LNE1 = T.FNE + (SEGS + 2);
   }
+  SegXSlot* xs = reinterpret_cast<SegXSlot*>(smem + inst_lds_bytes(a.si) + ((N * 4u + 15u) & ~15u) +
+                                             (uint32_t)slot * a.chain_bytes + a.chain_bytes -
+                                             kSegXBytes);
+  int32_t* xr = reinterpret_cast<int32_t*>(xs + 2 * kSegMaxWaves);  // S, R, Tt, seg_ok, ck lo/hi
   auto d0 = [&](uint32_t x, uint32_t y) __attribute__((always_inline)) -> uint32_t {
     if ((x | y) == 0u) return 0u;  // two depots: an empty route lasts 0
     if (x == 0u) return leg[y];
@@ -345,7 +371,7 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
   };
 
   // ---- the current tour: tokens and edges into LDS ----------------------------
-  {
+  if (cw == 0) {
     const uint16_t* gcur = a.cur + (int64_t)chain * n;
     for (int q = lane; q <= n; q += 64) {
       const uint32_t c = q < n ? min((uint32_t)gcur[q], Nm1) : 0u;
@@ -368,29 +394,45 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
 #ifdef VRPMS_SEG_PROF
       const unsigned long long pb0 = wall_clock64();
 #endif
-      rebuild();
+      if (cw == 0) {
+        rebuild();
+        if (first) {  // the start tour's key: from the tables when it serves everyone
+          if (seg_ok && R - Tt <= K) ck = cvrp_key(0, T.dsp[R], T.smx[0], I.sp.objective);
+          else ck = eval_tour<true>(I.D, I.sp, tourA, n).key;
+        }
+        if (W > 1 && lane == 0) {
+          xr[0] = S;
+          xr[1] = R;
+          xr[2] = Tt;
+          xr[3] = seg_ok ? 1 : 0;
+          xr[4] = (int32_t)(uint32_t)ck;
+          xr[5] = (int32_t)(uint32_t)(ck >> 32);
+        }
+      }
+      if (W > 1) {  // wavefront 0's tables and scalars
+        __syncthreads();
+        S = xr[0];
+        R = xr[1];
+        Tt = xr[2];
+        seg_ok = xr[3] != 0;
+        ck = ((uint64_t)(uint32_t)xr[5] << 32) | (uint32_t)xr[4];
+      }
+      first = false;
       need_build = false;
 #ifdef VRPMS_SEG_PROF
       pf[1] += wall_clock64() - pb0;
       pf[7] += 1;
+      if (st == 0) pf[5] = wall_clock64() - pk0;
 #endif
-      if (first) {  // the start tour's key: from the tables when it serves everyone
-        first = false;
-        if (seg_ok && R - Tt <= K) ck = cvrp_key(0, T.dsp[R], T.smx[0], I.sp.objective);
-        else ck = eval_tour<true>(I.D, I.sp, tourA, n).key;
-#ifdef VRPMS_SEG_PROF
-        pf[5] = wall_clock64() - pk0;
-#endif
-      }
       if (ck < bk) {
         bk = ck;
-        for (int q = lane; q < n; q += 64) gbest[q] = T.tok[q];
+        if (cw == 0)
+          for (int q = lane; q < n; q += 64) gbest[q] = T.tok[q];
       }
     }
     if (st >= a.steps || n < 2) break;
 #ifdef VRPMS_SEG_PROF
     const unsigned long long pt0 = wall_clock64();
-    int nfull = 0;
 #endif
     const uint64_t step = a.step0 + (uint64_t)st;
     // an unserved customer cannot be accepted from a tour serving everyone
@@ -402,7 +444,7 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
     uint32_t bj0 = 0, bj1 = 0, bj2 = 0, bj3 = 0;
 #pragma unroll 1
     for (int mi = 0; mi < a.M; ++mi) {
-      const uint32_t idx = (uint32_t)(lane + 64 * mi);
+      const uint32_t idx = (uint32_t)(lane + 64 * (cw + W * mi));
       const u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)chain, idx,
                              a.seed_lo, a.seed_hi);
       const Move m = decode_move_window(r.x, r.y, r.z, n, a.window, a.window_types);
@@ -562,9 +604,6 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
       if (full) {
         auto moved = [&](int q) { return tourA(map_src(mmap, q)); };
         k = eval_tour<true>(I.D, I.sp, moved, n).key;
-#ifdef VRPMS_SEG_PROF
-        ++nfull;
-#endif
       }
       if (k < bkey) {  // ties keep the earlier (smaller) move index
         bkey = k;
@@ -577,12 +616,42 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
         bj3 = jx3;
       }
     }
-    // the chain's (key, move index) minimum
+    // the chain's (key, move index) minimum: over the lanes, then (W > 1)
+    // over the wavefronts through LDS
     int wl;
-    const uint64_t k = wave_argmin_lane(bkey, wl);
+    uint64_t k = wave_argmin_lane(bkey, wl);
     const uint32_t imin = wave_min_u32_uniform(bkey == k ? bidx : 0xffffffffu);
     const int bl = (int)(imin & 63u);
-    const uint32_t uw = (uint32_t)wave_bcast((int)bw, bl);
+    uint32_t uw = (uint32_t)wave_bcast((int)bw, bl);
+    Move mb;
+    mb.typ = (uint32_t)wave_bcast((int)bmv.typ, bl);
+    mb.i = wave_bcast(bmv.i, bl);
+    mb.j = wave_bcast(bmv.j, bl);
+    uint32_t w0 = (uint32_t)wave_bcast((int)bj0, bl), w1 = (uint32_t)wave_bcast((int)bj1, bl);
+    uint32_t w2 = (uint32_t)wave_bcast((int)bj2, bl), w3 = (uint32_t)wave_bcast((int)bj3, bl);
+#ifdef VRPMS_SEG_PROF
+    const unsigned long long px0 = wall_clock64();
+    pf[0] += px0 - pt0;
+#endif
+    if (W > 1) {
+      SegXSlot* xb = xs + (st & 1) * kSegMaxWaves;
+      if (lane == 0) xb[cw] = SegXSlot{k, imin, uw, mb.typ, mb.i, mb.j, {w0, w1, w2, w3}, 0u};
+      __syncthreads();
+      SegXSlot b = xb[0];
+      for (int v = 1; v < W; ++v) {
+        const SegXSlot o = xb[v];
+        if (o.key < b.key || (o.key == b.key && o.idx < b.idx)) b = o;
+      }
+      k = b.key;
+      uw = b.w;
+      mb.typ = b.typ;
+      mb.i = b.i;
+      mb.j = b.j;
+      w0 = b.jx[0];
+      w1 = b.jx[1];
+      w2 = b.jx[2];
+      w3 = b.jx[3];
+    }
     bool accept = k <= ck;
     if (!accept) {
       const uint64_t d = (k >> 28) - (ck >> 28);
@@ -590,16 +659,11 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
       accept = (uw >> 8) < accept_threshold(dp, invT);
     }
 #ifdef VRPMS_SEG_PROF
-    pf[0] += wall_clock64() - pt0;
+    pf[4] += wall_clock64() - px0;
     pf[2] += 1;
     pf[3] += accept ? 1 : 0;
-    pf[4] += (unsigned long long)__popcll(__ballot(nfull > 0));
 #endif
     if (accept) {
-      Move mb;
-      mb.typ = (uint32_t)wave_bcast((int)bmv.typ, bl);
-      mb.i = wave_bcast(bmv.i, bl);
-      mb.j = wave_bcast(bmv.j, bl);
       const int blo = min(mb.i, mb.j), bhi = max(mb.i, mb.j);
       // a move among separators only (e.g. two separators swapped) leaves the
       // tour as it is: no rebuild
@@ -607,45 +671,48 @@ __global__ __launch_bounds__(256) void sa_seg_kernel(SegArgs a) {
                         (mb.typ != kMoveSwap && T.SC[bhi + 1] - T.SC[blo] == bhi - blo + 1);
       ck = k;
       if (!same) {
-        const MoveMap mmb = move_map(mb);
-        const uint32_t w0 = (uint32_t)wave_bcast((int)bj0, bl), w1 = (uint32_t)wave_bcast((int)bj1, bl);
-        const uint32_t w2 = (uint32_t)wave_bcast((int)bj2, bl), w3 = (uint32_t)wave_bcast((int)bj3, bl);
-        // the new tour's tokens and edges: a kept adjacency's edge is a
-        // difference of PE (forward, or reversed on the symmetric matrix; PE
-        // is complete even when the segment tables are not), the four
-        // junctions are the winner's gathers
-        uint32_t v_tok[kSegRegs], v_e[kSegRegs];
+        if (W > 1) __syncthreads();  // every wavefront is done reading the tables
+        if (cw == 0) {
+          const MoveMap mmb = move_map(mb);
+          // the new tour's tokens and edges: a kept adjacency's edge is a
+          // difference of PE (forward, or reversed on the symmetric matrix; PE
+          // is complete even when the segment tables are not), the four
+          // junctions are the winner's gathers
+          uint32_t v_tok[kSegRegs], v_e[kSegRegs];
 #pragma unroll
-        for (int i = 0; i < kSegRegs; ++i) {
-          const int q = lane + 64 * i;
-          v_tok[i] = 0u;
-          v_e[i] = 0u;
-          if (q > n) continue;
-          const int sq = map_src(mmb, q), sp = map_src(mmb, q - 1);
-          if (q < n) v_tok[i] = T.tok[sq];
-          if (q == blo) v_e[i] = w0;
-          else if (q == blo + 1) v_e[i] = w1;
-          else if (q == bhi) v_e[i] = w2;
-          else if (q == bhi + 1) v_e[i] = w3;
-          else if (sp + 1 == sq) v_e[i] = T.PE[sq + 1] - T.PE[sq];
-          else v_e[i] = T.PE[sp + 1] - T.PE[sp];  // reversed: the edge between A[sq] and A[sp]
-        }
-        wave_sync();
+          for (int i = 0; i < kSegRegs; ++i) {
+            const int q = lane + 64 * i;
+            v_tok[i] = 0u;
+            v_e[i] = 0u;
+            if (q > n) continue;
+            const int sq = map_src(mmb, q), sp = map_src(mmb, q - 1);
+            if (q < n) v_tok[i] = T.tok[sq];
+            if (q == blo) v_e[i] = w0;
+            else if (q == blo + 1) v_e[i] = w1;
+            else if (q == bhi) v_e[i] = w2;
+            else if (q == bhi + 1) v_e[i] = w3;
+            else if (sp + 1 == sq) v_e[i] = T.PE[sq + 1] - T.PE[sq];
+            else v_e[i] = T.PE[sp + 1] - T.PE[sp];  // reversed: the edge between A[sq] and A[sp]
+          }
+          wave_sync();
 #pragma unroll
-        for (int i = 0; i < kSegRegs; ++i) {
-          const int q = lane + 64 * i;
-          if (q > n) continue;
-          if (q < n) T.tok[q] = (uint16_t)v_tok[i];
-          T.PE[q + 1] = v_e[i];
+          for (int i = 0; i < kSegRegs; ++i) {
+            const int q = lane + 64 * i;
+            if (q > n) continue;
+            if (q < n) T.tok[q] = (uint16_t)v_tok[i];
+            T.PE[q + 1] = v_e[i];
+          }
         }
         need_build = true;
       } else if (ck < bk) {
         bk = ck;
-        for (int q = lane; q < n; q += 64) gbest[q] = T.tok[q];
+        if (cw == 0)
+          for (int q = lane; q < n; q += 64) gbest[q] = T.tok[q];
       }
     }
     invT = invT * a.inv_alpha;
   }
+  if (cw != 0) return;
   uint16_t* gout = a.cur + (int64_t)chain * n;
   for (int q = lane; q < n; q += 64) gout[q] = T.tok[q];
   if (lane == 0) {
@@ -677,20 +744,28 @@ int launch_sa_seg(const vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* d_cu
   const int lv = seg_levels(rm);
   const uint32_t cb = seg_chain_bytes(n, segs, rm, lv);
   const size_t base = inst_lds_bytes_host(si) + (((size_t)in.N * 4u + 15u) & ~(size_t)15u);
+  // wavefronts per chain: W > 1 prices the step's moves on W SIMDs at once
+  // (same moves, same winner, so the same trajectories as W = 1), while the
+  // chains' wavefronts stay resident (two per SIMD at this kernel's VGPRs)
+  int W = std::min(moves / 64, kSegMaxWaves);
+  while (W > 1 && (int64_t)p->chains * W > 8 * (int64_t)ctx->num_cus) W >>= 1;
+  if (const char* e = std::getenv("VRPMS_SEG_WAVES")) W = std::max(1, std::min(atoi(e), kSegMaxWaves));
+  while (W > 1 && (moves / 64) % W != 0) --W;
   int cpw = 4;
   // fewer chains than 4 per CU: spread them, one wavefront per workgroup
   if (p->chains < 4 * ctx->num_cus) cpw = p->chains < 2 * ctx->num_cus ? 1 : 2;
+  if (W > 1) cpw = 1;
   while (cpw > 1 && base + (size_t)cpw * cb > ctx->max_lds) cpw >>= 1;
   const size_t lds = base + (size_t)cpw * cb;
   if (lds > ctx->max_lds) return 1;
   SegArgs a{si, p->chains, n, p->steps, p->window, wtypes, p->inv_t0, p->inv_alpha,
             (uint32_t)p->seed, (uint32_t)(p->seed >> 32), p->step0, d_cur, d_cur_key, d_best,
-            d_best_key, moves / 64, cpw, segs, rm, lv, cb};
+            d_best_key, moves / 64 / W, cpw, segs, rm, lv, cb, W};
   auto go = [&](auto kern) {
     if (lds > 65536)
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    kern<<<dim3((p->chains + cpw - 1) / cpw), dim3(64 * cpw), lds, s>>>(a);
+    kern<<<dim3((p->chains + cpw - 1) / cpw), dim3(64 * cpw * W), lds, s>>>(a);
   };
   if (in.use16) go(sa_seg_kernel<uint16_t>);
   else go(sa_seg_kernel<int32_t>);
