@@ -41,23 +41,26 @@ def run(chains, moves):
     x = synth.x_style(1000, seed=0)
     ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
     edge = runners.typical_edge(x.durations)
-    buf = (ctypes.c_ulonglong * (8 * 8192))()
+    NP = 12
+    buf = (ctypes.c_ulonglong * (NP * 8192))()
     r = runners.SARunner(ctx, x.n, chains=chains, total_steps=1000, durations=x.durations,
                          n_sep=x.K - 1, window=32, window_types=2, start="pack", moves=moves)
     for tag, T, steps in (("hot T=0.5e", 0.5, 1000), ("warm T=0.05e", 0.05, 2000),
                           ("cold T=0.005e", 0.005, 3000), ("cold T=0.005e", 0.005, 3000)):
-        lib.vrpms_debug_seg_prof(buf, 8 * 8192, 1)
+        lib.vrpms_debug_seg_prof(buf, NP * 8192, 1)
         r.inv_t = np.float32(1.0 / (T * edge))
         r.inv_alpha = np.float32(1.0)
         t0 = time.perf_counter()
         r.epoch(steps)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        lib.vrpms_debug_seg_prof(buf, 8 * 8192, 1)
-        a = np.array(buf[:8 * chains], dtype=np.float64).reshape(chains, 8).sum(0)
+        lib.vrpms_debug_seg_prof(buf, NP * 8192, 1)
+        a = np.array(buf[:NP * chains], dtype=np.float64).reshape(chains, NP).sum(0)
         st = a[2]
         print(f"{tag}: {steps / dt:,.0f} steps/s/chain | per step: pricing {a[0] / st * 10:.0f} ns, "
-              f"rebuild {a[1] / max(a[7], 1) * 10:.0f} ns x {a[7] / st:.3f}/step, "
+              f"rebuild {a[1] / max(a[7], 1) * 10:.0f} ns x {a[7] / st:.3f}/step "
+              f"(positions {a[8] / max(a[7], 1) * 10:.0f}, segments {a[9] / max(a[7], 1) * 10:.0f}, "
+              f"routes {a[10] / max(a[7], 1) * 10:.0f}, sparse {a[11] / max(a[7], 1) * 10:.0f}), "
               f"accept rate {a[3] / st:.3f}, "
               f"exchange {a[4] / st * 10:.0f} ns, setup {a[5] / chains * 10 / 1e3:.1f} us, "
               f"kernel {a[6] / chains * 10 / 1e3:.1f} us/chain | best "

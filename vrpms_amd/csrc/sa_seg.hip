@@ -75,11 +75,12 @@ struct SegXSlot {
 constexpr int kSegMaxWaves = 4;
 constexpr uint32_t kSegXBytes = 2 * kSegMaxWaves * sizeof(SegXSlot) + 32;
 
-// per-chain LDS: u32 [PE n+2 | PD n+2 | dur rm+1 | dsp, pmx, smx rm+1 each |
-// sparse (lv-1) x rm], then u16 [tok n+2 | SC n+2 | SP, RB, FNE, LNE1 segs+2]
+// per-chain LDS: u32 [PE n+2 | PD n+2 | LG n+2 | dur rm+1 | dsp, pmx, smx rm+1
+// each | sparse (lv-1) x rm], then u16 [tok n+2 | SC n+2 | SP, RB, FNE, LNE1
+// segs+2]
 __host__ __device__ inline uint32_t seg_chain_bytes(int n, int segs, int rm, int lv) {
   const uint32_t np2 = ((uint32_t)n + 2u + 1u) & ~1u;
-  const uint32_t u32s = 2u * np2 + 4u * (uint32_t)(rm + 1) + (uint32_t)(lv - 1) * (uint32_t)rm;
+  const uint32_t u32s = 3u * np2 + 4u * (uint32_t)(rm + 1) + (uint32_t)(lv - 1) * (uint32_t)rm;
   const uint32_t u16s = 2u * np2 + 4u * (uint32_t)(segs + 2);
   return ((4u * u32s + 2u * u16s + 15u) & ~15u) + kSegXBytes;
 }
@@ -136,15 +137,17 @@ VRPMS_DEV uint32_t dpp_rscan_max(uint32_t v, uint32_t& total) {
 }
 
 struct SegTabs {
-  uint32_t *PE, *PD, *dur, *dsp, *pmx, *smx, *sp;
+  uint32_t *PE, *PD, *LG, *dur, *dsp, *pmx, *smx, *sp;  // LG[q] = leg of the token at q
   uint16_t *tok, *SC, *SP, *RB, *FNE, *LNE1;
 };
 
 #ifdef VRPMS_SEG_PROF
 // per-chain counters (A/B builds only: tools/seg_prof.py): pricing ticks,
 // rebuild ticks, steps, accepts, cross-wavefront exchange ticks, setup ticks,
-// kernel ticks, rebuilds (wall_clock64, 100 MHz)
-__device__ unsigned long long g_seg_prof[8 * 8192];
+// kernel ticks, rebuilds, then the rebuild's parts: positions, segments,
+// routes, sparse table (wall_clock64, 100 MHz)
+constexpr int kSegProf = 12;
+__device__ unsigned long long g_seg_prof[kSegProf * 8192];
 #endif
 
 template <typename MatT>
@@ -182,7 +185,8 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
                                               (uint32_t)slot * a.chain_bytes);
     T.PE = u;
     T.PD = u + np2;
-    T.dur = u + 2 * np2;
+    T.LG = u + 2 * np2;
+    T.dur = u + 3 * np2;
     T.dsp = T.dur + (RM + 1);
     T.pmx = T.dsp + (RM + 1);
     T.smx = T.pmx + (RM + 1);
@@ -214,39 +218,75 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
   auto tourA = [&](int q) __attribute__((always_inline)) { return (uint32_t)T.tok[q]; };
 
   // ---- tables from the tokens in T.tok and the edges in T.PE[q + 1] -------
+  // Positions qa..qb hold new tokens / raw edges; the prefix sums before qa
+  // are current, and after qb every PE entry is off by the same amount
+  // (pe_old = PE[qb + 1] before the edges qa..qb were rewritten): a move
+  // permutes the tokens of its span in place, so the demand and separator
+  // prefixes after it are unchanged and the edge prefix shifts by the
+  // change of its junction edges.  The first build passes 0, n.
+#ifdef VRPMS_SEG_PROF
+  unsigned long long pf[kSegProf] = {};
+  unsigned long long pmark = 0;
+#define SEG_PT(k)                            \
+  do {                                       \
+    const unsigned long long nw = wall_clock64(); \
+    pf[k] += nw - pmark;                     \
+    pmark = nw;                              \
+  } while (0)
+#else
+#define SEG_PT(k) \
+  do {            \
+  } while (0)
+#endif
+  int reb_a = 0, reb_b = n;
+  uint32_t pe_old = 0;
   auto rebuild = [&]() __attribute__((always_inline)) {
     wave_sync();
+#ifdef VRPMS_SEG_PROF
+    pmark = wall_clock64();
+#endif
     // positions: PE (edges) and PD (demands) prefix sums in one 64-bit DPP
     // scan, the separator count SC in a 32-bit one, separator positions SP
-    uint64_t carry = 0;
-    uint32_t scarry = 0;
+    const int qa = reb_a, qb = reb_b;
+    uint64_t carry = ((uint64_t)T.PD[qa] << 32) | T.PE[qa];
+    uint32_t scarry = qa ? (uint32_t)T.SC[qa] : 0u;
+    if (qa == 0) carry = 0;
 #pragma unroll 1
-    for (int base = 0; base <= n; base += 64) {
+    for (int base = qa; base <= qb; base += 64) {
       const int q = base + lane;
-      const bool in = q < n;
+      const bool in = q < n && q <= qb;
       const uint32_t c = in ? (uint32_t)T.tok[q] : 1u;
-      uint64_t v = q <= n ? ((uint64_t)(in && c ? (uint32_t)dem[c] : 0u) << 32) | T.PE[q + 1] : 0ull;
+      uint64_t v = q <= qb ? ((uint64_t)(in && c ? (uint32_t)dem[c] : 0u) << 32) | T.PE[q + 1] : 0ull;
       const uint64_t tot = wave_scan_add_u64(v);
       uint32_t stot;
       const uint32_t sv = dpp_scan<false>(in && c == 0u ? 1u : 0u, stot);
-      if (q <= n) {
+      if (q <= qb) {
         T.PE[q + 1] = (uint32_t)(carry + v);
         T.PD[q + 1] = (uint32_t)((carry + v) >> 32);
       }
       if (in) {
+        T.LG[q] = c ? leg[c] : 0u;
         T.SC[q + 1] = (uint16_t)(scarry + sv);
         if (c == 0u && scarry + sv <= (uint32_t)SEGS) T.SP[scarry + sv - 1] = (uint16_t)q;
       }
       carry += tot;
       scarry += stot;
     }
+    if (qb < n) {  // the edge prefix after the span moves by its junctions' change
+      const uint32_t dpe = (uint32_t)carry - pe_old;
+      if (dpe != 0u)
+#pragma unroll 4
+        for (int q = qb + 1 + lane; q <= n; q += 64) T.PE[q + 1] += dpe;
+    } else {
+      S = (int)scarry;
+    }
     if (lane == 0) {
       T.PE[0] = 0u;
       T.PD[0] = 0u;
       T.SC[0] = 0;
     }
-    S = (int)scarry;
     wave_sync();
+    SEG_PT(8);
     seg_ok = S <= SEGS;
     if (!seg_ok) return;
     // segments, one lane each: how many routes the greedy split makes of it
@@ -302,6 +342,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
     }
     if (lane == 0) T.RB[S + 1] = (uint16_t)R;
     wave_sync();
+    SEG_PT(9);
     // route durations, one lane per segment
 #pragma unroll 1
     for (int g = lane; g <= S; g += 64) {
@@ -352,6 +393,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
       T.pmx[0] = 0u;
     }
     wave_sync();
+    SEG_PT(10);
 #pragma unroll 1
     for (int l = 1; l < LV; ++l) {
       const int w = 1 << (l - 1);
@@ -360,6 +402,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
       for (int r = lane; r + 2 * w <= R; r += 64) dst[r] = max(src[r], src[r + w]);
       wave_sync();
     }
+    SEG_PT(11);
     const int l1 = T.LNE1[S];
     Tt = l1 ? S - (l1 - 1) : S;
   };
@@ -385,9 +428,6 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
   uint64_t ck = 0;
   bool need_build = true, first = true;
   float invT = a.inv_t0;
-#ifdef VRPMS_SEG_PROF
-  unsigned long long pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
 #pragma unroll 1
   for (int st = 0;; ++st) {
     if (need_build) {
@@ -460,27 +500,128 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
       uint64_t k = ~0ull;
       bool full = !seg_ok;
       if (seg_ok) {
-        // the open route and what the walk has closed
-        uint32_t c_dur = 0, c_load = 0, c_prev = 0, c_sum = 0, c_max = 0;
+        // The table reads a move needs are issued in three dependent rounds
+        // (separator counts at the pieces' ends; separator positions and
+        // route indices; prefix sums / legs at the runs' ends and route
+        // table entries), then the pieces are composed in registers.  Only a
+        // run that overflows the open route (a binary-searched capacity cut)
+        // or a reversed multi-route segment reads the tables again.
+        const bool opt = m.typ == kMove2Opt, swp = m.typ == kMoveSwap, fwd = m.i < m.j;
+        // The moved span as pieces of the current tour (moved_index,
+        // tour.hpp) in three slots -- 2-opt [A[i..j] reversed] | swap [A[j]]
+        // [A[i+1..j-1]] [A[i]] | relocate i<j [A[i+1..j]] [A[i]] | relocate
+        // i>j [A[i]] [A[j..i-1]] -- then the rest of the last changed segment
+        // A[hi+1 .. en] and its closing separator.  Every lane runs the same
+        // predicated steps per slot, so the wave's control flow stays
+        // uniform: the part before the piece's first separator (in the moved
+        // order) joins the open route, the separator closes it, whole
+        // segments between its separators come from the route tables, the
+        // part after its last separator opens the next route.
+        int X[3], Y[3];
+        uint32_t JV[3];
+        X[0] = opt ? m.i : swp ? m.j : fwd ? m.i + 1 : m.i;
+        Y[0] = opt ? m.j : swp ? m.j : fwd ? m.j : m.i;
+        JV[0] = jx0;
+        X[1] = opt ? 1 : swp ? m.i + 1 : fwd ? m.i : m.j;
+        Y[1] = opt ? 0 : swp ? m.j - 1 : fwd ? m.i : m.i - 1;
+        JV[1] = fwd && !swp ? jx2 : jx1;
+        X[2] = swp ? m.i : 1;
+        Y[2] = swp ? m.i : 0;
+        JV[2] = jx2;
+        // round 1: separator counts
+        const int s0 = T.SC[lo], sH = T.SC[hi + 1];
+        const int lneS = T.LNE1[S];
+        const uint32_t dspR = T.dsp[R];
+        int SA[3], SB[3];
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const bool live = X[s] <= Y[s];
+          SA[s] = live ? (int)T.SC[X[s]] : 0;
+          SB[s] = live ? (int)T.SC[Y[s] + 1] : 0;
+        }
+        // round 2: separator positions, route indices
+        const int stp = SPX(s0 - 1) + 1, en = SPX(sH);
+        const int ra = T.RB[s0], rz = T.RB[sH + 1];  // sH = the last changed segment
+        int SMIN[3], SMAX[3], R0[3], R1[3], GF[3];
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const bool hs = SA[s] != SB[s], rev = opt && s == 0;
+          SMIN[s] = hs ? (int)T.SP[SA[s]] : 0;
+          SMAX[s] = hs ? (int)T.SP[SB[s] - 1] : 0;
+          // segments g0 = SA + 1 .. g1 = SB - 1 lie between the piece's
+          // separators (SC[SP[k]] = k)
+          const bool mid = SB[s] - SA[s] >= 2;
+          R0[s] = mid ? (int)T.RB[SA[s] + 1] : 0;
+          R1[s] = mid ? (int)T.RB[SB[s]] : 0;
+          GF[s] = mid ? (rev ? (int)T.FNE[SA[s] + 1] : (int)T.LNE1[SB[s] - 1] - 1) : 0;
+        }
+        // round 3: the runs' prefix sums and legs, the route tables
+        struct RunP {
+          int x, y;
+          uint32_t pdx, pdy, pex, pey, lgx, lgy;
+        };
+        auto pre = [&](int x, int y) __attribute__((always_inline)) -> RunP {
+          RunP p{x, y, 0u, 0u, 0u, 0u, 0u, 0u};
+          if (x <= y) {
+            p.pdx = T.PD[x];
+            p.pdy = T.PD[y + 1];
+            p.pex = T.PE[x + 1];
+            p.pey = T.PE[y + 1];
+            p.lgx = T.LG[x];
+            p.lgy = T.LG[y];
+          }
+          return p;
+        };
+        const RunP p_start = pre(stp, lo - 1);
+        const RunP p_tail = pre(hi + 1, (en < n ? en : n) - 1);
+        RunP PA[3], PDn[3];
+        uint32_t ISUM[3], IMAX[3];
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const bool live = X[s] <= Y[s], hs = SA[s] != SB[s], rev = opt && s == 0;
+          const int x = X[s], y = Y[s], smin = SMIN[s], smax = SMAX[s];
+          PA[s] = pre(!hs ? x : rev ? smax + 1 : x, !hs ? (live ? y : x - 1) : rev ? y : smin - 1);
+          PDn[s] = pre(hs ? (rev ? x : smax + 1) : 1, hs ? (rev ? smin - 1 : y) : 0);
+          ISUM[s] = 0u;
+          IMAX[s] = 0u;
+          if (R1[s] > R0[s]) {
+            ISUM[s] = T.dsp[R1[s]] - T.dsp[R0[s]];
+            IMAX[s] = rmaxq(R0[s], R1[s] - 1);
+          }
+        }
+        const uint32_t dspa = T.dsp[ra], dspz = T.dsp[rz], pmxa = T.pmx[ra], smxz = T.smx[rz];
+
+        // the open route and what the composition has closed
+        uint32_t c_dur = 0, c_load = 0, c_pl = 0, c_sum = 0, c_max = 0;  // c_pl: leg of its last customer
+        bool c_has = false;
         int c_cnt = 0;
         uint32_t isum = 0, imax = 0;
         int icnt = 0, seps = 0;
         bool cust = false;
         auto close = [&]() __attribute__((always_inline)) {
-          const uint32_t d = c_dur + (c_prev ? leg[c_prev] : 0u);
+          const uint32_t d = c_dur + c_pl;
           c_sum += d;
           c_max = max(c_max, d);
           ++c_cnt;
-          c_dur = c_load = c_prev = 0u;
+          c_dur = c_load = c_pl = 0u;
+          c_has = false;
         };
         // customers A[x..y] joined to the open route in the moved order (rev:
         // A[y] first), cut where the greedy split's next customer does not
         // fit; jv = the junction edge into the first one when the open route
         // holds a customer
-        auto run = [&](int x, int y, bool rev, uint32_t jv) __attribute__((always_inline)) {
+        auto run = [&](const RunP& p, bool rev, uint32_t jv) __attribute__((always_inline)) {
+          int x = p.x, y = p.y;
           if (x > y) return;
           seps = 0;
           cust = true;
+          if (p.pdy - p.pdx <= cap - c_load) {  // fits: from the round-3 values
+            c_dur += (c_has ? jv : (rev ? p.lgy : p.lgx)) + p.pey - p.pex;
+            c_load += p.pdy - p.pdx;
+            c_pl = rev ? p.lgx : p.lgy;
+            c_has = true;
+            return;
+          }
           while (true) {
             const uint32_t room = cap - c_load;
             const bool fits = T.PD[y + 1] - T.PD[x] <= room;
@@ -496,81 +637,44 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
               if (rev) pa = l + 1; else pb = l - 1;
             }
             if (pa <= pb) {
-              const uint32_t F = rev ? T.tok[pb] : T.tok[pa];
-              c_dur += (c_prev ? jv : leg[F]) + T.PE[pb + 1] - T.PE[pa + 1];
+              c_dur += (c_has ? jv : T.LG[rev ? pb : pa]) + T.PE[pb + 1] - T.PE[pa + 1];
               c_load += T.PD[pb + 1] - T.PD[pa];
-              c_prev = rev ? T.tok[pa] : T.tok[pb];
+              c_pl = T.LG[rev ? pa : pb];
+              c_has = true;
             }
             if (fits) break;
             close();
             if (rev) y = pa - 1; else x = pb + 1;
           }
         };
-        const int s0 = T.SC[lo];
-        const int stp = SPX(s0 - 1) + 1;
-        const int en = SPX(T.SC[hi + 1]);
-        const bool opt = m.typ == kMove2Opt, swp = m.typ == kMoveSwap, fwd = m.i < m.j;
         // the start of the first changed segment, up to lo
-        run(stp, lo - 1, false, 0u);
-        // The moved span as pieces of the current tour (moved_index,
-        // tour.hpp) in four slots -- 2-opt [A[i..j] reversed] | swap [A[j]]
-        // [A[i+1..j-1]] [A[i]] | relocate i<j [A[i+1..j]] [A[i]] | relocate
-        // i>j [A[i]] [A[j..i-1]] -- then slot 3, the rest of the last changed
-        // segment A[hi+1 .. en] (its closing separator included).  Every lane
-        // runs the same four predicated steps per slot, so the wave's control
-        // flow stays uniform: the part before the piece's first separator (in
-        // the moved order) joins the open route, the separator closes it,
-        // whole segments between its separators come from the route tables,
-        // the part after its last separator opens the next route.
-#pragma unroll 1
-        for (int sl = 0; sl < 4; ++sl) {
-          int x, y;
-          uint32_t jv;
-          if (sl == 0) {
-            x = opt ? m.i : swp ? m.j : fwd ? m.i + 1 : m.i;
-            y = opt ? m.j : swp ? m.j : fwd ? m.j : m.i;
-            jv = jx0;
-          } else if (sl == 1) {
-            x = opt ? 1 : swp ? m.i + 1 : fwd ? m.i : m.j;
-            y = opt ? 0 : swp ? m.j - 1 : fwd ? m.i : m.i - 1;
-            jv = fwd && !swp ? jx2 : jx1;
-          } else if (sl == 2) {
-            x = swp ? m.i : 1;
-            y = swp ? m.i : 0;
-            jv = jx2;
-          } else {
-            x = hi + 1;
-            y = en < n ? en : n - 1;
-            jv = jx3;
-          }
-          const bool rev = opt && sl == 0;
-          const bool live = x <= y;
-          const int sa = live ? (int)T.SC[x] : 0, sb = live ? (int)T.SC[y + 1] : 0;
-          const bool hs = sa != sb;  // the piece holds a separator
-          const int smin = hs ? (int)T.SP[sa] : 0, smax = hs ? (int)T.SP[sb - 1] : 0;
+        run(p_start, false, 0u);
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const bool hs = SA[s] != SB[s], rev = opt && s == 0;
           // (A) up to the first separator in the moved order
-          run(!hs ? x : rev ? smax + 1 : x, !hs ? (live ? y : x - 1) : rev ? y : smin - 1, rev, jv);
+          run(PA[s], rev, JV[s]);
           if (hs) {
             // (B) the separator closes the open route
             close();
             ++seps;
             // (C) whole segments between the piece's separators
-            if (smin < smax) {
-              const int g0 = T.SC[smin] + 1, g1 = T.SC[smax];
-              const int r0 = T.RB[g0], r1 = T.RB[g1 + 1];
+            if (SB[s] - SA[s] >= 2) {
+              const int g0 = SA[s] + 1, g1 = SB[s] - 1;
+              const int r0 = R0[s], r1 = R1[s];
               if (rev && r1 - r0 != g1 - g0 + 1) {
                 // reversed and split by capacity: a reversal splits differently, walk them
                 for (int g = g1; g >= g0; --g) {
-                  run(SPX(g - 1) + 1, SPX(g) - 1, true, 0u);
+                  run(pre(SPX(g - 1) + 1, SPX(g) - 1), true, 0u);
                   close();
                   ++seps;
                 }
               } else {
-                isum += T.dsp[r1] - T.dsp[r0];
-                imax = max(imax, rmaxq(r0, r1 - 1));
+                isum += ISUM[s];
+                imax = max(imax, IMAX[s]);
                 icnt += r1 - r0;
                 // the last customer in the moved order and the separators after it
-                const int gf = rev ? (int)T.FNE[g0] : (int)T.LNE1[g1] - 1;
+                const int gf = GF[s];
                 const bool has = rev ? gf <= g1 : gf >= g0;
                 if (has) {
                   seps = rev ? gf - g0 + 1 : g1 + 1 - gf;
@@ -582,18 +686,20 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
             }
           }
           // (D) the part after the last separator opens the next route
-          run(hs ? (rev ? x : smax + 1) : 1, hs ? (rev ? smin - 1 : y) : 0, rev, 0u);
+          run(PDn[s], rev, 0u);
         }
-        if (en >= n) close();  // the tour's end closes the last route
-        const int glast = en < n ? (int)T.SC[en] : S;
-        const int ra = T.RB[s0], rz = T.RB[glast + 1];
+        // the rest of the last changed segment, closed by its separator (or
+        // the tour's end)
+        run(p_tail, false, jx3);
+        close();
+        if (en < n) ++seps;
         const int Rb = R - (rz - ra) + c_cnt + icnt;
         int Tb = Tt;
-        const bool tail_kept = en < n && (int)T.LNE1[S] - 1 > glast;
+        const bool tail_kept = en < n && lneS - 1 > sH;
         if (!tail_kept && cust) Tb = seps + (en < n ? n - 1 - en : 0);
         if (Rb - Tb <= K) {
-          const uint32_t dsum = T.dsp[ra] + c_sum + isum + T.dsp[R] - T.dsp[rz];
-          const uint32_t dmax = max(max(T.pmx[ra], T.smx[rz]), max(imax, c_max));
+          const uint32_t dsum = dspa + c_sum + isum + dspR - dspz;
+          const uint32_t dmax = max(max(pmxa, smxz), max(imax, c_max));
           k = cvrp_key(0, dsum, dmax, I.sp.objective);
         } else if (shortcut) {
           k = ~0ull;
@@ -674,17 +780,23 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
         if (W > 1) __syncthreads();  // every wavefront is done reading the tables
         if (cw == 0) {
           const MoveMap mmb = move_map(mb);
-          // the new tour's tokens and edges: a kept adjacency's edge is a
-          // difference of PE (forward, or reversed on the symmetric matrix; PE
-          // is complete even when the segment tables are not), the four
+          // the new tour's tokens (positions blo..bhi) and edges (into
+          // positions blo..bhi + 1): a kept adjacency's edge is a difference
+          // of PE (forward, or reversed on the symmetric matrix; PE is
+          // complete even when the segment tables are not), the four
           // junctions are the winner's gathers
+          const int hq = min(bhi + 1, n);
+          reb_a = blo;
+          reb_b = hq;
+          pe_old = T.PE[hq + 1];
           uint32_t v_tok[kSegRegs], v_e[kSegRegs];
 #pragma unroll
           for (int i = 0; i < kSegRegs; ++i) {
-            const int q = lane + 64 * i;
+            if (blo + 64 * i > hq) break;
+            const int q = blo + lane + 64 * i;
             v_tok[i] = 0u;
             v_e[i] = 0u;
-            if (q > n) continue;
+            if (q > hq) continue;
             const int sq = map_src(mmb, q), sp = map_src(mmb, q - 1);
             if (q < n) v_tok[i] = T.tok[sq];
             if (q == blo) v_e[i] = w0;
@@ -697,8 +809,9 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
           wave_sync();
 #pragma unroll
           for (int i = 0; i < kSegRegs; ++i) {
-            const int q = lane + 64 * i;
-            if (q > n) continue;
+            if (blo + 64 * i > hq) break;
+            const int q = blo + lane + 64 * i;
+            if (q > hq) continue;
             if (q < n) T.tok[q] = (uint16_t)v_tok[i];
             T.PE[q + 1] = v_e[i];
           }
@@ -721,7 +834,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
 #ifdef VRPMS_SEG_PROF
     pf[6] = wall_clock64() - pk0;
     if (chain < 8192)
-      for (int i = 0; i < 8; ++i) g_seg_prof[8 * chain + i] += pf[i];
+      for (int i = 0; i < kSegProf; ++i) g_seg_prof[kSegProf * chain + i] += pf[i];
 #endif
   }
 }
@@ -781,9 +894,10 @@ extern "C" int vrpms_debug_seg_prof(unsigned long long* out, int count, int rese
       hipSuccess)
     return -2;
   if (reset) {
-    static unsigned long long zero[8 * 8192];
+    static unsigned long long zero[vrpms::kSegProf * 8192];
     (void)hipMemcpyToSymbol(HIP_SYMBOL(vrpms::g_seg_prof), zero, sizeof(zero));
   }
   return 0;
 }
+#undef SEG_PT
 #endif
