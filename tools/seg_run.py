@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """sa_seg_kernel alone on cfg 4 (X-1000, K - 1 separators, first-fit
 starts, windowed 2-opt + swap / relocate anywhere) -- a short target for
-rocprofv3 --pmc / --stats passes.  usage: seg_run.py [chains] [moves] [steps]"""
+rocprofv3 --pmc / --stats passes.  usage: seg_run.py [chains] [moves] [steps]   (SEG_LIB=<path>: another libvrpms.so)"""
 import os
 import sys
 
@@ -9,12 +9,14 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
-from vrpms_amd import runners, synth  # noqa: E402
+from vrpms_amd import _lib, runners, synth  # noqa: E402
 from vrpms_amd.core import CVRP, Context  # noqa: E402
 
 chains = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 moves = int(sys.argv[2]) if len(sys.argv) > 2 else 128
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 1000
+if os.environ.get("SEG_LIB"):  # an A/B build of the library
+    _lib.load(os.environ["SEG_LIB"])
 ctx = Context(0)
 x = synth.x_style(1000, seed=0)
 ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
