@@ -9,6 +9,8 @@ time, every demand fits an empty vehicle.
 """
 from __future__ import annotations
 
+import numpy as np
+
 from . import spec
 
 
@@ -175,33 +177,51 @@ def _moved(A, m):
 
 
 # ---------------------------------------------------------------------------
-# Segment pricing (sa_seg_kernel, oracle_c.c seg_key): uniform capacity,
-# static symmetric matrix, any tour.  The greedy split with unlimited
-# vehicles is the concatenation, over the separator-delimited segments, of
-# each segment's own greedy split from an empty vehicle (every separator
-# closes a route, an empty one lasting 0).  A route's duration is a sum of
-# consecutive edges of the tour (a separator standing for the depot), so
-# with prefix sums over the positions any run of a moved tour that reads the
-# current tour contiguously (forward, or reversed on a symmetric matrix) is
-# priced in O(1), and a capacity cut inside a run is found by a binary search
-# on the prefix demands.  The fleet limit is one count: with R routes (empty
-# segments included) and T separators after the last customer, the split
-# serves everyone iff R - T <= K (R - 1 - T closures precede the last
-# customer).  Start times do not enter a static route's duration.
+# Segment pricing (sa_seg_kernel, oracle_c.c seg_key): static symmetric
+# matrix, every demand fits an empty vehicle, any tour.  The greedy split
+# with unlimited vehicles is the concatenation, over the separator-delimited
+# segments, of each segment's own greedy split, started on the vehicle its
+# first route is given (every separator closes a route, an empty one lasting
+# 0).  A route's duration is a sum of consecutive edges of the tour (a
+# separator standing for the depot), so with prefix sums over the positions
+# any run of a moved tour that reads the current tour contiguously (forward,
+# or reversed on a symmetric matrix) is priced in O(1), and a capacity cut
+# inside a run is found by a binary search on the prefix demands.  The fleet
+# limit is one count: with R routes (empty segments included) and T
+# separators after the last customer, the split serves everyone iff R - T <=
+# K (R - 1 - T closures precede the last customer).  Start times do not
+# enter a static route's duration.
+#
+# Heterogeneous fleets (per-vehicle capacities, route r on vehicle r): a
+# move that changes the number of routes before a stretch of the current
+# tour hands that stretch's routes to other vehicles (r -> r + delta).
+# Route r keeps its split on vehicle r + delta iff need[r] <= cap(r + delta)
+# <= allow[r] (need = its load; allow = load + the demand of the customer
+# that did not fit - 1 when a capacity cut closed it, else unbounded), so
+# whole segments are still priced from the tables when that holds for all
+# their routes, and walked otherwise; an unchanged tail that fails it is
+# re-evaluated in full.
 # ---------------------------------------------------------------------------
+INF = 1 << 62
+FULL = "full"
+
+
 class SegTables:
-    """Tables of tour A (uniform capacity `cap`, every demand <= cap).
+    """Tables of tour A (capacity `cap`: one int for the whole fleet, or one
+    per vehicle; every demand <= the smallest).
 
     e(p), p in [0, n]: edge into position p from the token before it (A[-1] =
     A[n] = 0), 0 between two depots.  PE[q] = sum e(p < q) (q <= n + 1);
     PD[q] = demand of A[0..q-1]; SC[q] = separators in A[0..q-1]; SP[k] =
     position of separator k (spx(-1) = -1, spx(S) = n); PC[q] / NC[q]: last /
     first customer position <= q / >= q (-1 / n: none).  Routes (unlimited
-    vehicles): RB[s] = first route of segment s (RB[S + 1] = R), dur[r]; T =
-    separators after the last customer."""
+    vehicles, route r on vehicle min(r, K - 1)): RB[s] = first route of
+    segment s (RB[S + 1] = R), dur[r], need[r], allow[r]; T = separators
+    after the last customer."""
 
     def __init__(self, D, A, dem, cap):
-        self.D, self.dem, self.cap = D, dem, cap
+        self.D, self.dem = D, dem
+        self.caps = [int(cap)] if isinstance(cap, (int, np.integer)) else [int(c) for c in cap]
         self.A = list(A)
         n = self.n = len(A)
         ext = [0] + self.A + [0]
@@ -224,13 +244,15 @@ class SegTables:
         for q in range(n - 1, -1, -1):
             nxt = q if self.A[q] else nxt
             self.NC[q] = nxt
-        self.dur, self.RB = [], []
+        self.dur, self.RB, self.need, self.allow = [], [], [], []
         for s in range(self.S + 1):
             self.RB.append(len(self.dur))
-            acc = Acc()
+            acc = Acc(v=len(self.dur))
             run(self, acc, self.spx(s - 1) + 1, self.spx(s) - 1, False)
             close_route(self, acc)
             self.dur += acc.routes
+            self.need += acc.needs
+            self.allow += acc.allows
         self.R = len(self.dur)
         self.RB.append(self.R)
         self.T = n - 1 - self.PC[n - 1] if n else 0
@@ -250,27 +272,44 @@ class SegTables:
     def d0(self, a, b):
         return 0 if a == 0 and b == 0 else int(self.D[a, b])
 
+    def cap_of(self, v):
+        return self.caps[min(v, len(self.caps) - 1)]
+
+    def keeps(self, r0, r1, delta):
+        """Routes r0..r1-1 split the same on vehicles r + delta."""
+        return all(self.need[r] <= self.cap_of(r + delta) <= self.allow[r] for r in range(r0, r1))
+
+    def one_class(self, v0, v1):
+        """Vehicles v0..v1 all have the same capacity (v1 < v0: none)."""
+        return all(self.cap_of(v) == self.cap_of(v0) for v in range(v0, v1 + 1))
+
 
 class Acc:
-    """The open route of a pricing walk and what the walk has closed."""
+    """The open route of a pricing walk (on vehicle v) and what the walk has
+    closed."""
 
-    def __init__(self, dur=0, load=0, prev=0):
-        self.dur, self.load, self.prev = dur, load, prev
-        self.routes = []
+    def __init__(self, dur=0, load=0, prev=0, v=0):
+        self.dur, self.load, self.prev, self.v = dur, load, prev, v
+        self.routes, self.needs, self.allows = [], [], []
 
 
-def close_route(T, acc):
+def close_route(T, acc, nxt_dem=None):
+    """Close the open route; nxt_dem = the demand of the customer that did
+    not fit (a capacity cut), None for a separator or the tour's end."""
     acc.routes.append(acc.dur + T.d0(acc.prev, 0))
+    acc.needs.append(acc.load)
+    acc.allows.append(INF if nxt_dem is None else acc.load + nxt_dem - 1)
     acc.dur = acc.load = acc.prev = 0
+    acc.v += 1
 
 
 def run(T, acc, a, b, rev):
     """Customers A[a..b] (no separator among them) joined to the open route
     in the moved order (reversed: A[b] first), cutting the route wherever
-    the greedy split's next customer does not fit."""
+    the greedy split's next customer does not fit its vehicle."""
     PE, PD, A = T.PE, T.PD, T.A
     while a <= b:
-        room = T.cap - acc.load
+        room = T.cap_of(acc.v) - acc.load
         if PD[b + 1] - PD[a] <= room:
             acc.dur += T.d0(acc.prev, A[b] if rev else A[a]) + PE[b + 1] - PE[a + 1]
             acc.load += PD[b + 1] - PD[a]
@@ -290,7 +329,7 @@ def run(T, acc, a, b, rev):
                 acc.dur += T.d0(acc.prev, A[a]) + PE[q + 1] - PE[a + 1]
                 acc.load += PD[q + 1] - PD[a]
                 acc.prev = A[q]
-            close_route(T, acc)
+            close_route(T, acc, PD[q + 2] - PD[q + 1])
             a = q + 1
         else:
             # first x in [a, b + 1] with PD[b + 1] - PD[x] <= room
@@ -306,13 +345,14 @@ def run(T, acc, a, b, rev):
                 acc.dur += T.d0(acc.prev, A[b]) + PE[b + 1] - PE[x + 1]
                 acc.load += PD[b + 1] - PD[x]
                 acc.prev = A[x]
-            close_route(T, acc)
+            close_route(T, acc, PD[x] - PD[x - 1])
             b = x - 1
 
 
 def price_seg(T: SegTables, m, K: int, objective: int = 0):
-    """Key of T.A moved by m, or None when the moved tour leaves a customer
-    unserved (R - T > K)."""
+    """Key of T.A moved by m; None when the moved tour leaves a customer
+    unserved (R - T > K); FULL when (heterogeneous fleet) the tail after the
+    changed segments moves to vehicles that split it differently."""
     typ, i, j = m
     A, SC = T.A, T.SC
     n = T.n
@@ -328,7 +368,7 @@ def price_seg(T: SegTables, m, K: int, objective: int = 0):
         mid = [(i + 1, j, False), (i, i, False)]
     else:
         mid = [(i, i, False), (j, i - 1, False)]
-    acc = Acc()
+    acc = Acc(v=T.RB[s0])
     inner = {"sum": 0, "max": 0, "cnt": 0}
     tr = {"seps": 0, "cust": False}      # separators since the last customer of the region
 
@@ -356,15 +396,26 @@ def price_seg(T: SegTables, m, K: int, objective: int = 0):
         if smin < smax:                  # whole segments of A between the piece's separators
             g0, g1 = SC[smin] + 1, SC[smax]
             r0, r1 = T.RB[g0], T.RB[g1 + 1]
-            if rev and r1 - r0 != g1 - g0 + 1:
-                # a reversed segment of several routes splits differently: walk them
-                for g in range(g1, g0 - 1, -1):
-                    crun(T.spx(g - 1) + 1, T.spx(g) - 1, True)
+            v = acc.v                    # the vehicle their first route gets now
+            if rev:
+                # a reversed segment of several routes splits differently, and
+                # reversed single-route segments keep their splits when one
+                # capacity class serves them before and after
+                # (the moved order hands them to the vehicles in reverse)
+                tabled = r1 - r0 == g1 - g0 + 1 and T.one_class(r0, r1 - 1) and \
+                    T.one_class(v, v + r1 - r0 - 1) and T.cap_of(v) == T.cap_of(r0)
+            else:
+                tabled = v == r0 or T.keeps(r0, r1, v - r0)
+            if not tabled:               # walk them
+                gs = range(g1, g0 - 1, -1) if rev else range(g0, g1 + 1)
+                for g in gs:
+                    crun(T.spx(g - 1) + 1, T.spx(g) - 1, rev)
                     sep()
             else:
                 inner["sum"] += T.dsp[r1] - T.dsp[r0]
                 inner["max"] = max([inner["max"]] + T.dur[r0:r1])
                 inner["cnt"] += r1 - r0
+                acc.v += r1 - r0
                 if rev:
                     c = T.NC[smin]       # the interior's last customer in the moved order
                     if c < smax:
@@ -399,6 +450,8 @@ def price_seg(T: SegTables, m, K: int, objective: int = 0):
         Tb = tr["seps"] + (n - 1 - en if en < n else 0)
     else:
         Tb = T.T
+    if R != T.R and not T.keeps(rz, T.R, R - T.R):
+        return FULL                      # the tail's routes move to vehicles that split them differently
     if R - Tb > K:
         return None
     dsum = T.dsp[ra] + sum(acc.routes) + inner["sum"] + T.dsp[T.R] - T.dsp[rz]

@@ -91,3 +91,53 @@ def test_segment_pricing_matches_full_evaluation(nn, slack, obj, window, sep):
                 A = mv
                 T = rmod.SegTables(D, A, dem, cap)
     assert checked > 5 and checked + none == 900
+
+
+@pytest.mark.parametrize("nn,classes,shuffle,window,obj", [
+    (60, (1.0, 1.4, 0.7), False, 0, 0), (90, (1.0, 0.8), True, 8, 0),
+    (120, (1.2, 1.0, 0.75), False, 16, 1), (50, (1.0, 1.0, 1.5), True, 0, 0)])
+def test_segment_pricing_heterogeneous_fleet(nn, classes, shuffle, window, obj):
+    """Segment pricing with per-vehicle capacities (route r on vehicle r):
+    keys equal eval_cvrp, None exactly when a customer is unserved, FULL
+    (re-evaluate) only when the unchanged tail moves to vehicles that split
+    it differently -- capacity classes in vehicle order and shuffled, on
+    first-fit and random separator placements."""
+    rng = np.random.default_rng(nn * 7 + len(classes))
+    checked = none = full = 0
+    for trial in range(3):
+        inst = synth.cvrp(nn, max(3, nn // 10), seed=trial + 11 * nn, slack=1.6)
+        K = len(inst.capacities)
+        base = int(inst.capacities[0])
+        caps = [int(base * classes[min(len(classes) - 1, k * len(classes) // K)]) for k in range(K)]
+        if shuffle:
+            rng.shuffle(caps)
+        dem = [int(x) for x in inst.demand]
+        caps = [max(c, max(dem)) for c in caps]
+        D = inst.durations[0]
+        perm = rng.permutation(np.arange(1, nn + 1))
+        if trial < 2:
+            A = [int(x) for x in spec.pack_separators(perm, K - 1, dem, caps)]
+        else:
+            A = [int(x) for x in perm] + [0] * (K - 1)
+            rng.shuffle(A)
+        T = rmod.SegTables(D, A, dem, caps)
+        for _ in range(300):
+            n = len(A)
+            r = [int(x) for x in rng.integers(0, 2**32, size=3, dtype=np.uint64)]
+            typ, i, j = spec.decode_move_window(r[0], r[1], r[2], n, window, 0)
+            mv = rmod._moved(A, (typ, i, j))
+            ref = spec.eval_cvrp(inst.durations, mv, inst.demand, caps, inst.start_times, obj)
+            got = rmod.price_seg(T, (typ, i, j), K, obj)
+            if got == rmod.FULL:
+                full += 1
+            elif ref["unvisited"] == 0:
+                assert got == ref["key"], (trial, typ, i, j)
+                checked += 1
+            else:
+                assert got is None, (trial, typ, i, j)
+                none += 1
+            if rng.random() < 0.4 and (ref["unvisited"] == 0 or rng.random() < 0.3):
+                A = mv
+                T = rmod.SegTables(D, A, dem, caps)
+    assert checked > 30 and checked + none + full == 900
+    assert full < 300

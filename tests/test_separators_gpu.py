@@ -376,7 +376,36 @@ SEG_CASES = [
      0, 128),
     ("cvrp1200_long_tours", lambda: synth.cvrp(1200, 60, seed=10), "pack", 4, 60, 1 / 300.0, 32, 2,
      64),
+    # heterogeneous fleets (per-vehicle capacities): the variant that tracks each
+    # route's vehicle -- capacity classes in vehicle order with staggered starts,
+    # shuffled per-vehicle capacities, and a hot infeasible start whose segments
+    # split into several routes (the split's fixed-point pass, tail re-evaluation)
+    ("x1000_three_classes_starts", lambda: _starts(_classes(synth.x_style(1000, seed=11),
+                                                            (1.25, 1.0, 0.8))), "pack", 8, 150,
+     1 / 300.0, 32, 2, 128),
+    ("x1000_shuffled_caps_full_range", lambda: _classes(synth.x_style(1000, seed=12),
+                                                        (1.3, 1.0, 0.85, 1.1), shuffle=True),
+     "pack", 8, 100, 1 / 300.0, 0, 0, 64),
+    ("cvrp300_het_hot_random", lambda: _classes(synth.cvrp(300, 24, seed=13, slack=1.2),
+                                                (1.5, 1.0, 0.7)), "random", 8, 80, 1e-7, 0, 0, 128),
+    ("cvrp300_het_warm_m256", lambda: _classes(synth.cvrp(300, 24, seed=14, slack=1.3),
+                                               (1.2, 0.9), shuffle=True), "pack", 8, 200,
+     1 / 60.0, 24, 2, 256),
 ]
+
+
+def _classes(inst, fracs, shuffle=False):
+    """inst with per-vehicle capacities: len(fracs) classes of base * frac in
+    vehicle order (shuffled: in a random order), each at least the largest
+    demand."""
+    import dataclasses
+    K = len(inst.capacities)
+    base = int(inst.capacities[0])
+    caps = np.array([max(int(base * fracs[k * len(fracs) // K]), int(inst.demand.max()))
+                     for k in range(K)], dtype=np.int64)
+    if shuffle:
+        np.random.default_rng(K).shuffle(caps)
+    return dataclasses.replace(inst, capacities=caps)
 
 
 def _starts(inst):

@@ -41,7 +41,7 @@ def run(chains, moves):
     x = synth.x_style(1000, seed=0)
     ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
     edge = runners.typical_edge(x.durations)
-    NP = 12
+    NP = 18
     buf = (ctypes.c_ulonglong * (NP * 8192))()
     r = runners.SARunner(ctx, x.n, chains=chains, total_steps=1000, durations=x.durations,
                          n_sep=x.K - 1, window=32, window_types=2, start="pack", moves=moves)
@@ -57,10 +57,13 @@ def run(chains, moves):
         lib.vrpms_debug_seg_prof(buf, NP * 8192, 1)
         a = np.array(buf[:NP * chains], dtype=np.float64).reshape(chains, NP).sum(0)
         st = a[2]
+        mv = st * max(1, moves // 64 // int(os.environ.get("VRPMS_SEG_WAVES", "1"))) / 10
         print(f"{tag}: {steps / dt:,.0f} steps/s/chain | per step: pricing {a[0] / st * 10:.0f} ns, "
               f"rebuild {a[1] / max(a[7], 1) * 10:.0f} ns x {a[7] / st:.3f}/step "
               f"(positions {a[8] / max(a[7], 1) * 10:.0f}, segments {a[9] / max(a[7], 1) * 10:.0f}, "
               f"routes {a[10] / max(a[7], 1) * 10:.0f}, sparse {a[11] / max(a[7], 1) * 10:.0f}), "
+              f"pricing parts per move (draw {a[12] / mv:.0f}, r1 {a[13] / mv:.0f}, r2 {a[14] / mv:.0f}, "
+              f"r3 {a[15] / mv:.0f}, compose {a[16] / mv:.0f}, full {a[17] / mv:.0f}), "
               f"accept rate {a[3] / st:.3f}, "
               f"exchange {a[4] / st * 10:.0f} ns, setup {a[5] / chains * 10 / 1e3:.1f} us, "
               f"kernel {a[6] / chains * 10 / 1e3:.1f} us/chain | best "

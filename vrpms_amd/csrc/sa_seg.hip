@@ -76,12 +76,14 @@ constexpr int kSegMaxWaves = 4;
 constexpr uint32_t kSegXBytes = 2 * kSegMaxWaves * sizeof(SegXSlot) + 32;
 
 // per-chain LDS: u32 [PE n+2 | PD n+2 | LG n+2 | dur rm+1 | dsp, pmx, smx rm+1
-// each | sparse (lv-1) x rm], then u16 [tok n+2 | SC n+2 | SP, RB, FNE, LNE1
-// segs+2]
-__host__ __device__ inline uint32_t seg_chain_bytes(int n, int segs, int rm, int lv) {
+// each | sparse (lv-1) x rm | (het) need, allow rm+1 each], then u16 [tok n+2 |
+// SC n+2 | SP, RB, FNE, LNE1 segs+2 | (het) BAD 4 x (rm+1) | cend K]
+__host__ __device__ inline uint32_t seg_chain_bytes(int n, int segs, int rm, int lv, bool het, int K) {
   const uint32_t np2 = ((uint32_t)n + 2u + 1u) & ~1u;
-  const uint32_t u32s = 3u * np2 + 4u * (uint32_t)(rm + 1) + (uint32_t)(lv - 1) * (uint32_t)rm;
-  const uint32_t u16s = 2u * np2 + 4u * (uint32_t)(segs + 2);
+  const uint32_t u32s = 3u * np2 + 4u * (uint32_t)(rm + 1) + (uint32_t)(lv - 1) * (uint32_t)rm +
+                        (het ? 2u * (uint32_t)(rm + 1) : 0u);
+  const uint32_t u16s = 2u * np2 + 4u * (uint32_t)(segs + 2) +
+                        (het ? 4u * (uint32_t)(rm + 1) + (uint32_t)K : 0u);
   return ((4u * u32s + 2u * u16s + 15u) & ~15u) + kSegXBytes;
 }
 
@@ -139,18 +141,27 @@ VRPMS_DEV uint32_t dpp_rscan_max(uint32_t v, uint32_t& total) {
 struct SegTabs {
   uint32_t *PE, *PD, *LG, *dur, *dsp, *pmx, *smx, *sp;  // LG[q] = leg of the token at q
   uint16_t *tok, *SC, *SP, *RB, *FNE, *LNE1;
+  // heterogeneous fleets: per route its load (need) and the largest capacity
+  // that splits it the same (allow); BAD[d][r] = routes < r that would split
+  // differently on vehicle r + delta(d), delta = -2, -1, 1, 2; cend[v] = the
+  // last vehicle of v's run of equal capacities (0xffff: the run reaches K - 1)
+  uint32_t *need, *allow;
+  uint16_t *BAD, *cend;
 };
 
 #ifdef VRPMS_SEG_PROF
 // per-chain counters (A/B builds only: tools/seg_prof.py): pricing ticks,
 // rebuild ticks, steps, accepts, cross-wavefront exchange ticks, setup ticks,
 // kernel ticks, rebuilds, then the rebuild's parts: positions, segments,
-// routes, sparse table (wall_clock64, 100 MHz)
-constexpr int kSegProf = 12;
+// routes, sparse table, then the pricing's (each closed by a wait for every
+// outstanding load, so only roughly the kernel's own schedule): draw and
+// junction tokens, round 1, round 2, round 3, composition, full
+// re-evaluation (wall_clock64, 100 MHz)
+constexpr int kSegProf = 18;
 __device__ unsigned long long g_seg_prof[kSegProf * 8192];
 #endif
 
-template <typename MatT>
+template <typename MatT, bool HET>  // HET: per-vehicle capacities
 __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 #ifdef VRPMS_SEG_PROF
@@ -176,6 +187,11 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
   if (chain >= a.chains) return;  // (W = 1) no block-wide barrier after this point
   const int n = a.n, K = a.si.K, RM = a.rm, LV = a.lv, SEGS = a.segs;
   const uint32_t cap = (uint32_t)I.sp.cap[0];
+  // route r runs on vehicle r (the last vehicle's capacity past the fleet:
+  // routes there serve no one, the fleet count rejects them)
+  auto capv = [&](int v) __attribute__((always_inline)) -> uint32_t {
+    return HET ? (uint32_t)I.sp.cap[v < 0 ? 0 : (v < K ? v : K - 1)] : cap;
+  };
   const int32_t* dem = I.sp.dem;
   const uint32_t Nm1 = N - 1;
   SegTabs T;
@@ -198,7 +214,38 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
     T.RB = T.SP + (SEGS + 2);
     T.FNE = T.RB + (SEGS + 2);
     T.LNE1 = T.FNE + (SEGS + 2);
+    T.need = T.allow = nullptr;
+    T.BAD = T.cend = nullptr;
+    if (HET) {
+      T.need = T.sp + (LV - 1) * RM;
+      T.allow = T.need + (RM + 1);
+      h = reinterpret_cast<uint16_t*>(T.allow + (RM + 1));
+      T.tok = h;
+      T.SC = h + np2;
+      T.SP = T.SC + np2;
+      T.RB = T.SP + (SEGS + 2);
+      T.FNE = T.RB + (SEGS + 2);
+      T.LNE1 = T.FNE + (SEGS + 2);
+      T.BAD = T.LNE1 + (SEGS + 2);
+      T.cend = T.BAD + 4 * (RM + 1);
+      for (int v = lane; v < K; v += 64) {
+        int u = v;
+        while (u < K - 1 && I.sp.cap[u + 1] == I.sp.cap[v]) ++u;
+        T.cend[v] = (uint16_t)(u >= K - 1 ? 0xffff : u);
+      }
+    }
   }
+  // vehicles v0..v1 share one capacity (v1 < v0: none)
+  auto one_class = [&](int v0, int v1) __attribute__((always_inline)) -> bool {
+    return v1 < v0 || (int)T.cend[v0 < K ? v0 : K - 1] >= v1;
+  };
+  // routes r0..r1-1 split the same on vehicles r + d, |d| <= 2 (d = 0: yes)
+  auto keeps = [&](int r0, int r1, int d) __attribute__((always_inline)) -> bool {
+    if (d == 0) return true;
+    if (d < -2 || d > 2) return false;
+    const uint16_t* b = T.BAD + (d < 0 ? d + 2 : d + 1) * (RM + 1);
+    return b[r1] == b[r0];
+  };
   SegXSlot* xs = reinterpret_cast<SegXSlot*>(smem + inst_lds_bytes(a.si) + ((N * 4u + 15u) & ~15u) +
                                              (uint32_t)slot * a.chain_bytes + a.chain_bytes -
                                              kSegXBytes);
@@ -229,6 +276,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
   unsigned long long pmark = 0;
 #define SEG_PT(k)                            \
   do {                                       \
+    __builtin_amdgcn_s_waitcnt(0);           \
     const unsigned long long nw = wall_clock64(); \
     pf[k] += nw - pmark;                     \
     pmark = nw;                              \
@@ -239,6 +287,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
   } while (0)
 #endif
   int reb_a = 0, reb_b = n;
+  bool rb_valid = false;  // T.RB holds a previous split (the heterogeneous pass starts from it)
   uint32_t pe_old = 0;
   auto rebuild = [&]() __attribute__((always_inline)) {
     wave_sync();
@@ -291,37 +340,69 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
     if (!seg_ok) return;
     // segments, one lane each: how many routes the greedy split makes of it
     // (binary-searched capacity cuts), the first route RB, the nearest
-    // non-empty segments at or before (LNE1, +1) / at or after (FNE)
-    uint32_t rcarry = 0, lcarry = 0;
+    // non-empty segments at or before (LNE1, +1) / at or after (FNE).  A
+    // heterogeneous fleet splits a segment on the vehicles from RB on, which
+    // depend on the segments before it: the pass repeats from the previous
+    // RB until no first route moves (a segment's count is then taken on its
+    // own vehicles), or else one lane walks the segments in order.
+    auto seg_routes = [&](int g, int vb) __attribute__((always_inline)) -> uint32_t {
+      const int s0 = SPX(g - 1) + 1, s1 = SPX(g) - 1;
+      uint32_t cnt = 1;
+      int x = s0, v = vb;
+      while (x <= s1 && T.PD[s1 + 1] - T.PD[x] > capv(v)) {  // cut: last q fitting from x
+        const uint32_t thr = T.PD[x] + capv(v);
+        int l = x, h = s1;  // first q in [x, s1] with PD[q + 1] > thr (exists)
+        while (l < h) {
+          const int md = (l + h) >> 1;
+          if (T.PD[md + 1] > thr) h = md; else l = md + 1;
+        }
+        ++cnt;
+        ++v;
+        x = l;
+      }
+      return cnt;
+    };
+    uint32_t rcarry = 0;
+    bool moved = true;
 #pragma unroll 1
-    for (int base = 0; base <= S; base += 64) {
-      const int g = base + lane;
-      uint32_t cnt = 0, ne = 0;
-      if (g <= S) {
-        const int s0 = SPX(g - 1) + 1, s1 = SPX(g) - 1;
-        ne = s1 >= s0 ? 1u : 0u;
-        cnt = 1;
-        int x = s0;
-        while (x <= s1 && T.PD[s1 + 1] - T.PD[x] > cap) {  // cut: last q fitting from x
-          const uint32_t thr = T.PD[x] + cap;
-          int l = x, h = s1;  // first q in [x, s1] with PD[q + 1] > thr (exists)
-          while (l < h) {
-            const int md = (l + h) >> 1;
-            if (T.PD[md + 1] > thr) h = md; else l = md + 1;
-          }
-          ++cnt;
-          x = l;
+    for (int it = 0; moved && it < (HET ? 6 : 1); ++it) {
+      rcarry = 0;
+      uint32_t lcarry = 0;
+      moved = false;
+#pragma unroll 1
+      for (int base = 0; base <= S; base += 64) {
+        const int g = base + lane;
+        uint32_t cnt = 0, ne = 0, guess = 0;
+        if (g <= S) {
+          const int s0 = SPX(g - 1) + 1, s1 = SPX(g) - 1;
+          ne = s1 >= s0 ? 1u : 0u;
+          guess = HET ? (!rb_valid && it == 0 ? (uint32_t)g : (uint32_t)T.RB[g]) : 0u;
+          cnt = seg_routes(g, (int)guess);
+        }
+        uint32_t tc, tl;
+        const uint32_t inc = dpp_scan<false>(cnt, tc);
+        const uint32_t lne = dpp_scan<true>(ne ? (uint32_t)g + 1u : 0u, tl);
+        const uint32_t rb = rcarry + inc - cnt;
+        if (HET && __ballot(g <= S && rb != guess) != 0ull) moved = true;
+        if (g <= S) {
+          T.RB[g] = (uint16_t)rb;
+          T.LNE1[g] = (uint16_t)max(lcarry, lne);
+        }
+        rcarry += tc;
+        lcarry = max(lcarry, tl);
+      }
+      wave_sync();
+    }
+    if (HET && moved) {  // not settled: one lane, segment by segment
+      if (lane == 0) {
+        uint32_t v = 0;
+        for (int g = 0; g <= S; ++g) {
+          T.RB[g] = (uint16_t)v;
+          v += seg_routes(g, (int)v);
         }
       }
-      uint32_t tc, tl;
-      const uint32_t inc = dpp_scan<false>(cnt, tc);
-      const uint32_t lne = dpp_scan<true>(ne ? (uint32_t)g + 1u : 0u, tl);
-      if (g <= S) {
-        T.RB[g] = (uint16_t)(rcarry + inc - cnt);
-        T.LNE1[g] = (uint16_t)max(lcarry, lne);
-      }
-      rcarry += tc;
-      lcarry = max(lcarry, tl);
+      wave_sync();
+      rcarry = (uint32_t)T.RB[S] + seg_routes(S, (int)T.RB[S]);
     }
     R = (int)rcarry;
     seg_ok = R <= RM;
@@ -343,26 +424,57 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
     if (lane == 0) T.RB[S + 1] = (uint16_t)R;
     wave_sync();
     SEG_PT(9);
-    // route durations, one lane per segment
+    // route durations (heterogeneous: loads and allowances), one lane per segment
 #pragma unroll 1
     for (int g = lane; g <= S; g += 64) {
       const int s0 = SPX(g - 1) + 1, s1 = SPX(g) - 1;
       int r = T.RB[g], x = s0;
-      while (x <= s1 && T.PD[s1 + 1] - T.PD[x] > cap) {
-        const uint32_t thr = T.PD[x] + cap;
+      while (x <= s1 && T.PD[s1 + 1] - T.PD[x] > capv(r)) {
+        const uint32_t thr = T.PD[x] + capv(r);
         int l = x, h = s1;
         while (l < h) {
           const int md = (l + h) >> 1;
           if (T.PD[md + 1] > thr) h = md; else l = md + 1;
+        }
+        if (HET) {  // cut before A[l]: this vehicle takes up to load + dem(A[l]) - 1
+          T.need[r] = T.PD[l] - T.PD[x];
+          T.allow[r] = T.PD[l + 1] - T.PD[x] - 1u;
         }
         // route: depot -> A[x..l-1] -> depot
         T.dur[r++] = leg[T.tok[x]] + T.PE[l] - T.PE[x + 1] + leg[T.tok[l - 1]];
         x = l;
       }
       // the last (or only) route: A[x..s1], closed by the separator (or the end)
+      if (HET) {
+        T.need[r] = x <= s1 ? T.PD[s1 + 1] - T.PD[x] : 0u;
+        T.allow[r] = 0xffffffffu;
+      }
       T.dur[r] = x <= s1 ? leg[T.tok[x]] + T.PE[s1 + 2] - T.PE[x + 1] : T.PE[s1 + 2] - T.PE[x];
     }
     wave_sync();
+    if (HET) {  // BAD[d]: routes that would split differently one or two vehicles on / back
+#pragma unroll 1
+      for (int d = 0; d < 4; ++d) {
+        const int dl = d < 2 ? d - 2 : d - 1;
+        uint16_t* b = T.BAD + d * (RM + 1);
+        uint32_t carry = 0;
+#pragma unroll 1
+        for (int base = 0; base < R; base += 64) {
+          const int r = base + lane;
+          uint32_t bad = 0;
+          if (r < R) {
+            const uint32_t c = capv(r + dl);
+            bad = (r + dl < 0 || T.need[r] > c || c > T.allow[r]) ? 1u : 0u;
+          }
+          uint32_t tb;
+          const uint32_t inc = dpp_scan<false>(bad, tb);
+          if (r < R) b[r + 1] = (uint16_t)(carry + inc);
+          carry += tb;
+        }
+        if (lane == 0) b[0] = 0;
+      }
+      wave_sync();
+    }
     // per-route prefix sums / maxima (dsp / pmx [r] over routes < r), suffix
     // maxima (smx [r] over routes >= r), sparse table of maxima
     uint32_t cds = 0, cmx = 0;
@@ -403,6 +515,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
       wave_sync();
     }
     SEG_PT(11);
+    rb_valid = true;
     const int l1 = T.LNE1[S];
     Tt = l1 ? S - (l1 - 1) : S;
   };
@@ -485,6 +598,9 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
 #pragma unroll 1
     for (int mi = 0; mi < a.M; ++mi) {
       const uint32_t idx = (uint32_t)(lane + 64 * (cw + W * mi));
+#ifdef VRPMS_SEG_PROF
+      pmark = wall_clock64();
+#endif
       const u32x4 r = philox((uint32_t)step, (uint32_t)(step >> 32), (uint32_t)chain, idx,
                              a.seed_lo, a.seed_hi);
       const Move m = decode_move_window(r.x, r.y, r.z, n, a.window, a.window_types);
@@ -528,6 +644,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
         X[2] = swp ? m.i : 1;
         Y[2] = swp ? m.i : 0;
         JV[2] = jx2;
+        SEG_PT(12);
         // round 1: separator counts
         const int s0 = T.SC[lo], sH = T.SC[hi + 1];
         const int lneS = T.LNE1[S];
@@ -539,6 +656,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
           SA[s] = live ? (int)T.SC[X[s]] : 0;
           SB[s] = live ? (int)T.SC[Y[s] + 1] : 0;
         }
+        SEG_PT(13);
         // round 2: separator positions, route indices
         const int stp = SPX(s0 - 1) + 1, en = SPX(sH);
         const int ra = T.RB[s0], rz = T.RB[sH + 1];  // sH = the last changed segment
@@ -555,6 +673,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
           R1[s] = mid ? (int)T.RB[SB[s]] : 0;
           GF[s] = mid ? (rev ? (int)T.FNE[SA[s] + 1] : (int)T.LNE1[SB[s] - 1] - 1) : 0;
         }
+        SEG_PT(14);
         // round 3: the runs' prefix sums and legs, the route tables
         struct RunP {
           int x, y;
@@ -591,6 +710,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
         }
         const uint32_t dspa = T.dsp[ra], dspz = T.dsp[rz], pmxa = T.pmx[ra], smxz = T.smx[rz];
 
+        SEG_PT(15);
         // the open route and what the composition has closed
         uint32_t c_dur = 0, c_load = 0, c_pl = 0, c_sum = 0, c_max = 0;  // c_pl: leg of its last customer
         bool c_has = false;
@@ -598,11 +718,13 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
         uint32_t isum = 0, imax = 0;
         int icnt = 0, seps = 0;
         bool cust = false;
+        int vo = ra;  // (heterogeneous) the open route's vehicle
         auto close = [&]() __attribute__((always_inline)) {
           const uint32_t d = c_dur + c_pl;
           c_sum += d;
           c_max = max(c_max, d);
           ++c_cnt;
+          ++vo;
           c_dur = c_load = c_pl = 0u;
           c_has = false;
         };
@@ -615,7 +737,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
           if (x > y) return;
           seps = 0;
           cust = true;
-          if (p.pdy - p.pdx <= cap - c_load) {  // fits: from the round-3 values
+          if (p.pdy - p.pdx <= capv(vo) - c_load) {  // fits: from the round-3 values
             c_dur += (c_has ? jv : (rev ? p.lgy : p.lgx)) + p.pey - p.pex;
             c_load += p.pdy - p.pdx;
             c_pl = rev ? p.lgx : p.lgy;
@@ -623,7 +745,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
             return;
           }
           while (true) {
-            const uint32_t room = cap - c_load;
+            const uint32_t room = capv(vo) - c_load;
             const bool fits = T.PD[y + 1] - T.PD[x] <= room;
             int pa = x, pb = y;
             if (!fits) {
@@ -662,10 +784,21 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
             if (SB[s] - SA[s] >= 2) {
               const int g0 = SA[s] + 1, g1 = SB[s] - 1;
               const int r0 = R0[s], r1 = R1[s];
-              if (rev && r1 - r0 != g1 - g0 + 1) {
-                // reversed and split by capacity: a reversal splits differently, walk them
-                for (int g = g1; g >= g0; --g) {
-                  run(pre(SPX(g - 1) + 1, SPX(g) - 1), true, 0u);
+              // a reversal splits a segment of several routes differently;
+              // (heterogeneous) forward they keep their splits when every
+              // route does on the vehicles it moves to, reversed (which hands
+              // them to the vehicles in reverse) when one capacity serves them
+              // before and after
+              bool tabled = !rev || r1 - r0 == g1 - g0 + 1;
+              if (HET && tabled) {
+                tabled = rev ? one_class(r0, r1 - 1) && one_class(vo, vo + r1 - r0 - 1) &&
+                                   capv(vo) == capv(r0)
+                             : keeps(r0, r1, vo - r0);
+              }
+              if (!tabled) {  // walk them
+                for (int t = 0; t <= g1 - g0; ++t) {
+                  const int g = rev ? g1 - t : g0 + t;
+                  run(pre(SPX(g - 1) + 1, SPX(g) - 1), rev, 0u);
                   close();
                   ++seps;
                 }
@@ -673,6 +806,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
                 isum += ISUM[s];
                 imax = max(imax, IMAX[s]);
                 icnt += r1 - r0;
+                vo += r1 - r0;
                 // the last customer in the moved order and the separators after it
                 const int gf = GF[s];
                 const bool has = rev ? gf <= g1 : gf >= g0;
@@ -697,7 +831,9 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
         int Tb = Tt;
         const bool tail_kept = en < n && lneS - 1 > sH;
         if (!tail_kept && cust) Tb = seps + (en < n ? n - 1 - en : 0);
-        if (Rb - Tb <= K) {
+        if (HET && !keeps(rz, R, Rb - R)) {
+          full = true;  // the tail's routes move to vehicles that split them differently
+        } else if (Rb - Tb <= K) {
           const uint32_t dsum = dspa + c_sum + isum + dspR - dspz;
           const uint32_t dmax = max(max(pmxa, smxz), max(imax, c_max));
           k = cvrp_key(0, dsum, dmax, I.sp.objective);
@@ -707,10 +843,12 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
           full = true;
         }
       }
+      SEG_PT(16);
       if (full) {
         auto moved = [&](int q) { return tourA(map_src(mmap, q)); };
         k = eval_tour<true>(I.D, I.sp, moved, n).key;
       }
+      SEG_PT(17);
       if (k < bkey) {  // ties keep the earlier (smaller) move index
         bkey = k;
         bidx = idx;
@@ -845,17 +983,20 @@ int launch_sa_seg(const vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* d_cu
                   uint64_t* d_cur_key, uint16_t* d_best, uint64_t* d_best_key, int n,
                   uint32_t wtypes, int moves, hipStream_t s) {
   const Instance& in = ctx->inst;
-  if (in.problem != VRPMS_CVRP || in.H != 1 || !in.symmetric || !in.uniform_cap ||
-      in.max_dem > in.cap0 || n < 2 || n >= 64 * kSegRegs || n > 65535 || moves % 64 != 0 ||
+  // every demand fits the smallest vehicle; per-vehicle capacities take the
+  // heterogeneous variant
+  if (in.problem != VRPMS_CVRP || in.H != 1 || !in.symmetric || in.max_dem > in.min_cap ||
+      in.K > 65535 || n < 2 || n >= 64 * kSegRegs || n > 65535 || moves % 64 != 0 ||
       moves / 64 > kSegMaxMoves)
     return 1;
+  const bool het = !in.uniform_cap;
   SearchInst si = search_inst(ctx);
   si.mat_lds = 0;  // the matrix stays in L2: a move gathers <= 4 entries
   // separators: a tour of the N - 1 customers and n - (N - 1) separators
   const int segs = std::max(8, ((std::max(0, n - (in.N - 1)) + 2 + 7) & ~7));
   const int rm = std::max(2 * in.K + 2, segs + 2) + 8;
   const int lv = seg_levels(rm);
-  const uint32_t cb = seg_chain_bytes(n, segs, rm, lv);
+  const uint32_t cb = seg_chain_bytes(n, segs, rm, lv, het, in.K);
   const size_t base = inst_lds_bytes_host(si) + (((size_t)in.N * 4u + 15u) & ~(size_t)15u);
   // wavefronts per chain: W > 1 prices the step's moves on W SIMDs at once
   // (same moves, same winner, so the same trajectories as W = 1), while the
@@ -880,8 +1021,13 @@ int launch_sa_seg(const vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* d_cu
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     kern<<<dim3((p->chains + cpw - 1) / cpw), dim3(64 * cpw * W), lds, s>>>(a);
   };
-  if (in.use16) go(sa_seg_kernel<uint16_t>);
-  else go(sa_seg_kernel<int32_t>);
+  if (het) {
+    if (in.use16) go(sa_seg_kernel<uint16_t, true>);
+    else go(sa_seg_kernel<int32_t, true>);
+  } else {
+    if (in.use16) go(sa_seg_kernel<uint16_t, false>);
+    else go(sa_seg_kernel<int32_t, false>);
+  }
   VRPMS_HIP(hipGetLastError());
   return VRPMS_OK;
 }
