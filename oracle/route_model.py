@@ -199,8 +199,10 @@ def _moved(A, m):
 # <= allow[r] (need = its load; allow = load + the demand of the customer
 # that did not fit - 1 when a capacity cut closed it, else unbounded), so
 # whole segments are still priced from the tables when that holds for all
-# their routes, and walked otherwise; an unchanged tail that fails it is
-# re-evaluated in full.
+# their routes, and walked otherwise.  The unchanged tail after the move is
+# priced from the tables up to its first route that fails, whose segment is
+# walked on its new vehicles; delta then changes by that segment's change of
+# route count and the tail continues (FULL: |delta| > 2, re-evaluate).
 # ---------------------------------------------------------------------------
 INF = 1 << 62
 FULL = "full"
@@ -277,7 +279,14 @@ class SegTables:
 
     def keeps(self, r0, r1, delta):
         """Routes r0..r1-1 split the same on vehicles r + delta."""
-        return all(self.need[r] <= self.cap_of(r + delta) <= self.allow[r] for r in range(r0, r1))
+        return all(self.route_keeps(r, delta) for r in range(r0, r1))
+
+    def route_keeps(self, r, delta):
+        return r + delta >= 0 and self.need[r] <= self.cap_of(r + delta) <= self.allow[r]
+
+    def seg_of_route(self, r):
+        """The segment holding route r (last s with RB[s] <= r)."""
+        return max(s for s in range(self.S + 1) if self.RB[s] <= r)
 
     def one_class(self, v0, v1):
         """Vehicles v0..v1 all have the same capacity (v1 < v0: none)."""
@@ -352,7 +361,7 @@ def run(T, acc, a, b, rev):
 def price_seg(T: SegTables, m, K: int, objective: int = 0):
     """Key of T.A moved by m; None when the moved tour leaves a customer
     unserved (R - T > K); FULL when (heterogeneous fleet) the tail after the
-    changed segments moves to vehicles that split it differently."""
+    changed segments moves by more than two vehicles."""
     typ, i, j = m
     A, SC = T.A, T.SC
     n = T.n
@@ -443,19 +452,40 @@ def price_seg(T: SegTables, m, K: int, objective: int = 0):
         close_route(T, acc)
     g_last = SC[en] if en < n else T.S   # last segment of the region
     ra, rz = T.RB[s0], T.RB[g_last + 1]  # current routes the region replaces
-    R = T.R - (rz - ra) + len(acc.routes) + inner["cnt"]
+    # the tail: routes rz.. of the current tour on vehicles shifted by delta
+    tail = []                            # its route durations in the moved tour
+    r, delta = rz, acc.v - rz            # (r: always the first route of a segment)
+    while r < T.R:
+        if delta < -2 or delta > 2:
+            return FULL
+        if delta == 0:
+            tail += T.dur[r:]
+            break
+        rb = r
+        while rb < T.R and T.route_keeps(rb, delta):
+            rb += 1
+        if rb == T.R:
+            tail += T.dur[r:]
+            break
+        g = T.seg_of_route(rb)           # walk the segment holding the first that fails
+        tail += T.dur[r:T.RB[g]]
+        w = Acc(v=T.RB[g] + delta)
+        run(T, w, T.spx(g - 1) + 1, T.spx(g) - 1, False)
+        close_route(T, w)
+        tail += w.routes
+        delta += len(w.routes) - (T.RB[g + 1] - T.RB[g])
+        r = T.RB[g + 1]
+    R = ra + len(acc.routes) + inner["cnt"] + len(tail)
     if en < n and T.PC[n - 1] > en:     # the tail after the region keeps the last customer
         Tb = T.T
     elif tr["cust"]:
         Tb = tr["seps"] + (n - 1 - en if en < n else 0)
     else:
         Tb = T.T
-    if R != T.R and not T.keeps(rz, T.R, R - T.R):
-        return FULL                      # the tail's routes move to vehicles that split them differently
     if R - Tb > K:
         return None
-    dsum = T.dsp[ra] + sum(acc.routes) + inner["sum"] + T.dsp[T.R] - T.dsp[rz]
-    dmax = max([T.pmx[ra], T.smx[rz], inner["max"]] + acc.routes)
+    dsum = T.dsp[ra] + sum(acc.routes) + inner["sum"] + sum(tail)
+    dmax = max([T.pmx[ra], inner["max"]] + acc.routes + tail)
     if objective == spec.OBJ_SUM:
         return spec.pack_key(0, dsum, dmax)
     return spec.pack_key(0, dmax, dsum)

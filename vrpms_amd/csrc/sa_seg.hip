@@ -827,15 +827,68 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
         run(p_tail, false, jx3);
         close();
         if (en < n) ++seps;
-        const int Rb = R - (rz - ra) + c_cnt + icnt;
+        // the unchanged tail: routes rz.. of the current tour.  A
+        // heterogeneous fleet hands them to vehicles shifted by delta: routes
+        // that keep their splits there come from the tables, the segment of
+        // the first that does not is walked on its new vehicles, and delta
+        // moves by that segment's change of route count
+        uint32_t tsum = dspR - dspz, tmax = smxz;
+        int tcnt = R - rz;
+        if (HET) {
+          tsum = tmax = 0u;
+          tcnt = 0;
+          int r = rz, g = sH + 1, delta = vo - rz;
+          const int seps0 = seps;
+          const bool cust0 = cust;
+          while (r < R) {
+            if (delta < -2 || delta > 2) {
+              full = true;
+              break;
+            }
+            const uint16_t* b = T.BAD + (delta < 0 ? delta + 2 : delta + 1) * (RM + 1);
+            const uint32_t b0 = delta ? b[r] : 0u;
+            if (delta == 0 || b[R] == b0) {
+              tsum += dspR - T.dsp[r];
+              tmax = max(tmax, T.smx[r]);
+              tcnt += R - r;
+              break;
+            }
+            int l = r, h = R - 1;  // the first route that splits differently
+            while (l < h) {
+              const int md = (l + h) >> 1;
+              if (b[md + 1] != b0) h = md; else l = md + 1;
+            }
+            int gl = g, gh = S;  // its segment: the last one starting at or before it
+            while (gl < gh) {
+              const int md = (gl + gh + 1) >> 1;
+              if ((int)T.RB[md] <= l) gl = md; else gh = md - 1;
+            }
+            const int rs = T.RB[gl], re = T.RB[gl + 1];
+            if (rs > r) {
+              tsum += T.dsp[rs] - T.dsp[r];
+              tmax = max(tmax, rmaxq(r, rs - 1));
+              tcnt += rs - r;
+            }
+            const int c0 = c_cnt;
+            vo = rs + delta;
+            run(pre(SPX(gl - 1) + 1, SPX(gl) - 1), false, 0u);
+            close();
+            delta += (c_cnt - c0) - (re - rs);
+            r = re;
+            g = gl + 1;
+          }
+          seps = seps0;
+          cust = cust0;
+        }
+        const int Rb = ra + c_cnt + icnt + tcnt;
         int Tb = Tt;
         const bool tail_kept = en < n && lneS - 1 > sH;
         if (!tail_kept && cust) Tb = seps + (en < n ? n - 1 - en : 0);
-        if (HET && !keeps(rz, R, Rb - R)) {
-          full = true;  // the tail's routes move to vehicles that split them differently
+        if (full) {
+          // (heterogeneous) the tail moved by more than two vehicles
         } else if (Rb - Tb <= K) {
-          const uint32_t dsum = dspa + c_sum + isum + dspR - dspz;
-          const uint32_t dmax = max(max(pmxa, smxz), max(imax, c_max));
+          const uint32_t dsum = dspa + c_sum + isum + tsum;
+          const uint32_t dmax = max(max(pmxa, tmax), max(imax, c_max));
           k = cvrp_key(0, dsum, dmax, I.sp.objective);
         } else if (shortcut) {
           k = ~0ull;
