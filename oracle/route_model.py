@@ -202,10 +202,11 @@ def _moved(A, m):
 # their routes, and walked otherwise.  The unchanged tail after the move is
 # priced from the tables up to its first route that fails, whose segment is
 # walked on its new vehicles; delta then changes by that segment's change of
-# route count and the tail continues (FULL: |delta| > 2, re-evaluate).
+# route count and the tail continues (FULL: |delta| > SHIFT, re-evaluate).
 # ---------------------------------------------------------------------------
 INF = 1 << 62
 FULL = "full"
+SHIFT = 6        # the kernel's shift tables: |delta| <= 6 (kSegShift)
 
 
 class SegTables:
@@ -361,7 +362,7 @@ def run(T, acc, a, b, rev):
 def price_seg(T: SegTables, m, K: int, objective: int = 0):
     """Key of T.A moved by m; None when the moved tour leaves a customer
     unserved (R - T > K); FULL when (heterogeneous fleet) the tail after the
-    changed segments moves by more than two vehicles."""
+    changed segments moves by more than SHIFT vehicles."""
     typ, i, j = m
     A, SC = T.A, T.SC
     n = T.n
@@ -456,7 +457,7 @@ def price_seg(T: SegTables, m, K: int, objective: int = 0):
     tail = []                            # its route durations in the moved tour
     r, delta = rz, acc.v - rz            # (r: always the first route of a segment)
     while r < T.R:
-        if delta < -2 or delta > 2:
+        if delta < -SHIFT or delta > SHIFT:
             return FULL
         if delta == 0:
             tail += T.dur[r:]

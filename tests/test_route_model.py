@@ -99,8 +99,8 @@ def test_segment_pricing_matches_full_evaluation(nn, slack, obj, window, sep):
 def test_segment_pricing_heterogeneous_fleet(nn, classes, shuffle, window, obj):
     """Segment pricing with per-vehicle capacities (route r on vehicle r):
     keys equal eval_cvrp, None exactly when a customer is unserved, FULL
-    (re-evaluate) only when the unchanged tail moves by more than two
-    vehicles; tail routes that would split differently on their new vehicles
+    (re-evaluate) only when the unchanged tail moves by more than
+    route_model.SHIFT vehicles; tail routes that would split differently on their new vehicles
     are walked -- capacity classes in vehicle order and shuffled, on
     first-fit and random separator placements."""
     rng = np.random.default_rng(nn * 7 + len(classes))

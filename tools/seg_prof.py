@@ -5,7 +5,8 @@ rebuild) time (wall_clock64 ticks of lane 0, 100 MHz), the accept rate and
 the cross-wavefront exchange (W > 1, VRPMS_SEG_WAVES) -- on X-1000 first-fit start tours at a hot
 and a cold fixed temperature.
 
-usage: tools/seg_prof.py build   (CPU: compile the variant)
+usage: tools/seg_prof.py build   (CPU: compile the variant; SEG_PROF_HET=1: three
+                                 capacity classes)
        tools/seg_prof.py [chains] [moves]   (GPU)"""
 import ctypes
 import os
@@ -39,7 +40,12 @@ def run(chains, moves):
     lib.vrpms_debug_seg_prof.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     ctx = Context(0)
     x = synth.x_style(1000, seed=0)
-    ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
+    caps = x.capacities
+    if os.environ.get("SEG_PROF_HET"):  # three capacity classes (tools/het_rate.py)
+        K, base = len(caps), int(caps[0])
+        caps = np.array([max(int(base * (1.4, 1.1, 0.9)[k * 3 // K]), int(x.demand.max()))
+                         for k in range(K)])
+    ctx.set_instance(CVRP, x.durations, x.demand, caps, x.start_times)
     edge = runners.typical_edge(x.durations)
     NP = 18
     buf = (ctypes.c_ulonglong * (NP * 8192))()

@@ -42,6 +42,7 @@ namespace vrpms {
 
 constexpr int kSegRegs = 20;      // positions per lane in registers on an accept: n < 64 * 20
 constexpr int kSegMaxMoves = 8;   // moves per lane per step (64 M per step)
+constexpr int kSegShift = 6;      // heterogeneous fleets: vehicle shifts |delta| <= 6 from tables
 
 struct SegArgs {
   SearchInst si;
@@ -77,13 +78,14 @@ constexpr uint32_t kSegXBytes = 2 * kSegMaxWaves * sizeof(SegXSlot) + 32;
 
 // per-chain LDS: u32 [PE n+2 | PD n+2 | LG n+2 | dur rm+1 | dsp, pmx, smx rm+1
 // each | sparse (lv-1) x rm | (het) need, allow rm+1 each], then u16 [tok n+2 |
-// SC n+2 | SP, RB, FNE, LNE1 segs+2 | (het) BAD 4 x (rm+1) | cend K]
+// SC n+2 | SP, RB, FNE, LNE1 segs+2 | (het) NB 2 kSegShift x (rm+1) | SEGR rm+1 |
+// cend K]
 __host__ __device__ inline uint32_t seg_chain_bytes(int n, int segs, int rm, int lv, bool het, int K) {
   const uint32_t np2 = ((uint32_t)n + 2u + 1u) & ~1u;
   const uint32_t u32s = 3u * np2 + 4u * (uint32_t)(rm + 1) + (uint32_t)(lv - 1) * (uint32_t)rm +
                         (het ? 2u * (uint32_t)(rm + 1) : 0u);
   const uint32_t u16s = 2u * np2 + 4u * (uint32_t)(segs + 2) +
-                        (het ? 4u * (uint32_t)(rm + 1) + (uint32_t)K : 0u);
+                        (het ? (2u * kSegShift + 1u) * (uint32_t)(rm + 1) + (uint32_t)K : 0u);
   return ((4u * u32s + 2u * u16s + 15u) & ~15u) + kSegXBytes;
 }
 
@@ -142,11 +144,13 @@ struct SegTabs {
   uint32_t *PE, *PD, *LG, *dur, *dsp, *pmx, *smx, *sp;  // LG[q] = leg of the token at q
   uint16_t *tok, *SC, *SP, *RB, *FNE, *LNE1;
   // heterogeneous fleets: per route its load (need) and the largest capacity
-  // that splits it the same (allow); BAD[d][r] = routes < r that would split
-  // differently on vehicle r + delta(d), delta = -2, -1, 1, 2; cend[v] = the
-  // last vehicle of v's run of equal capacities (0xffff: the run reaches K - 1)
+  // that splits it the same (allow); NB[d][r] = the first route >= r that
+  // would split differently on vehicle r + delta(d) (R: none), delta =
+  // -kSegShift..-1, 1..kSegShift; SEGR[r] = the segment of route r; cend[v] =
+  // the last vehicle of v's run of equal capacities (0xffff: the run reaches
+  // K - 1)
   uint32_t *need, *allow;
-  uint16_t *BAD, *cend;
+  uint16_t *NB, *SEGR, *cend;
 };
 
 #ifdef VRPMS_SEG_PROF
@@ -215,7 +219,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
     T.FNE = T.RB + (SEGS + 2);
     T.LNE1 = T.FNE + (SEGS + 2);
     T.need = T.allow = nullptr;
-    T.BAD = T.cend = nullptr;
+    T.NB = T.SEGR = T.cend = nullptr;
     if (HET) {
       T.need = T.sp + (LV - 1) * RM;
       T.allow = T.need + (RM + 1);
@@ -226,8 +230,9 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
       T.RB = T.SP + (SEGS + 2);
       T.FNE = T.RB + (SEGS + 2);
       T.LNE1 = T.FNE + (SEGS + 2);
-      T.BAD = T.LNE1 + (SEGS + 2);
-      T.cend = T.BAD + 4 * (RM + 1);
+      T.NB = T.LNE1 + (SEGS + 2);
+      T.SEGR = T.NB + 2 * kSegShift * (RM + 1);
+      T.cend = T.SEGR + (RM + 1);
       for (int v = lane; v < K; v += 64) {
         int u = v;
         while (u < K - 1 && I.sp.cap[u + 1] == I.sp.cap[v]) ++u;
@@ -239,12 +244,15 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
   auto one_class = [&](int v0, int v1) __attribute__((always_inline)) -> bool {
     return v1 < v0 || (int)T.cend[v0 < K ? v0 : K - 1] >= v1;
   };
-  // routes r0..r1-1 split the same on vehicles r + d, |d| <= 2 (d = 0: yes)
+  // the NB row of shift d (0 < |d| <= kSegShift)
+  auto nb_row = [&](int d) __attribute__((always_inline)) -> const uint16_t* {
+    return T.NB + (d < 0 ? d + kSegShift : d + kSegShift - 1) * (RM + 1);
+  };
+  // routes r0..r1-1 split the same on vehicles r + d, |d| <= kSegShift (d = 0: yes)
   auto keeps = [&](int r0, int r1, int d) __attribute__((always_inline)) -> bool {
-    if (d == 0) return true;
-    if (d < -2 || d > 2) return false;
-    const uint16_t* b = T.BAD + (d < 0 ? d + 2 : d + 1) * (RM + 1);
-    return b[r1] == b[r0];
+    if (d == 0 || r0 >= r1) return true;
+    if (d < -kSegShift || d > kSegShift) return false;
+    return (int)nb_row(d)[r0] >= r1;
   };
   SegXSlot* xs = reinterpret_cast<SegXSlot*>(smem + inst_lds_bytes(a.si) + ((N * 4u + 15u) & ~15u) +
                                              (uint32_t)slot * a.chain_bytes + a.chain_bytes -
@@ -439,6 +447,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
         if (HET) {  // cut before A[l]: this vehicle takes up to load + dem(A[l]) - 1
           T.need[r] = T.PD[l] - T.PD[x];
           T.allow[r] = T.PD[l + 1] - T.PD[x] - 1u;
+          T.SEGR[r] = (uint16_t)g;
         }
         // route: depot -> A[x..l-1] -> depot
         T.dur[r++] = leg[T.tok[x]] + T.PE[l] - T.PE[x + 1] + leg[T.tok[l - 1]];
@@ -448,30 +457,30 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
       if (HET) {
         T.need[r] = x <= s1 ? T.PD[s1 + 1] - T.PD[x] : 0u;
         T.allow[r] = 0xffffffffu;
+        T.SEGR[r] = (uint16_t)g;
       }
       T.dur[r] = x <= s1 ? leg[T.tok[x]] + T.PE[s1 + 2] - T.PE[x + 1] : T.PE[s1 + 2] - T.PE[x];
     }
     wave_sync();
-    if (HET) {  // BAD[d]: routes that would split differently one or two vehicles on / back
+    if (HET) {  // NB[d]: the next route that would split differently 1..kSegShift vehicles on / back
 #pragma unroll 1
-      for (int d = 0; d < 4; ++d) {
-        const int dl = d < 2 ? d - 2 : d - 1;
-        uint16_t* b = T.BAD + d * (RM + 1);
-        uint32_t carry = 0;
+      for (int d = 0; d < 2 * kSegShift; ++d) {
+        const int dl = d < kSegShift ? d - kSegShift : d - kSegShift + 1;
+        uint16_t* b = T.NB + d * (RM + 1);
+        uint32_t carry = 0;  // suffix maximum of 0xffff - r over the routes r that fail
 #pragma unroll 1
-        for (int base = 0; base < R; base += 64) {
-          const int r = base + lane;
-          uint32_t bad = 0;
+        for (int top = (R / 64) * 64; top >= 0; top -= 64) {
+          const int r = top + lane;
+          uint32_t v = 0;
           if (r < R) {
             const uint32_t c = capv(r + dl);
-            bad = (r + dl < 0 || T.need[r] > c || c > T.allow[r]) ? 1u : 0u;
+            v = (r + dl < 0 || T.need[r] > c || c > T.allow[r]) ? 0xffffu - (uint32_t)r : 0u;
           }
-          uint32_t tb;
-          const uint32_t inc = dpp_scan<false>(bad, tb);
-          if (r < R) b[r + 1] = (uint16_t)(carry + inc);
-          carry += tb;
+          uint32_t tm;
+          const uint32_t m = max(dpp_rscan_max(v, tm), carry);
+          if (r <= R) b[r] = (uint16_t)(m ? 0xffffu - m : (uint32_t)R);
+          carry = max(carry, tm);
         }
-        if (lane == 0) b[0] = 0;
       }
       wave_sync();
     }
@@ -837,32 +846,22 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
         if (HET) {
           tsum = tmax = 0u;
           tcnt = 0;
-          int r = rz, g = sH + 1, delta = vo - rz;
+          int r = rz, delta = vo - rz;
           const int seps0 = seps;
           const bool cust0 = cust;
           while (r < R) {
-            if (delta < -2 || delta > 2) {
+            if (delta < -kSegShift || delta > kSegShift) {
               full = true;
               break;
             }
-            const uint16_t* b = T.BAD + (delta < 0 ? delta + 2 : delta + 1) * (RM + 1);
-            const uint32_t b0 = delta ? b[r] : 0u;
-            if (delta == 0 || b[R] == b0) {
+            const int l = delta ? (int)nb_row(delta)[r] : R;  // the first route that splits differently
+            if (l >= R) {
               tsum += dspR - T.dsp[r];
               tmax = max(tmax, T.smx[r]);
               tcnt += R - r;
               break;
             }
-            int l = r, h = R - 1;  // the first route that splits differently
-            while (l < h) {
-              const int md = (l + h) >> 1;
-              if (b[md + 1] != b0) h = md; else l = md + 1;
-            }
-            int gl = g, gh = S;  // its segment: the last one starting at or before it
-            while (gl < gh) {
-              const int md = (gl + gh + 1) >> 1;
-              if ((int)T.RB[md] <= l) gl = md; else gh = md - 1;
-            }
+            const int gl = T.SEGR[l];  // walk its segment
             const int rs = T.RB[gl], re = T.RB[gl + 1];
             if (rs > r) {
               tsum += T.dsp[rs] - T.dsp[r];
@@ -875,7 +874,6 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
             close();
             delta += (c_cnt - c0) - (re - rs);
             r = re;
-            g = gl + 1;
           }
           seps = seps0;
           cust = cust0;
@@ -885,7 +883,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
         const bool tail_kept = en < n && lneS - 1 > sH;
         if (!tail_kept && cust) Tb = seps + (en < n ? n - 1 - en : 0);
         if (full) {
-          // (heterogeneous) the tail moved by more than two vehicles
+          // (heterogeneous) the tail moved by more than kSegShift vehicles
         } else if (Rb - Tb <= K) {
           const uint32_t dsum = dspa + c_sum + isum + tsum;
           const uint32_t dmax = max(max(pmxa, tmax), max(imax, c_max));
