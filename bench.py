@@ -60,6 +60,9 @@ def parse():
                     help="SA steps per island epoch (40 x 500 ~ 1 s of wall time)")
     ap.add_argument("--quality-seconds", type=float, default=5.0,
                     help="wall time per side for the best-cost gap (0 disables)")
+    ap.add_argument("--x1000-quality-seconds", type=float, default=10.0,
+                    help="wall time per side for the cfg-4 X-1000 best-cost gap (seed 0; the "
+                         "host leg at 32 and at 64 moves per step, the better kept; 0 disables)")
     return ap.parse_args()
 
 
@@ -265,6 +268,30 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
             out["gap"] = (g["duration_sum"] - c["duration_sum"]) / c["duration_sum"] if ok else None
             out["gap_sign"] = "negative = GPU better"
     return out
+
+
+def x1000_quality(ctx, seconds, dist, with_cpu):
+    """The metric's second half on cfg 4 (X-style CVRP-1000, seed 0): the
+    GPU leg (sa_seg_kernel, 256 chains x 128 moves per step, W = 2
+    wavefronts per chain) against the host port (oracle_sa_run_resync with
+    its C segment pricing seg_key, one chain per thread) at 32 and at 64
+    moves per step, the better host result kept -- the cells of
+    tools/quality_sweep.py --instance x1000."""
+    from vrpms_amd import synth
+    from vrpms_amd.core import CVRP
+    x = synth.x_style(1000, seed=0)
+    ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
+    kw = dict(chains=256, moves=128, label="x1000 seed 0", window=32, window_types=2,
+              start="pack")
+    q = quality(ctx, x, seconds, 1, 0, dist, with_cpu=with_cpu, cpu_moves=32, **kw)
+    if with_cpu:
+        q2 = quality(ctx, x, seconds, 1, 0, dist, with_cpu=True, cpu_moves=64, gpu=False, **kw)
+        q["cpu_alternatives"] = [q2["cpu"]]
+        if q2["cpu"]["unvisited"] == 0 and q2["cpu"]["duration_sum"] < q["cpu"]["duration_sum"]:
+            q["cpu_alternatives"] = [q["cpu"]]
+            q["cpu"] = q2["cpu"]
+            q["gap"] = (q["gpu"]["duration_sum"] - q["cpu"]["duration_sum"]) / q["cpu"]["duration_sum"]
+    return q
 
 
 def other_configs(ctx, torch, dev, seed=0, r_lds=None):
@@ -673,6 +700,14 @@ def main():
         except Exception:
             qual = {"error": traceback.format_exc(limit=3)}
 
+    xq = None
+    if args.x1000_quality_seconds > 0 and world == 1:
+        try:
+            xq = x1000_quality(ctx, args.x1000_quality_seconds, dist,
+                               with_cpu=(rank == 0 and not args.no_cpu_baseline))
+        except Exception:
+            xq = {"error": traceback.format_exc(limit=3)}
+
     isl = None
     if args.island_epochs > 0:
         # after every other device use of the matrix instance: it loads its own
@@ -733,6 +768,8 @@ def main():
         out["rows_vs_words_identical"] = same
         if qual is not None:
             out["quality"] = qual
+        if xq is not None:
+            out["quality_x1000"] = xq
         if isl is not None:
             out["islands"] = isl
         if world == 1 and not args.no_cpu_baseline:
