@@ -233,10 +233,17 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
       T.NB = T.LNE1 + (SEGS + 2);
       T.SEGR = T.NB + 2 * kSegShift * (RM + 1);
       T.cend = T.SEGR + (RM + 1);
-      for (int v = lane; v < K; v += 64) {
-        int u = v;
-        while (u < K - 1 && I.sp.cap[u + 1] == I.sp.cap[v]) ++u;
-        T.cend[v] = (uint16_t)(u >= K - 1 ? 0xffff : u);
+      // cend[v] = the first u >= v whose successor's capacity differs: a
+      // suffix maximum of 0xffff - u over those u, 64 vehicles at a time
+      uint32_t carry = 0;
+      for (int top = ((K - 1) / 64) * 64; top >= 0; top -= 64) {
+        const int v = top + lane;
+        const uint32_t x =
+            (v < K - 1 && I.sp.cap[v + 1] != I.sp.cap[v]) ? 0xffffu - (uint32_t)v : 0u;
+        uint32_t tm;
+        const uint32_t m = max(dpp_rscan_max(x, tm), carry);
+        if (v < K) T.cend[v] = (uint16_t)(m ? 0xffffu - m : 0xffffu);
+        carry = max(carry, tm);
       }
     }
   }
@@ -753,30 +760,77 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
             c_has = true;
             return;
           }
+          // the prefix demands at the run's ends ride along: PD[x] / PD[y + 1]
+          // are known from round 3 and, after a cut, from the appended part
+          uint32_t pdx = p.pdx, pdy = p.pdy;
           while (true) {
             const uint32_t room = capv(vo) - c_load;
-            const bool fits = T.PD[y + 1] - T.PD[x] <= room;
+            const bool fits = pdy - pdx <= room;
             int pa = x, pb = y;
             if (!fits) {
-              // first q in [x - 1, y + 1] with PD[q + 1] > thr, on the monotone PD
-              const int thr = rev ? (int)(T.PD[y + 1] - room) - 1 : (int)(T.PD[x] + room);
-              int l = x - 1, h = y + 1;
+              // first q in [x - 1, y + 1] with PD[q + 1] > thr, on the monotone
+              // PD (one customer: it does not fit, q = x)
+              const int thr = rev ? (int)(pdy - room) - 1 : (int)(pdx + room);
+              int l = x, h = x;
+              if (x < y) {
+                l = x - 1;
+                h = y + 1;
+              }
               while (l < h) {
                 const int md = (l + h) >> 1;
                 if ((int)T.PD[md + 1] > thr) h = md; else l = md + 1;
               }
               if (rev) pa = l + 1; else pb = l - 1;
             }
+            uint32_t pda = pdx, pdb = pdy;  // PD[pa], PD[pb + 1]
             if (pa <= pb) {
+              if (!fits) {
+                pda = rev ? T.PD[pa] : pdx;
+                pdb = rev ? pdy : T.PD[pb + 1];
+              }
               c_dur += (c_has ? jv : T.LG[rev ? pb : pa]) + T.PE[pb + 1] - T.PE[pa + 1];
-              c_load += T.PD[pb + 1] - T.PD[pa];
+              c_load += pdb - pda;
               c_pl = T.LG[rev ? pa : pb];
               c_has = true;
             }
             if (fits) break;
             close();
-            if (rev) y = pa - 1; else x = pb + 1;
+            // (nothing appended: x / y stay, and so do their prefix demands)
+            if (rev) {
+              y = pa - 1;
+              if (pa <= pb) pdy = pda;  // PD[y + 1] = PD[pa]
+            } else {
+              x = pb + 1;
+              if (pa <= pb) pdx = pdb;  // PD[x] = PD[pb + 1]
+            }
           }
+        };
+        // (heterogeneous) routes r..rend-1 of the current tour, the first on
+        // vehicle vo: every route keeps its split on vehicle r + delta (delta =
+        // vo - r) up to the first that does not (NB), whose segment is walked
+        // on its new vehicles, delta then moving by its change of route count;
+        // tabled routes add to (xs, xm, xc), walked ones close into the open
+        // route's totals.  false: a shift beyond the tables (re-evaluate)
+        auto shifted = [&](int r, int rend, uint32_t& xs, uint32_t& xm, int& xc)
+                           __attribute__((always_inline)) -> bool {
+          while (r < rend) {
+            const int d = vo - r;
+            if (d < -kSegShift || d > kSegShift) return false;
+            const int l = d ? min((int)nb_row(d)[r], rend) : rend;
+            const int gl = l < rend ? (int)T.SEGR[l] : 0;
+            const int rs = l < rend ? (int)T.RB[gl] : rend;
+            if (rs > r) {
+              xs += T.dsp[rs] - T.dsp[r];
+              xm = max(xm, rmaxq(r, rs - 1));
+              xc += rs - r;
+              vo += rs - r;
+            }
+            if (l >= rend) break;
+            run(pre(SPX(gl - 1) + 1, SPX(gl) - 1), false, 0u);
+            close();
+            r = T.RB[gl + 1];
+          }
+          return true;
         };
         // the start of the first changed segment, up to lo
         run(p_start, false, 0u);
@@ -798,11 +852,13 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
               // route does on the vehicles it moves to, reversed (which hands
               // them to the vehicles in reverse) when one capacity serves them
               // before and after
-              bool tabled = !rev || r1 - r0 == g1 - g0 + 1;
+              bool tabled = !rev || r1 - r0 == g1 - g0 + 1, split = false;
               if (HET && tabled) {
-                tabled = rev ? one_class(r0, r1 - 1) && one_class(vo, vo + r1 - r0 - 1) &&
-                                   capv(vo) == capv(r0)
-                             : keeps(r0, r1, vo - r0);
+                if (rev)
+                  tabled = one_class(r0, r1 - 1) && one_class(vo, vo + r1 - r0 - 1) &&
+                           capv(vo) == capv(r0);
+                else if (!keeps(r0, r1, vo - r0))
+                  split = true;  // forward: tables up to each route that fails, its segment walked
               }
               if (!tabled) {  // walk them
                 for (int t = 0; t <= g1 - g0; ++t) {
@@ -812,10 +868,18 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
                   ++seps;
                 }
               } else {
-                isum += ISUM[s];
-                imax = max(imax, IMAX[s]);
-                icnt += r1 - r0;
-                vo += r1 - r0;
+                if (split) {
+                  const int seps0 = seps;
+                  const bool cust0 = cust;
+                  if (!shifted(r0, r1, isum, imax, icnt)) full = true;
+                  seps = seps0;
+                  cust = cust0;
+                } else {
+                  isum += ISUM[s];
+                  imax = max(imax, IMAX[s]);
+                  icnt += r1 - r0;
+                  vo += r1 - r0;
+                }
                 // the last customer in the moved order and the separators after it
                 const int gf = GF[s];
                 const bool has = rev ? gf <= g1 : gf >= g0;
@@ -846,35 +910,9 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
         if (HET) {
           tsum = tmax = 0u;
           tcnt = 0;
-          int r = rz, delta = vo - rz;
           const int seps0 = seps;
           const bool cust0 = cust;
-          while (r < R) {
-            if (delta < -kSegShift || delta > kSegShift) {
-              full = true;
-              break;
-            }
-            const int l = delta ? (int)nb_row(delta)[r] : R;  // the first route that splits differently
-            if (l >= R) {
-              tsum += dspR - T.dsp[r];
-              tmax = max(tmax, T.smx[r]);
-              tcnt += R - r;
-              break;
-            }
-            const int gl = T.SEGR[l];  // walk its segment
-            const int rs = T.RB[gl], re = T.RB[gl + 1];
-            if (rs > r) {
-              tsum += T.dsp[rs] - T.dsp[r];
-              tmax = max(tmax, rmaxq(r, rs - 1));
-              tcnt += rs - r;
-            }
-            const int c0 = c_cnt;
-            vo = rs + delta;
-            run(pre(SPX(gl - 1) + 1, SPX(gl) - 1), false, 0u);
-            close();
-            delta += (c_cnt - c0) - (re - rs);
-            r = re;
-          }
+          if (!shifted(rz, R, tsum, tmax, tcnt)) full = true;
           seps = seps0;
           cust = cust0;
         }
