@@ -1111,6 +1111,7 @@ int launch_sa_seg(const vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* d_cu
   // separators: a tour of the N - 1 customers and n - (N - 1) separators
   const int segs = std::max(8, ((std::max(0, n - (in.N - 1)) + 2 + 7) & ~7));
   const int rm = std::max(2 * in.K + 2, segs + 2) + 8;
+  if (rm > 65535) return 1;  // route indices are u16 in the tables
   const int lv = seg_levels(rm);
   const uint32_t cb = seg_chain_bytes(n, segs, rm, lv, het, in.K);
   const size_t base = inst_lds_bytes_host(si) + (((size_t)in.N * 4u + 15u) & ~(size_t)15u);
