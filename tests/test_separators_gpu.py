@@ -391,7 +391,20 @@ SEG_CASES = [
     ("cvrp300_het_warm_m256", lambda: _classes(synth.cvrp(300, 24, seed=14, slack=1.3),
                                                (1.2, 0.9), shuffle=True), "pack", 8, 200,
      1 / 60.0, 24, 2, 256),
+    # four wavefronts x two moves per lane, and an int32 matrix (entries past 65535)
+    ("x1000_het_m512", lambda: _classes(synth.x_style(1000, seed=15), (1.4, 1.1, 0.9)), "pack",
+     4, 80, 1 / 300.0, 32, 2, 512),
+    ("cvrp300_het_i32", lambda: _scaled(_classes(synth.cvrp(300, 24, seed=16, slack=1.3),
+                                                 (1.3, 1.0, 0.8)), 90), "pack", 8, 120,
+     1 / 27000.0, 24, 2, 128),
 ]
+
+
+def _scaled(inst, k):
+    """inst with its (symmetric) durations times k: entries past 65535 put the
+    matrix in int32."""
+    import dataclasses
+    return dataclasses.replace(inst, durations=inst.durations * k)
 
 
 def _classes(inst, fracs, shuffle=False):
