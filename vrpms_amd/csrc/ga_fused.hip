@@ -15,8 +15,10 @@
 //   * children are scored in place by the headline kernel's split step
 //     (chains.hpp: v_perm + v_dot2 gather addressing, branch-free split,
 //     exact re-walk of the rare lanes that meet the fleet limit);
-//   * a mutation is applied by all 64 lanes through moved_index (one LDS
-//     copy + one gathered write) instead of a serial lane-0 loop.
+//   * a mutation is folded into the child's OX1 writes (each gene goes to
+//     the position the move sends its OX1 position to), and the genes taken
+//     from A are marked with a per-child stamp instead of a cleared bitmap:
+//     per child one pass over A's span and one over B, no barrier pass.
 //
 // The launch count per call drops from 3 per generation to 1, and no tour
 // crosses HBM between generations.
@@ -57,8 +59,7 @@ struct GaFusedArgs {
   uint32_t pmut, seed_lo, seed_hi;
   uint64_t gen0;
   uint32_t rs;  // LDS bytes per tour row (multiple of 4, rs / 4 odd)
-  uint32_t off_rows, off_pk, off_ck, off_prow, off_crow, off_sk, off_si, off_used, off_tmp,
-      off_bits;
+  uint32_t off_rows, off_pk, off_ck, off_prow, off_crow, off_sk, off_si, off_used, off_bits;
   uint16_t* pop_tours;  // [islands][pop][n] in/out
   uint64_t* pop_keys;   // [islands][pop] in/out
 };
@@ -77,7 +78,6 @@ static GaFusedLayout ga_fused_layout(int N, int n, int P) {
   if (((rs / 4) & 1u) == 0) rs += 4;  // odd dword stride: rows spread over the banks
   int M = 1;
   while (M < 2 * P) M <<= 1;
-  const uint32_t words = ((uint32_t)N + 31u) / 32u;
   size_t off = al16((size_t)N * N * 8);
   GaFusedArgs& a = L.a;
   a.rs = rs;
@@ -89,8 +89,7 @@ static GaFusedLayout ga_fused_layout(int N, int n, int P) {
   a.off_crow = (uint32_t)off;   off = al16(off + (size_t)P * 2);
   a.off_sk = (uint32_t)off;     off = al16(off + (size_t)M * 8);
   a.off_si = (uint32_t)off;     off = al16(off + (size_t)M * 4);
-  a.off_used = (uint32_t)off;   off = al16(off + (size_t)16 * words * 4);
-  a.off_tmp = (uint32_t)off;    off = al16(off + (size_t)16 * rs);
+  a.off_used = (uint32_t)off;   off = al16(off + (size_t)16 * N * 4);  // gene stamps per wave
   a.off_bits = (uint32_t)off;   off = al16(off + ((size_t)2 * P / 32 + 1) * 4);
   L.bytes = off;
   return L;
@@ -108,7 +107,6 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
   const int P = a.pop, n = a.n, island = blockIdx.x;
   const int wave = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const uint32_t rs = a.rs;
-  const uint32_t words = ((uint32_t)a.f.N + 31u) / 32u;
   uint8_t* rows = smem + a.off_rows;
   uint64_t* pk = reinterpret_cast<uint64_t*>(smem + a.off_pk);
   uint64_t* ck = reinterpret_cast<uint64_t*>(smem + a.off_ck);
@@ -116,8 +114,8 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
   uint16_t* crow = reinterpret_cast<uint16_t*>(smem + a.off_crow);
   uint64_t* sk = reinterpret_cast<uint64_t*>(smem + a.off_sk);
   uint32_t* si = reinterpret_cast<uint32_t*>(smem + a.off_si);
-  uint32_t* used = reinterpret_cast<uint32_t*>(smem + a.off_used) + wave * words;
-  uint8_t* tmp = smem + a.off_tmp + wave * rs;
+  // mk[g] == the current child's stamp: gene g is in the child's A[lo..hi]
+  uint32_t* mk = reinterpret_cast<uint32_t*>(smem + a.off_used) + wave * (uint32_t)a.f.N;
   uint32_t* bits = reinterpret_cast<uint32_t*>(smem + a.off_bits);
   uint16_t* gpop = a.pop_tours + (int64_t)island * P * n;
   uint64_t* gkeys = a.pop_keys + (int64_t)island * P;
@@ -135,7 +133,10 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
     crow[i] = (uint16_t)(P + i);
     pk[i] = gkeys[i];
   }
+  for (int i = threadIdx.x; i < 16 * a.f.N; i += blockDim.x)
+    reinterpret_cast<uint32_t*>(smem + a.off_used)[i] = 0u;
   __syncthreads();
+  const int cpw = (P + 15) / 16;  // children per wavefront per generation
 
   WordChains<1> ch;
   ch.setup(a.f, smem);
@@ -183,14 +184,27 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
         continue;
       }
       const int lo = wave_bcast(v_lo, k), hi = wave_bcast(v_hi, k);
+      // the child's mutation (wave-uniform) folded into its writes: the gene
+      // OX1 puts at position p goes to the position the move maps p to (the
+      // inverse of moved_index), so no copy-and-gather pass follows
+      const bool mut = wave_bcast(v_mut, k) != 0;
+      const uint32_t mtyp = (uint32_t)wave_bcast(v_mtyp, k);
+      const int mi = wave_bcast(v_mi, k), mj = wave_bcast(v_mj, k);
+      auto dst_of = [&](int p) __attribute__((always_inline)) -> int {
+        if (!mut) return p;
+        if (mtyp == kMoveSwap) return p == mi ? mj : (p == mj ? mi : p);
+        if (mtyp == kMove2Opt) return (p >= mi && p <= mj) ? mi + mj - p : p;
+        if (mi < mj) return p == mi ? mj : ((p > mi && p <= mj) ? p - 1 : p);
+        return p == mi ? mj : ((p >= mj && p < mi) ? p + 1 : p);
+      };
       // OX1: out[lo..hi] = A[lo..hi]; the rest, from position hi+1 (wrapping),
-      // are B's genes from B[hi+1] onwards (wrapping) not yet used
-      for (uint32_t w = lane; w < words; w += 64) used[w] = 0u;
-      wave_sync();
+      // are B's genes from B[hi+1] onwards (wrapping) not yet used -- a gene
+      // is used when its stamp is this child's (no bitmap to clear)
+      const uint32_t stamp = 1u + (uint32_t)(g * cpw + k);
       for (int q = lo + lane; q <= hi; q += 64) {
         const uint32_t gq = A[q];
-        out[q] = (uint8_t)gq;
-        atomicOr(&used[gq >> 5], 1u << (gq & 31u));
+        out[dst_of(q)] = (uint8_t)gq;
+        mk[gq] = stamp;
       }
       wave_sync();
       const int rest = n - (hi - lo + 1);
@@ -203,7 +217,7 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
           int src = hi + 1 + q;
           src = src >= n ? src - n : src;
           gq = B[src];
-          keep = ((used[gq >> 5] >> (gq & 31u)) & 1u) == 0u;
+          keep = mk[gq] != stamp;
         }
         const uint64_t ball = __ballot(keep);
         const int before = __popcll(ball & ((1ull << lane) - 1ull));
@@ -212,21 +226,10 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
           if (slot < rest) {
             int dst = hi + 1 + slot;
             dst = dst >= n ? dst - n : dst;
-            out[dst] = (uint8_t)gq;
+            out[dst_of(dst)] = (uint8_t)gq;
           }
         }
         filled += __popcll(ball);
-      }
-      wave_sync();
-      if (wave_bcast(v_mut, k)) {  // wave-uniform: one move, applied by all lanes
-        Move m;
-        m.typ = (uint32_t)wave_bcast(v_mtyp, k);
-        m.i = wave_bcast(v_mi, k);
-        m.j = wave_bcast(v_mj, k);
-        for (int q = lane; q < n; q += 64) tmp[q] = out[q];
-        wave_sync();
-        for (int q = lane; q < n; q += 64) out[q] = tmp[moved_index(q, m)];
-        wave_sync();
       }
     }
     __syncthreads();
