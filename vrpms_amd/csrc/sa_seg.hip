@@ -377,10 +377,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
       }
       return cnt;
     };
-    // (one capacity) each segment's duration as if it were one route, with
-    // its route-order prefix sums / maxima: the route tables themselves
-    // whenever every segment is one route (R = S + 1), the common case
-    uint32_t rcarry = 0, cds = 0, cmx = 0;
+    uint32_t rcarry = 0;
     bool moved = true;
 #pragma unroll 1
     for (int it = 0; moved && it < (HET ? 6 : 1); ++it) {
@@ -390,14 +387,12 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
 #pragma unroll 1
       for (int base = 0; base <= S; base += 64) {
         const int g = base + lane;
-        uint32_t cnt = 0, ne = 0, guess = 0, d1 = 0;
+        uint32_t cnt = 0, ne = 0, guess = 0;
         if (g <= S) {
           const int s0 = SPX(g - 1) + 1, s1 = SPX(g) - 1;
           ne = s1 >= s0 ? 1u : 0u;
           guess = HET ? (!rb_valid && it == 0 ? (uint32_t)g : (uint32_t)T.RB[g]) : 0u;
           cnt = seg_routes(g, (int)guess);
-          if (!HET)
-            d1 = s1 >= s0 ? T.LG[s0] + T.PE[s1 + 2] - T.PE[s0 + 1] : T.PE[s1 + 2] - T.PE[s0];
         }
         uint32_t tc, tl;
         const uint32_t inc = dpp_scan<false>(cnt, tc);
@@ -410,17 +405,6 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
         }
         rcarry += tc;
         lcarry = max(lcarry, tl);
-        if (!HET) {
-          uint32_t ts, tm;
-          const uint32_t ids = dpp_scan<false>(d1, ts), imx = dpp_scan<true>(d1, tm);
-          if (g <= S) {
-            T.dur[g] = d1;
-            T.dsp[g + 1] = cds + ids;
-            T.pmx[g + 1] = max(cmx, imx);
-          }
-          cds += ts;
-          cmx = max(cmx, tm);
-        }
       }
       wave_sync();
     }
@@ -438,9 +422,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
     R = (int)rcarry;
     seg_ok = R <= RM;
     if (!seg_ok) return;
-    const bool one_each = !HET && R == S + 1;  // route r = segment r: tables done above
     uint32_t fcarry = 0;  // FNE[g] = S + 1 - (suffix max of S + 1 - g over non-empty g)
-    uint32_t smc = 0;     // (one_each) suffix maxima of the route durations
 #pragma unroll 1
     for (int top = (S / 64) * 64; top >= 0; top -= 64) {
       const int g = top + lane;
@@ -453,22 +435,13 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
       f = max(dpp_rscan_max(f, tf), fcarry);
       if (g <= S) T.FNE[g] = (uint16_t)(S + 1 - (int)f);
       fcarry = max(fcarry, tf);
-      if (one_each) {
-        uint32_t tm;
-        const uint32_t sm = max(dpp_rscan_max(g <= S ? T.dur[g] : 0u, tm), smc);
-        if (g <= S) T.smx[g] = sm;
-        smc = max(smc, tm);
-      }
     }
-    if (lane == 0) {
-      T.RB[S + 1] = (uint16_t)R;
-      if (one_each) T.smx[R] = 0u;
-    }
+    if (lane == 0) T.RB[S + 1] = (uint16_t)R;
     wave_sync();
     SEG_PT(9);
     // route durations (heterogeneous: loads and allowances), one lane per segment
 #pragma unroll 1
-    for (int g = one_each ? S + 1 : lane; g <= S; g += 64) {
+    for (int g = lane; g <= S; g += 64) {
       const int s0 = SPX(g - 1) + 1, s1 = SPX(g) - 1;
       int r = T.RB[g], x = s0;
       while (x <= s1 && T.PD[s1 + 1] - T.PD[x] > capv(r)) {
@@ -520,9 +493,9 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
     }
     // per-route prefix sums / maxima (dsp / pmx [r] over routes < r), suffix
     // maxima (smx [r] over routes >= r), sparse table of maxima
-    cds = cmx = 0;
+    uint32_t cds = 0, cmx = 0;
 #pragma unroll 1
-    for (int base = 0; base < (one_each ? 0 : R); base += 64) {
+    for (int base = 0; base < R; base += 64) {
       const int r = base + lane;
       const uint32_t d = r < R ? T.dur[r] : 0u;
       uint32_t ts, tm;
@@ -536,7 +509,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
     }
     uint32_t smx = 0;
 #pragma unroll 1
-    for (int top = one_each ? -64 : (R / 64) * 64; top >= 0; top -= 64) {
+    for (int top = (R / 64) * 64; top >= 0; top -= 64) {
       const int r = top + lane;
       uint32_t tm;
       const uint32_t sm = max(dpp_rscan_max(r < R ? T.dur[r] : 0u, tm), smx);
