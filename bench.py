@@ -54,10 +54,10 @@ def parse():
                     help="target CPU work for the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-other-configs", action="store_true")
-    ap.add_argument("--island-epochs", type=int, default=40,
+    ap.add_argument("--island-epochs", type=int, default=60,
                     help="cfg 4 island-SA leg (all ranks, RCCL elite all-gather); 0 disables")
     ap.add_argument("--island-steps", type=int, default=500,
-                    help="SA steps per island epoch (40 x 500 ~ 1 s of wall time)")
+                    help="SA steps per island epoch (60 x 500 ~ 1.1 s of wall time)")
     ap.add_argument("--quality-seconds", type=float, default=5.0,
                     help="wall time per side for the best-cost gap (0 disables)")
     ap.add_argument("--x1000-quality-seconds", type=float, default=10.0,
@@ -267,6 +267,43 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
             ok = g["unvisited"] == 0 and c["unvisited"] == 0 and c["duration_sum"]
             out["gap"] = (g["duration_sum"] - c["duration_sum"]) / c["duration_sum"] if ok else None
             out["gap_sign"] = "negative = GPU better"
+    return out
+
+
+def algo_quality(ctx, inst, seconds, seed=0):
+    """The GA and ACO endpoints' best cost at the same wall time as the SA
+    quality leg (cfg 2, api/vrp/{ga,aco}/index.py): each runs on the GPU for
+    `seconds` of wall time -- GA 256 islands x 256 (randomPermutationCount),
+    20 fused generations per epoch; ACO 64 colonies x 64 ants, 5 iterations
+    per epoch, best-so-far deposit every 5th -- with elite migration every 5
+    epochs (inject(elites(16)), as the SA leg).  Their giant tours carry no
+    separators: the A3 greedy split places the route boundaries."""
+    import torch
+    from vrpms_amd import runners
+    out = {}
+    for name in ("ga", "aco"):
+        if name == "ga":
+            r = runners.GARunner(ctx, inst.n, islands=256, pop=256, seed=seed, gens_per_epoch=20)
+            unit, per = "generations", 20
+        else:
+            r = runners.ACORunner(ctx, inst.n, colonies=64, ants=64, seed=seed,
+                                  iters_per_epoch=5, bsf_period=5)
+            unit, per = "iterations", 5
+        r.epoch()                              # first launch: code object load
+        torch.cuda.synchronize(ctx.dev)
+        t0 = time.perf_counter()
+        e = 0
+        while time.perf_counter() - t0 < seconds:
+            r.epoch()
+            e += 1
+            if e % 5 == 0:
+                r.inject(*r.elites(16))
+            torch.cuda.synchronize(ctx.dev)
+        wall = time.perf_counter() - t0
+        key, _ = r.best()
+        out[name] = {unit: (e + 1) * per, "epochs": e, "wall_s": wall,
+                     "unvisited": key >> 56, "duration_sum": (key >> 28) & (2**28 - 1)}
+        del r
     return out
 
 
@@ -697,6 +734,13 @@ def main():
         try:
             qual = quality(ctx, inst, args.quality_seconds, world, rank, dist,
                            with_cpu=(rank == 0 and not args.no_cpu_baseline))
+            by = algo_quality(ctx, inst, args.quality_seconds)
+            base = qual.get("cpu", qual.get("gpu"))
+            for v in by.values():
+                if base and v["unvisited"] == 0 and base["unvisited"] == 0:
+                    v["gap_vs_host_sa"] = (v["duration_sum"] - base["duration_sum"]) \
+                        / base["duration_sum"]
+            qual["by_algorithm"] = by
         except Exception:
             qual = {"error": traceback.format_exc(limit=3)}
 
