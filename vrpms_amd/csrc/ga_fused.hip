@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "chains.hpp"
 #include "common.hpp"
@@ -60,6 +61,7 @@ struct GaFusedArgs {
   uint64_t gen0;
   uint32_t rs;  // LDS bytes per tour row (multiple of 4, rs / 4 odd)
   uint32_t off_rows, off_pk, off_ck, off_prow, off_crow, off_sk, off_si, off_used, off_bits;
+  uint32_t off_rk, off_ri;  // child runs of merge_select
   uint16_t* pop_tours;  // [islands][pop][n] in/out
   uint64_t* pop_keys;   // [islands][pop] in/out
 };
@@ -89,8 +91,11 @@ static GaFusedLayout ga_fused_layout(int N, int n, int P) {
   a.off_crow = (uint32_t)off;   off = al16(off + (size_t)P * 2);
   a.off_sk = (uint32_t)off;     off = al16(off + (size_t)M * 8);
   a.off_si = (uint32_t)off;     off = al16(off + (size_t)M * 4);
-  a.off_used = (uint32_t)off;   off = al16(off + (size_t)16 * N * 4);  // gene stamps per wave
+  a.off_used = (uint32_t)off;   off = al16(off + (size_t)32 * N * 4);  // 2 stamp arrays per wave
   a.off_bits = (uint32_t)off;   off = al16(off + ((size_t)2 * P / 32 + 1) * 4);
+  const size_t runs = (size_t)64 * ((P + 63) / 64);
+  a.off_rk = (uint32_t)off;     off = al16(off + runs * 8);
+  a.off_ri = (uint32_t)off;     off = al16(off + runs * 4);
   L.bytes = off;
   return L;
 }
@@ -133,9 +138,18 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
     crow[i] = (uint16_t)(P + i);
     pk[i] = gkeys[i];
   }
-  for (int i = threadIdx.x; i < 16 * a.f.N; i += blockDim.x)
+  for (int i = threadIdx.x; i < 32 * a.f.N; i += blockDim.x)
     reinterpret_cast<uint32_t*>(smem + a.off_used)[i] = 0u;
   __syncthreads();
+  // survivors leave every generation ascending by (key, slot); the parents
+  // handed in usually are too (the previous call's output), and then the
+  // selection merges instead of sorting
+  bool sorted_parents;
+  {
+    int bad = 0;
+    for (int i = 1 + threadIdx.x; i < P; i += blockDim.x) bad |= pk[i - 1] > pk[i] ? 1 : 0;
+    sorted_parents = __syncthreads_or(bad) == 0;
+  }
   const int cpw = (P + 15) / 16;  // children per wavefront per generation
 
   WordChains<1> ch;
@@ -151,9 +165,11 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
     // parallel (two Philox blocks, both tournaments, the OX1 cut points, the
     // mutation): 64 children per wave in one pass instead of 64 serial ones.
     int v_pa = 0, v_pb = 0, v_lo = 0, v_hi = 0, v_mut = 0, v_mtyp = 0, v_mi = 0, v_mj = 0;
+    int v_out = 0;
     {
       const int child = wave + 16 * lane;
       if (child < P) {
+        v_out = crow[child];
         const uint32_t cid = (uint32_t)(island * P + child);
         const u32x4 r = philox((uint32_t)gen, (uint32_t)(gen >> 32), cid, 0u, a.seed_lo, a.seed_hi);
         const u32x4 r2 =
@@ -174,63 +190,99 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
         }
       }
     }
-    for (int k = 0; wave + 16 * k < P; ++k) {
-      const int child = wave + 16 * k;
-      const uint8_t* A = rows + (uint32_t)wave_bcast(v_pa, k) * rs;
-      const uint8_t* B = rows + (uint32_t)wave_bcast(v_pb, k) * rs;
-      uint8_t* out = rows + (uint32_t)crow[child] * rs;
-      if (n < 2) {
-        for (int q = lane; q < n; q += 64) out[q] = A[q];
-        continue;
+    // Two children of the wave at a time (each with its own stamp array),
+    // their A spans, B reads and stamp lookups issued together: the LDS
+    // round trips of one child hide behind the other's.
+    auto breed = [&](auto nc_tag, int k) __attribute__((always_inline)) {
+      constexpr int NC = decltype(nc_tag)::value;
+      const uint8_t* A[NC];
+      const uint8_t* B[NC];
+      uint8_t* out[NC];
+      uint32_t* m[NC];
+      int lo[NC], hi[NC], mi[NC], mj[NC], rest[NC], filled[NC];
+      bool mut[NC];
+      uint32_t mtyp[NC], stamp[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        A[c] = rows + (uint32_t)wave_bcast(v_pa, k + c) * rs;
+        B[c] = rows + (uint32_t)wave_bcast(v_pb, k + c) * rs;
+        out[c] = rows + (uint32_t)wave_bcast(v_out, k + c) * rs;
+        m[c] = mk + (uint32_t)((k + c) & 1) * 16u * (uint32_t)a.f.N;
+        lo[c] = wave_bcast(v_lo, k + c);
+        hi[c] = wave_bcast(v_hi, k + c);
+        // the child's mutation (wave-uniform) folded into its writes: the
+        // gene OX1 puts at position p goes to the position the move maps p
+        // to (the inverse of moved_index), so no copy-and-gather pass follows
+        mut[c] = wave_bcast(v_mut, k + c) != 0;
+        mtyp[c] = (uint32_t)wave_bcast(v_mtyp, k + c);
+        mi[c] = wave_bcast(v_mi, k + c);
+        mj[c] = wave_bcast(v_mj, k + c);
+        stamp[c] = 1u + (uint32_t)(g * cpw + k + c);
+        rest[c] = n - (hi[c] - lo[c] + 1);
+        filled[c] = 0;
       }
-      const int lo = wave_bcast(v_lo, k), hi = wave_bcast(v_hi, k);
-      // the child's mutation (wave-uniform) folded into its writes: the gene
-      // OX1 puts at position p goes to the position the move maps p to (the
-      // inverse of moved_index), so no copy-and-gather pass follows
-      const bool mut = wave_bcast(v_mut, k) != 0;
-      const uint32_t mtyp = (uint32_t)wave_bcast(v_mtyp, k);
-      const int mi = wave_bcast(v_mi, k), mj = wave_bcast(v_mj, k);
-      auto dst_of = [&](int p) __attribute__((always_inline)) -> int {
-        if (!mut) return p;
-        if (mtyp == kMoveSwap) return p == mi ? mj : (p == mj ? mi : p);
-        if (mtyp == kMove2Opt) return (p >= mi && p <= mj) ? mi + mj - p : p;
-        if (mi < mj) return p == mi ? mj : ((p > mi && p <= mj) ? p - 1 : p);
-        return p == mi ? mj : ((p >= mj && p < mi) ? p + 1 : p);
+      auto dst_of = [&](int c, int p) __attribute__((always_inline)) -> int {
+        if (!mut[c]) return p;
+        const int i = mi[c], j = mj[c];
+        if (mtyp[c] == kMoveSwap) return p == i ? j : (p == j ? i : p);
+        if (mtyp[c] == kMove2Opt) return (p >= i && p <= j) ? i + j - p : p;
+        if (i < j) return p == i ? j : ((p > i && p <= j) ? p - 1 : p);
+        return p == i ? j : ((p >= j && p < i) ? p + 1 : p);
       };
-      // OX1: out[lo..hi] = A[lo..hi]; the rest, from position hi+1 (wrapping),
-      // are B's genes from B[hi+1] onwards (wrapping) not yet used -- a gene
-      // is used when its stamp is this child's (no bitmap to clear)
-      const uint32_t stamp = 1u + (uint32_t)(g * cpw + k);
-      for (int q = lo + lane; q <= hi; q += 64) {
-        const uint32_t gq = A[q];
-        out[dst_of(q)] = (uint8_t)gq;
-        mk[gq] = stamp;
-      }
+      // OX1: out[lo..hi] = A[lo..hi]; the rest, from position hi+1
+      // (wrapping), are B's genes from B[hi+1] onwards (wrapping) not yet
+      // used -- a gene is used when its stamp is this child's (no bitmap to
+      // clear)
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        for (int q = lo[c] + lane; q <= hi[c]; q += 64) {
+          const uint32_t gq = A[c][q];
+          out[c][dst_of(c, q)] = (uint8_t)gq;
+          m[c][gq] = stamp[c];
+        }
       wave_sync();
-      const int rest = n - (hi - lo + 1);
-      int filled = 0;
-      for (int base = 0; base < n; base += 64) {
-        const int q = base + lane;
-        uint32_t gq = 0;
-        bool keep = false;
-        if (q < n) {
-          int src = hi + 1 + q;
-          src = src >= n ? src - n : src;
-          gq = B[src];
-          keep = mk[gq] != stamp;
-        }
-        const uint64_t ball = __ballot(keep);
-        const int before = __popcll(ball & ((1ull << lane) - 1ull));
-        if (keep) {
-          const int slot = filled + before;
-          if (slot < rest) {
-            int dst = hi + 1 + slot;
-            dst = dst >= n ? dst - n : dst;
-            out[dst_of(dst)] = (uint8_t)gq;
+      for (int base = 0; base < n; base += 128) {
+        uint32_t gq[NC][2];
+        bool keep[NC][2];
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int q = base + 64 * h + lane;
+            int src = hi[c] + 1 + q;
+            src = src >= n ? src - n : src;
+            gq[c][h] = q < n ? (uint32_t)B[c][src] : 0u;
           }
-        }
-        filled += __popcll(ball);
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            keep[c][h] = base + 64 * h + lane < n && m[c][gq[c][h]] != stamp[c];
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const uint64_t ball = __ballot(keep[c][h]);
+            const int slot = filled[c] + __popcll(ball & ((1ull << lane) - 1ull));
+            if (keep[c][h] && slot < rest[c]) {
+              int dst = hi[c] + 1 + slot;
+              dst = dst >= n ? dst - n : dst;
+              out[c][dst_of(c, dst)] = (uint8_t)gq[c][h];
+            }
+            filled[c] += __popcll(ball);
+          }
       }
+    };
+    if (n < 2) {
+      for (int k = 0; wave + 16 * k < P; ++k) {
+        const uint8_t* A = rows + (uint32_t)wave_bcast(v_pa, k) * rs;
+        uint8_t* out = rows + (uint32_t)wave_bcast(v_out, k) * rs;
+        for (int q = lane; q < n; q += 64) out[q] = A[q];
+      }
+    } else {
+      int k = 0;
+      for (; wave + 16 * (k + 1) < P; k += 2) breed(std::integral_constant<int, 2>{}, k);
+      if (wave + 16 * k < P) breed(std::integral_constant<int, 1>{}, k);
     }
     __syncthreads();
     GA_T(0);
@@ -268,13 +320,19 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
     __syncthreads();
     GA_T(1);
     // ---- (mu + lambda) survivors by (key, index) -----------------------------
-    for (int i = threadIdx.x; i < a.M; i += blockDim.x) {
-      sk[i] = i < P ? pk[i] : (i < 2 * P ? ck[i - P] : ~0ull);
-      si[i] = (uint32_t)i;
+    if (sorted_parents) {
+      merge_select(pk, ck, P, reinterpret_cast<uint64_t*>(smem + a.off_rk),
+                   reinterpret_cast<uint32_t*>(smem + a.off_ri), sk, si);
+    } else {
+      for (int i = threadIdx.x; i < a.M; i += blockDim.x) {
+        sk[i] = i < P ? pk[i] : (i < 2 * P ? ck[i - P] : ~0ull);
+        si[i] = (uint32_t)i;
+      }
+      __syncthreads();
+      if (a.M >= 64 && a.M <= 1024) block_sort_pairs_waves(sk, si, a.M);
+      else block_sort_pairs(sk, si, a.M);
+      sorted_parents = true;
     }
-    __syncthreads();
-    if (a.M >= 64 && a.M <= 1024) block_sort_pairs_waves(sk, si, a.M);
-    else block_sort_pairs(sk, si, a.M);
     GA_T(2);
     uint16_t nrow[2] = {0, 0};
 #pragma unroll

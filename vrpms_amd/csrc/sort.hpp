@@ -104,4 +104,102 @@ VRPMS_DEV void block_sort_pairs_waves(uint64_t* sk, uint32_t* si, int M) {
   __syncthreads();
 }
 
+// x from lane (lane ^ stride), stride a compile-time power of two after
+// unrolling: DPP quad_perm (1, 2) and row_ror:8 (8) ride on a VALU move,
+// ds_swizzle's xor mode (4, 16) needs no address; only 32 crosses halves
+// through ds_bpermute.
+VRPMS_DEV uint32_t xor_lanes(uint32_t x, int stride) {
+  switch (stride) {
+    case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);
+    case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, true);
+    case 4: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x101F);
+    case 8: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xF, 0xF, true);
+    case 16: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);
+    default: return (uint32_t)__shfl_xor((int)x, stride, 64);
+  }
+}
+
+// Bitonic sort of one (key, index) pair per lane across a wavefront
+// (ascending by lane; 21 compare-exchange stages over xor_lanes).  All 64
+// lanes must be active.
+VRPMS_DEV void wave_sort64(uint64_t& k, uint32_t& v) {
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const uint64_t ok = ((uint64_t)xor_lanes((uint32_t)(k >> 32), stride) << 32) |
+                          xor_lanes((uint32_t)k, stride);
+      const uint32_t ov = xor_lanes(v, stride);
+      const bool lower = (l & stride) == 0, up = (l & size) == 0;
+      const bool other_less = ok < k || (ok == k && ov < v);
+      if (lower == up ? other_less : !other_less) {
+        k = ok;
+        v = ov;
+      }
+    }
+  }
+}
+
+VRPMS_DEV bool pair_less(uint64_t ka, uint32_t ia, uint64_t kb, uint32_t ib) {
+  return ka < kb || (ka == kb && ia < ib);
+}
+
+// (mu + lambda) selection by merge ranks instead of a full sort of 2P pairs:
+// the P parents pk[0..P) are already ascending by (key, slot) (the previous
+// selection's output), the P children ck[0..P) (indices P + c) are sorted in
+// runs of 64 inside wavefronts, and every pair's final position is its
+// position in its own run plus a lower bound in each other run.  Pairs are
+// unique (the index breaks ties), so sk[0..P) / si[0..P) equal the first P of
+// block_sort_pairs over the 2P pairs.  rk / ri hold the child runs
+// (64 * ceil(P / 64) entries); needs blockDim.x >= 64 * ceil(P / 64).
+// Every thread of the block must call it.
+VRPMS_DEV void merge_select(const uint64_t* pk, const uint64_t* ck, int P, uint64_t* rk,
+                            uint32_t* ri, uint64_t* sk, uint32_t* si) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int R = (P + 63) >> 6;
+  if (w < R) {  // wave-uniform
+    const int c = (w << 6) | l;
+    uint64_t k = c < P ? ck[c] : ~0ull;  // padding sorts last (index > 2P)
+    uint32_t v = c < P ? (uint32_t)(P + c) : 0xFFFFFFFFu;
+    wave_sort64(k, v);
+    rk[c] = k;
+    ri[c] = v;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 2 * P; e += blockDim.x) {
+    const bool child = e >= P;
+    const int c = e - P, own = child ? c >> 6 : -1;
+    if (child && (c & 63) >= P - (own << 6)) continue;  // run padding
+    const uint64_t k = child ? rk[c] : pk[e];
+    const uint32_t v = child ? ri[c] : (uint32_t)e;
+    int rank = child ? (c & 63) : e;
+    if (child) {
+      int lo = 0, hi = P;  // lower bound among the parents
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (pair_less(pk[mid], (uint32_t)mid, k, v)) lo = mid + 1;
+        else hi = mid;
+      }
+      rank += lo;
+    }
+    for (int r = 0; r < R; ++r) {  // lower bound in every other run
+      if (r == own) continue;
+      const uint64_t* rkr = rk + (r << 6);
+      const uint32_t* rir = ri + (r << 6);
+      int pos = 0;
+#pragma unroll
+      for (int s = 32; s > 0; s >>= 1)
+        if (pair_less(rkr[pos + s - 1], rir[pos + s - 1], k, v)) pos += s;
+      if (pair_less(rkr[pos], rir[pos], k, v)) ++pos;
+      rank += pos;
+    }
+    if (rank < P) {
+      sk[rank] = k;
+      si[rank] = v;
+    }
+  }
+  __syncthreads();
+}
+
 }  // namespace vrpms
