@@ -61,8 +61,13 @@ def parse():
     ap.add_argument("--quality-seconds", type=float, default=5.0,
                     help="wall time per side for the best-cost gap (0 disables)")
     ap.add_argument("--x1000-quality-seconds", type=float, default=10.0,
-                    help="wall time per side for the cfg-4 X-1000 best-cost gap (seed 0; the "
-                         "host leg at 32 and at 64 moves per step, the better kept; 0 disables)")
+                    help="wall time per side for the cfg-4 X-1000 best-cost gaps (seeds 0-2, "
+                         "the host leg at 32 and at 64 moves per step, the better kept, seed 0's "
+                         "host leg repeated for the run-to-run spread; 0 disables)")
+    ap.add_argument("--x1000-seeds", type=int, nargs="+", default=[0, 1, 2])
+    ap.add_argument("--td-quality-seconds", type=float, default=10.0,
+                    help="wall time per side for the cfg-3 TD-200 x 24 best-cost gap (seed 0; "
+                         "0 disables)")
     return ap.parse_args()
 
 
@@ -87,13 +92,40 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
+def host_cores():
+    """(threads, record) for the host legs: every CPU this process may run
+    on (sched_getaffinity), capped by the cgroup's CPU quota (cpu.max: a
+    quota of q CPUs' time makes more than ceil(q) busy threads time-slice)
+    and by OMP_NUM_THREADS when the box sets it; the record says which bound
+    applied."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = aff
+    bound = "sched_getaffinity"
+    if quota is not None and math.ceil(quota) < threads:
+        threads, bound = int(math.ceil(quota)), "cgroup cpu.max quota"
+    if omp and omp < threads:
+        threads, bound = omp, "OMP_NUM_THREADS"
+    return max(1, threads), {"threads": max(1, threads), "bound_by": bound,
+                             "sched_getaffinity": aff, "cgroup_cpu_quota": quota,
+                             "OMP_NUM_THREADS": omp or None, "os_cpu_count": os.cpu_count()}
+
+
 def cpu_baseline(inst, perms_dev, seconds):
     """Time the C oracle (OpenMP, all threads it is given) on a bounded
     sample of the same tours; returns the cpu_baseline object."""
     import numpy as np
     from oracle import coracle
     coracle.build()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or coracle.max_threads()
+    threads, cores = host_cores()
     S = int(min(perms_dev.shape[0], 4 << 20))
     sample = perms_dev[:S].cpu().numpy()
     passes, dt, ref = 0, 0.0, None
@@ -113,7 +145,7 @@ def cpu_baseline(inst, perms_dev, seconds):
         py_n += 1
     py_dt = time.perf_counter() - t0
     return {"value": S * passes / dt, "unit": "evals/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
+            "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(), "host_cores": cores,
             "sample": f"{passes} pass(es) over the first {S} of the same CVRP-100 tours, C "
                       f"restatement oracle/oracle_c.c (OpenMP, {threads} threads), "
                       f"{dt:.2f} s",
@@ -231,7 +263,7 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
                       "duration_sum": (key >> 28) & (2**28 - 1)}
     if with_cpu:
         from oracle import coracle
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or coracle.max_threads()
+        threads, cores = host_cores()
         if n_sep and start == "greedy":
             t0_ = ctx.insert_separators(ctx.random_tours(threads, n, 7), n_sep)
         elif n_sep and start == "pack":
@@ -256,7 +288,8 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
             step += steps
         cpu_wall = cool.elapsed()
         ck = int(bk.min())
-        out["cpu"] = {"chains": threads, "cores": threads, "moves_per_step": cpu_moves,
+        out["cpu"] = {"chains": threads, "cores": threads, "host_cores": cores,
+                      "moves_per_step": cpu_moves,
                       "steps_per_chain": step,
                       "wall_s": cpu_wall, "unvisited": ck >> 56,
                       "duration_sum": (ck >> 28) & (2**28 - 1),
@@ -307,28 +340,75 @@ def algo_quality(ctx, inst, seconds, seed=0):
     return out
 
 
-def x1000_quality(ctx, seconds, dist, with_cpu):
-    """The metric's second half on cfg 4 (X-style CVRP-1000, seed 0): the
-    GPU leg (sa_seg_kernel, 256 chains x 128 moves per step, W = 2
-    wavefronts per chain) against the host port (oracle_sa_run_resync with
-    its C segment pricing seg_key, one chain per thread) at 32 and at 64
-    moves per step, the better host result kept -- the cells of
-    tools/quality_sweep.py --instance x1000."""
+def _host_best(ctx, inst, seconds, dist, kw, moves_list):
+    """The host leg at each move count; (best leg, all legs) by durationSum."""
+    legs = [quality(ctx, inst, seconds, 1, 0, dist, with_cpu=True, cpu_moves=m, gpu=False,
+                    **kw)["cpu"] for m in moves_list]
+    ok = [c for c in legs if c["unvisited"] == 0]
+    best = min(ok, key=lambda c: c["duration_sum"]) if ok else legs[0]
+    return best, legs
+
+
+def _gap(g, c):
+    if g["unvisited"] == 0 and c["unvisited"] == 0 and c["duration_sum"]:
+        return (g["duration_sum"] - c["duration_sum"]) / c["duration_sum"]
+    return None
+
+
+def equal_time_cells(ctx, seconds, dist, with_cpu, instance="x1000", seeds=(0, 1, 2),
+                     cpu_moves=(32, 64), repeat_host=True):
+    """The metric's second half, several seeds: per seed the GPU
+    leg (x1000: sa_seg_kernel; tdvrp200: sa_route_kernel -- 256 chains x 128
+    moves per step, W = 2 wavefronts per chain) against the host port
+    (oracle_sa_run_resync, one chain per host thread) at each of `cpu_moves`
+    moves per step, the better host result kept.  `repeat_host` runs seed
+    0's better host leg a second time: the host's run-to-run spread (its
+    wall-time cooling follows the measured step rate, so two runs of one seed
+    differ) is reported beside the gaps, and a gap counts as a GPU win only
+    when it is below minus that spread."""
+    import statistics
+
     from vrpms_amd import synth
     from vrpms_amd.core import CVRP
-    x = synth.x_style(1000, seed=0)
-    ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
-    kw = dict(chains=256, moves=128, label="x1000 seed 0", window=32, window_types=2,
-              start="pack")
-    q = quality(ctx, x, seconds, 1, 0, dist, with_cpu=with_cpu, cpu_moves=32, **kw)
-    if with_cpu:
-        q2 = quality(ctx, x, seconds, 1, 0, dist, with_cpu=True, cpu_moves=64, gpu=False, **kw)
-        q["cpu_alternatives"] = [q2["cpu"]]
-        if q2["cpu"]["unvisited"] == 0 and q2["cpu"]["duration_sum"] < q["cpu"]["duration_sum"]:
-            q["cpu_alternatives"] = [q["cpu"]]
-            q["cpu"] = q2["cpu"]
-            q["gap"] = (q["gpu"]["duration_sum"] - q["cpu"]["duration_sum"]) / q["cpu"]["duration_sum"]
-    return q
+    make = {"x1000": lambda sd: synth.x_style(1000, seed=sd),
+            "tdvrp200": lambda sd: synth.td_cvrp(200, 16, seed=sd)}[instance]
+    kw = dict(chains=256, moves=128, window=32, window_types=2, start="pack")
+    cells = []
+    spread = None
+    for sd in seeds:
+        x = make(sd)
+        ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
+        q = quality(ctx, x, seconds, 1, 0, dist, with_cpu=False, label=f"{instance} seed {sd}",
+                    **kw)
+        cell = {"seed": sd, "gpu": q["gpu"]}
+        if with_cpu:
+            best, legs = _host_best(ctx, x, seconds, dist, kw, cpu_moves)
+            cell["cpu"] = best
+            cell["cpu_legs"] = [{"moves_per_step": c["moves_per_step"],
+                                 "duration_sum": c["duration_sum"], "unvisited": c["unvisited"],
+                                 "steps_per_chain": c["steps_per_chain"]} for c in legs]
+            cell["gap"] = _gap(q["gpu"], best)
+            if repeat_host and spread is None:
+                again = quality(ctx, x, seconds, 1, 0, dist, with_cpu=True, gpu=False,
+                                cpu_moves=best["moves_per_step"], **kw)["cpu"]
+                a, b = best["duration_sum"], again["duration_sum"]
+                spread = {"seed": sd, "moves_per_step": best["moves_per_step"],
+                          "runs": [a, b], "rel": abs(a - b) / min(a, b)}
+        cells.append(cell)
+    out = {"instance": instance, "T_s": seconds, "seeds": list(seeds),
+           "gpu_shape": "256 chains x 128 moves per step (W = 2)",
+           "host": f"oracle_sa_run_resync, better of {list(cpu_moves)} moves per step",
+           "window": 32, "window_types": 2, "start": "pack", "cells": cells,
+           "gap_sign": "negative = GPU better"}
+    gaps = [c["gap"] for c in cells if c.get("gap") is not None]
+    if gaps:
+        out["gap_median"] = statistics.median(gaps)
+        out["gpu_better"] = f"{sum(g < 0 for g in gaps)} / {len(gaps)}"
+    if spread is not None:
+        out["host_run_to_run"] = spread
+        if gaps:
+            out["median_beyond_spread"] = out["gap_median"] < -spread["rel"]
+    return out
 
 
 def other_configs(ctx, torch, dev, seed=0, r_lds=None):
@@ -744,13 +824,21 @@ def main():
         except Exception:
             qual = {"error": traceback.format_exc(limit=3)}
 
-    xq = None
+    xq = tdq = None
     if args.x1000_quality_seconds > 0 and world == 1:
         try:
-            xq = x1000_quality(ctx, args.x1000_quality_seconds, dist,
-                               with_cpu=(rank == 0 and not args.no_cpu_baseline))
+            xq = equal_time_cells(ctx, args.x1000_quality_seconds, dist,
+                                  with_cpu=(rank == 0 and not args.no_cpu_baseline),
+                                  seeds=tuple(args.x1000_seeds))
         except Exception:
             xq = {"error": traceback.format_exc(limit=3)}
+    if args.td_quality_seconds > 0 and world == 1:
+        try:
+            tdq = equal_time_cells(ctx, args.td_quality_seconds, dist,
+                                   with_cpu=(rank == 0 and not args.no_cpu_baseline),
+                                   instance="tdvrp200", seeds=(0,), repeat_host=False)
+        except Exception:
+            tdq = {"error": traceback.format_exc(limit=3)}
 
     isl = None
     if args.island_epochs > 0:
@@ -814,6 +902,8 @@ def main():
             out["quality"] = qual
         if xq is not None:
             out["quality_x1000"] = xq
+        if tdq is not None:
+            out["quality_tdvrp200"] = tdq
         if isl is not None:
             out["islands"] = isl
         if world == 1 and not args.no_cpu_baseline:

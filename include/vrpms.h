@@ -122,7 +122,7 @@ int vrpms_eval_path(vrpms_ctx* ctx, int32_t perm_bytes, int64_t ld, const void* 
  *   also used for heterogeneous fleets, A/B only). */
 #define VRPMS_OPT_WORDS_KERNEL 3
 /*   VRPMS_OPT_WORDS_ILP: candidates per lane in eval_cvrp_words2 (0 = auto:
- *   2; 1 or 2 force, A/B). */
+ *   2; 2 force; 1 only in libraries built with -DVRPMS_AB, A/B). */
 #define VRPMS_OPT_WORDS_ILP 4
 /*   VRPMS_OPT_WORDS_LOOKAHEAD: words ahead whose gathers eval_cvrp_words2
  *   keeps in flight (0 = auto, 1 or 2 force; A/B). */
@@ -154,6 +154,10 @@ int vrpms_eval_path(vrpms_ctx* ctx, int32_t perm_bytes, int64_t ld, const void* 
  *   when not every rank has joined by then, so a rank that never arrives
  *   yields VRPMS_ETIMEOUT instead of a hang. */
 #define VRPMS_OPT_ISLAND_TIMEOUT_S 10
+/*   VRPMS_OPT_SEG_WAVES: wavefronts per chain of the segment-priced SA kernel
+ *   (0 = auto: moves / 64 up to 4 while every chain's wavefronts stay
+ *   resident; 1..4 force, A/B -- the trajectories do not depend on it). */
+#define VRPMS_OPT_SEG_WAVES 11
 int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value);
 
 /* Decode ONE giant tour into the result dict of api/vrp/ga/index.py:49-53

@@ -769,6 +769,7 @@ typedef struct {
   int64_t rsum, rmax;
   int rcnt;
   int64_t* out; /* route durations (table build) or NULL */
+  int cuts, bud, dead; /* capacity cuts so far, the most the fleet allows, over it */
 } sacc_t;
 
 static inline int64_t d0(const inst_t* I, int a, int b) {
@@ -791,7 +792,7 @@ static inline void s_close(const inst_t* I, sacc_t* a) {
 static void s_run(const inst_t* I, const seg_t* C, const uint16_t* A, int a, int b, int rev,
                   sacc_t* c) {
   const int64_t *PE = C->PE, *PD = C->PD, cap = I->cap[0];
-  while (a <= b) {
+  while (a <= b && !c->dead) {
     const int64_t room = cap - c->load;
     if (PD[b + 1] - PD[a] <= room) {
       c->dur += d0(I, c->prev, rev ? A[b] : A[a]) + PE[b + 1] - PE[a + 1];
@@ -799,6 +800,11 @@ static void s_run(const inst_t* I, const seg_t* C, const uint16_t* A, int a, int
       c->prev = rev ? A[a] : A[b];
       return;
     }
+    if (c->cuts >= c->bud) { /* one cut more than the fleet allows: no search */
+      c->dead = 1;
+      return;
+    }
+    ++c->cuts;
     if (!rev) {
       int lo = a - 1, hi = b; /* last q in [a - 1, b] with PD[q + 1] - PD[a] <= room */
       while (lo < hi) {
@@ -848,7 +854,7 @@ static void seg_build(const inst_t* I, const uint16_t* A, int n, seg_t* C) {
   C->S = S;
   C->NC[n] = n;
   for (int q = n - 1; q >= 0; --q) C->NC[q] = A[q] ? q : C->NC[q + 1];
-  sacc_t c = {0, 0, 0, 0, 0, 0, C->dur};
+  sacc_t c = {0, 0, 0, 0, 0, 0, C->dur, 0, 0x7fffffff, 0};
   for (int g = 0; g <= S; ++g) {
     C->RB[g] = c.rcnt;
     s_run(I, C, A, sspx(C, g - 1) + 1, sspx(C, g) - 1, 0, &c);
@@ -943,15 +949,27 @@ static void g_piece(const inst_t* I, const seg_t* C, const uint16_t* A, int a, i
 }
 
 /* Key of A moved by m (route_model.price_seg); *unserved = 1 (key 0) when
- * the moved tour leaves a customer unvisited. */
+ * the moved tour leaves a customer unvisited.  `hopeless` (such a move can
+ * never be accepted): the moved tour has S + 1 + cuts routes and, when the
+ * tail after the last changed segment keeps its customers, the current
+ * tour's T trailing separators, so it serves everyone iff its cuts <=
+ * K - 1 - S + T; segments outside the changed ones keep their cuts, and an
+ * overflowing run past the rest of that budget stops there (unserved)
+ * instead of searching its cuts -- the device's rule (sa_seg_kernel). */
 static uint64_t seg_key(const inst_t* I, const uint16_t* A, const seg_t* C, const move_t* m,
-                        int* unserved) {
+                        int hopeless, int* unserved) {
   const int n = C->n, i = m->i, j = m->j;
   const int lo = i < j ? i : j, hi = i < j ? j : i;
   const int* SC = C->SC;
   const int s0 = SC[lo], st = sspx(C, s0 - 1) + 1, en = sspx(C, SC[hi + 1]);
+  const int glast = en < n ? SC[en] : C->S;
+  const int ra = C->RB[s0], rz = C->RB[glast + 1];
+  const int tail_kept = en < n && C->PC[n - 1] > en;
   sreg_t g;
   memset(&g, 0, sizeof(g));
+  g.c.bud = hopeless && tail_kept
+                ? (I->K - 1 - C->S + C->T) - ((ra - s0) + (C->R - rz) - (C->S - glast))
+                : 0x7fffffff;
   g_run(I, C, A, st, lo - 1, 0, &g);
   if (m->typ == 1) {
     g_piece(I, C, A, i, j, 1, &g);
@@ -972,12 +990,10 @@ static uint64_t seg_key(const inst_t* I, const uint16_t* A, const seg_t* C, cons
     g_run(I, C, A, hi + 1, n - 1, 0, &g);
     s_close(I, &g.c);
   }
-  const int glast = en < n ? SC[en] : C->S;
-  const int ra = C->RB[s0], rz = C->RB[glast + 1];
   const int R = C->R - (rz - ra) + g.c.rcnt + g.icnt;
   int Tb = C->T;
-  if (!(en < n && C->PC[n - 1] > en) && g.cust) Tb = g.seps + (en < n ? n - 1 - en : 0);
-  *unserved = R - Tb > I->K;
+  if (!tail_kept && g.cust) Tb = g.seps + (en < n ? n - 1 - en : 0);
+  *unserved = g.c.dead || R - Tb > I->K;
   if (*unserved) return 0;
   const int64_t dsum = C->dsp[ra] + g.c.rsum + g.isum + C->dsp[C->R] - C->dsp[rz];
   int64_t dmax = C->pmx[ra] > C->smx[rz] ? C->pmx[ra] : C->smx[rz];
@@ -1069,7 +1085,7 @@ int oracle_sa_run_resync(int problem, const int32_t* D, int H, int N, const int3
           uint64_t kk;
           if (sym) {
             int unserved = 0;
-            kk = seg_key(&I, A, &C, &m, &unserved);
+            kk = seg_key(&I, A, &C, &m, hopeless, &unserved);
             if (unserved) kk = hopeless ? ~0ull : tour_key(&I, A, n, &m);
           } else {
             kk = S.alive ? resync_key(&I, A, n, &m, &S, hopeless) : tour_key(&I, A, n, &m);

@@ -73,3 +73,19 @@ def test_resync_nonuniform_fleet_falls_back():
     if hasattr(inst, "_replace"):
         P = _starts(inst, 3, inst.K - 1, "random", 6)
         _both(inst, P, 100, 1 / 60.0, 1 / 0.99, 3)
+
+
+@pytest.mark.parametrize("n_sep_off", [1, 4])
+def test_resync_cold_cut_budget(n_sep_off):
+    """Cold chains on first-fit routes: most moved pieces overflow a full
+    route; segment pricing stops an overflowing run once the composed
+    segments' cuts exceed what the fleet count allows (K - 1 - S + T minus the
+    other segments' cuts).  n_sep_off 1: K - 1 separators, no cut is ever
+    affordable; 4: K - 4 separators, up to three routes may split."""
+    inst = synth.x_style(1000, seed=3)
+    P = _starts(inst, 4, inst.K - n_sep_off, "pack", 8)
+    edge = float(np.asarray(inst.durations)[np.asarray(inst.durations) > 0].mean())
+    _both(inst, P, 300, 1 / (0.005 * edge), 1.0, 17, window=32, types=2)
+    small = synth.cvrp(120, 10, seed=6)
+    P = _starts(small, 6, small.K - n_sep_off, "pack", 2)
+    _both(small, P, 400, 1 / 5.0, 1.0, 19)

@@ -142,7 +142,7 @@ def test_rows2_matches_packed_and_oracle(words_gen, coracle, n, K, ld, C):
         np.testing.assert_array_equal(got, ref)
 
 
-@pytest.mark.parametrize("ilp,la", [(1, 1), (2, 1), (1, 2), (2, 2)])
+@pytest.mark.parametrize("ilp,la", [(2, 1), (2, 2)])
 def test_words2_ilp_variants(words_gen, coracle, ilp, la):
     ctx = words_gen
     ctx.set_words_ilp(ilp)
@@ -310,7 +310,7 @@ def test_errors_are_raised(ctx):
 # (eval_words.hip split_step_fast / redo_exact): waves where some lanes
 # exhaust and others do not, on every ILP / look-ahead variant and on the
 # row-major kernel, against the oracle.
-@pytest.mark.parametrize("ilp,la", [(1, 1), (2, 1), (1, 2), (2, 2)])
+@pytest.mark.parametrize("ilp,la", [(2, 1), (2, 2)])
 @pytest.mark.parametrize("slack", [1.03, 0.9])
 def test_words2_mixed_exhaustion(words_gen, coracle, ilp, la, slack):
     ctx = words_gen
@@ -318,7 +318,7 @@ def test_words2_mixed_exhaustion(words_gen, coracle, ilp, la, slack):
     ctx.set_words_lookahead(la)
     inst = synth.cvrp(100, 8, seed=12, slack=slack)
     check_words(ctx, coracle, inst, synth.random_perms(8191, inst.n, seed=ilp + 2 * la), inst.n,
-                objective=ilp - 1)
+                objective=la - 1)
 
 
 @pytest.mark.parametrize("n,ld,slack", [(100, 100, 1.03), (97, 100, 0.95), (30, 32, 0.7)])

@@ -183,9 +183,12 @@ class _CommStandIn(StandInContext):
         self.timeout = s
 
     def island_unique_id(self):
+        if self.bad_rank == "uid":
+            raise RuntimeError("simulated ncclGetUniqueId failure")
         return bytes(128)
 
     def island_init(self, uid, rank, world):
+        self.init_called = True
         if rank == self.bad_rank:
             raise RuntimeError("simulated ncclCommInitRank failure")
         self._world = world
@@ -204,16 +207,19 @@ def _agree_worker(rank, world, port, bad_rank, q):
             islands.init_comm(ctx, timeout_s=5)
             q.put((rank, ("ok", ctx.island_comm_group, ctx.timeout)))
         except RuntimeError as e:
-            q.put((rank, ("raised", ctx.island_comm_group, str(e))))
+            q.put((rank, ("raised", ctx.island_comm_group, str(e),
+                          getattr(ctx, "init_called", False))))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("bad_rank", [-1, 1])
+@pytest.mark.parametrize("bad_rank", [-1, 1, "uid"])
 def test_init_comm_ranks_agree_on_the_exchange_path(bad_rank):
     """init_comm sets the communicator on every rank or on none: when one
     rank's vrpms_island_init fails, every rank raises (no rank is left to
-    call ncclAllGather while another calls torch's all-gather)."""
+    call ncclAllGather while another calls torch's all-gather).  "uid": rank
+    0 cannot create the unique id -- it still enters the broadcast (with
+    None), no rank calls island_init, every rank raises."""
     mpc = mp.get_context("spawn")
     q = mpc.Queue()
     port = _free_port()
@@ -224,7 +230,12 @@ def test_init_comm_ranks_agree_on_the_exchange_path(bad_rank):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    if bad_rank < 0:
+    if bad_rank == "uid":
+        assert out[0][0] == out[1][0] == "raised"
+        assert out[0][1] is None and out[1][1] is None
+        assert "ncclGetUniqueId" in out[0][2] and "unique id" in out[1][2]
+        assert not out[0][3] and not out[1][3]
+    elif bad_rank < 0:
         assert out[0] == out[1] == ("ok", (None, 2), 5)
     else:
         assert out[0][0] == out[1][0] == "raised"

@@ -397,7 +397,24 @@ SEG_CASES = [
     ("cvrp300_het_i32", lambda: _scaled(_classes(synth.cvrp(300, 24, seed=16, slack=1.3),
                                                  (1.3, 1.0, 0.8)), 90), "pack", 8, 120,
      1 / 27000.0, 24, 2, 128),
+    # cold chains on full first-fit routes: overflowing runs stop at the cut budget
+    # (K - 1 separators: no cut affordable; K - 4: up to three routes may split)
+    ("x1000_cold_cut_budget", lambda: synth.x_style(1000, seed=17), "pack", 8, 300, 1.0, 32, 2,
+     128),
+    ("cvrp300_few_seps_cold", lambda: synth.cvrp(300, 24, seed=18), "pack_few", 8, 300, 0.5, 24,
+     2, 128),
+    # total demand past 2^31 with the capacity: the u32 prefix demands cannot hold
+    # it, so the launcher hands the chains to the full re-evaluation kernels
+    ("cvrp150_huge_demand", lambda: _huge_demand(synth.cvrp(150, 12, seed=19)), "pack", 4, 40,
+     1 / 300.0, 0, 0, 64),
 ]
+
+
+def _huge_demand(inst):
+    """inst with demands x 1e7 (total ~2^33) and capacities to match."""
+    import dataclasses
+    k = 10_000_000
+    return dataclasses.replace(inst, demand=inst.demand * k, capacities=inst.capacities * k)
 
 
 def _scaled(inst, k):
@@ -437,8 +454,8 @@ def test_segment_sa_matches_c_restatement(ctx, coracle, name, maker, start, chai
     tokens, against the C restatement (full walks and segment pricing)."""
     inst = maker()
     load(ctx, inst)
-    S = inst.K - 1
-    if start == "pack":
+    S = inst.K - 4 if start == "pack_few" else inst.K - 1
+    if start in ("pack", "pack_few"):
         P0 = synth.random_perms(chains, inst.n, seed=9, dtype=np.uint16)
         P = np.array([spec.pack_separators(p, S, inst.demand, inst.capacities) for p in P0])
     else:

@@ -268,8 +268,19 @@ def test_remote_front_end_over_http(monkeypatch):
         v = solver.solve_vrp("ga", MATRIX, locs, [5, 5], [0, 30], [2], [],
                              random_permutation_count=10, iteration_count=5)
         assert v["durationSum"] == 21
-        assert seen[-1][3] == {"random_permutationCount": 10, "iteration_count": 5}
+        assert seen[-1][3] == {"random_permutationCount": 10, "iteration_count": 5, "seed": 0,
+                               "objective": "sum"}
         assert seen[-1][2]["ignored_customers"] == [2]
+        # objective, seed and time limit travel with the instance
+        solver.solve_vrp("sa", MATRIX, locs, [5, 5], [0, 30], [], [], seed=3, objective="max",
+                         time_limit=2.5)
+        assert seen[-1][3] == {"random_permutationCount": None, "iteration_count": None,
+                               "seed": 3, "time_limit": 2.5, "objective": "max"}
+        solver.solve_tsp("sa", MATRIX, [1, 2, 3], 0, 0, seed=5)
+        assert seen[-1][3] == {"seed": 5}
+        # a knob the box would not honour is refused, not dropped
+        with pytest.raises(ValueError, match="unsupported"):
+            solver.solve_vrp("sa", MATRIX, locs, [5, 5], [0, 30], [], [], chains=64)
         p = solver.solve_vrp_problem(MATRIX, locs, [5, 5], [0, 30], [2], [])
         assert p["tour"] == [0, 1, 3, 0] and p["total_time"] == 21 and p["unvisited"] == []
         with pytest.raises(ValueError, match="Invalid request"):

@@ -30,7 +30,7 @@ for step in "$@"; do
     tsel) run pytest_sel 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread -k "$TSEL" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
-    benchq) run bench_quick 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --x1000-quality-seconds 0 ;;
+    benchq) run bench_quick 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --x1000-quality-seconds 0 --td-quality-seconds 0 ;;
     probe) run sa_probe 300 python tools/sa_probe.py ;;
     quality) run quality_sweep 1100 python -u tools/quality_sweep.py ;;
     quality_short) run quality_sweep 400 python -u tools/quality_sweep.py --T 1 10 ;;
@@ -38,11 +38,11 @@ for step in "$@"; do
     prof)
       cd /tmp
       run rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv \
-          -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --x1000-quality-seconds 0
+          -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --x1000-quality-seconds 0 --td-quality-seconds 0
       cd "$ROOT" ;;
     pmc)
       cd /tmp
-      B="python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --quality-seconds 0 --x1000-quality-seconds 0 --no-other-configs --island-epochs 0"
+      B="python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --quality-seconds 0 --x1000-quality-seconds 0 --td-quality-seconds 0 --no-other-configs --island-epochs 0"
       run pmc_a 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS \
           --output-format csv -d "$OUT/pmc_a" -o run -- $B
       run pmc_b 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_SCA \

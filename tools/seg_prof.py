@@ -2,7 +2,7 @@
 """Where sa_seg_kernel's time goes (built with -DVRPMS_SEG_PROF into
 build_ab/segprof/libvrpms.so): per SA step the pricing and accept (table
 rebuild) time (wall_clock64 ticks of lane 0, 100 MHz), the accept rate and
-the cross-wavefront exchange (W > 1, VRPMS_SEG_WAVES) -- on X-1000 first-fit start tours at a hot
+the cross-wavefront exchange (W > 1, SEG_WAVES=W -> VRPMS_OPT_SEG_WAVES) -- on X-1000 first-fit start tours at a hot
 and a cold fixed temperature.
 
 usage: tools/seg_prof.py build   (CPU: compile the variant; SEG_PROF_HET=1: three
@@ -39,6 +39,7 @@ def run(chains, moves):
     lib.vrpms_debug_seg_prof.restype = ctypes.c_int
     lib.vrpms_debug_seg_prof.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     ctx = Context(0)
+    ctx.set_seg_waves(int(os.environ.get("SEG_WAVES", "0")))
     x = synth.x_style(1000, seed=0)
     caps = x.capacities
     if os.environ.get("SEG_PROF_HET"):  # three capacity classes (tools/het_rate.py)
@@ -63,7 +64,7 @@ def run(chains, moves):
         lib.vrpms_debug_seg_prof(buf, NP * 8192, 1)
         a = np.array(buf[:NP * chains], dtype=np.float64).reshape(chains, NP).sum(0)
         st = a[2]
-        mv = st * max(1, moves // 64 // int(os.environ.get("VRPMS_SEG_WAVES", "1"))) / 10
+        mv = st * max(1, moves // 64 // int(os.environ.get("SEG_WAVES", "1"))) / 10
         print(f"{tag}: {steps / dt:,.0f} steps/s/chain | per step: pricing {a[0] / st * 10:.0f} ns, "
               f"rebuild {a[1] / max(a[7], 1) * 10:.0f} ns x {a[7] / st:.3f}/step "
               f"(positions {a[8] / max(a[7], 1) * 10:.0f}, segments {a[9] / max(a[7], 1) * 10:.0f}, "

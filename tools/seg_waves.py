@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""sa_seg_kernel with W wavefronts per chain (VRPMS_SEG_WAVES) on cfg 4
+"""sa_seg_kernel with W wavefronts per chain (VRPMS_OPT_SEG_WAVES) on cfg 4
 (X-1000, K - 1 separators, first-fit starts, windowed 2-opt + swap /
 relocate anywhere): steps per second per chain and moves priced per second
 for W = 1, 2, 4 at each (chains, moves), and a check that every W follows
@@ -27,7 +27,7 @@ for chains, moves in cfgs:
     for w in (1, 2, 4):
         if moves // 64 % w:
             continue
-        os.environ["VRPMS_SEG_WAVES"] = str(w)
+        ctx.set_seg_waves(w)
         r = runners.SARunner(ctx, x.n, chains=chains, total_steps=steps, durations=x.durations,
                              n_sep=x.K - 1, window=32, window_types=2, start="pack", moves=moves)
         r.epoch(20)
@@ -43,4 +43,4 @@ for chains, moves in cfgs:
         print(f"chains {chains} moves {moves} W {w}: {steps / dt:,.0f} steps/s per chain, "
               f"{chains * moves * steps / dt / 1e9:.2f} G moves/s, best {k >> 28 & (2**28 - 1)}, "
               f"same trajectories as W=1: {same}", flush=True)
-os.environ.pop("VRPMS_SEG_WAVES", None)
+ctx.set_seg_waves(0)

@@ -183,6 +183,10 @@ class Context:
         chains), 1 or 2 force."""
         check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_ROUTE_WG_PER_CU, int(wg)))
 
+    def set_seg_waves(self, w: int):
+        """sa_seg_kernel wavefronts per chain: 0 = auto, 1..4 force (A/B)."""
+        check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_SEG_WAVES, int(w)))
+
     def set_ga_fused(self, mode: int):
         """0 = auto (fused one-workgroup-per-island GA when it fits), 2 = three kernels."""
         check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_GA_FUSED, int(mode)))

@@ -260,9 +260,22 @@ int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value) {
     return VRPMS_OK;
   }
   if (option == VRPMS_OPT_WORDS_ILP) {
+#ifdef VRPMS_AB
     if (value < 0 || value > 2)
       return fail(VRPMS_EINVAL, "vrpms_set_option: words ILP must be 0 (auto), 1 or 2");
+#else
+    if (value != 0 && value != 2)
+      return fail(VRPMS_EINVAL,
+                  "vrpms_set_option: words ILP must be 0 (auto) or 2 (the one-candidate-per-lane "
+                  "variant is built only with -DVRPMS_AB)");
+#endif
     ctx->opt_words_ilp = value;
+    return VRPMS_OK;
+  }
+  if (option == VRPMS_OPT_SEG_WAVES) {
+    if (value < 0 || value > 4)
+      return fail(VRPMS_EINVAL, "vrpms_set_option: segment-kernel wavefronts must be 0 (auto) .. 4");
+    ctx->opt_seg_waves = value;
     return VRPMS_OK;
   }
   if (option == VRPMS_OPT_ISLAND_TIMEOUT_S) {

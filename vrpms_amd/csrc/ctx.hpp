@@ -51,7 +51,7 @@ struct vrpms_ctx {
   int opt_split_mode = 0;       // VRPMS_OPT_SPLIT_MODE (0 auto, 2 force branchy)
   int opt_staged_m = 0;         // VRPMS_OPT_STAGED_M (0 auto, 1, 2 or 3)
   int opt_route_wg_per_cu = 0;  // sa_route_kernel workgroups per CU (0 auto, 1, 2)
-  int opt_words_ilp = 0;        // candidates per lane in eval_cvrp_words2 (0 auto, 1, 2 or 3)
+  int opt_words_ilp = 0;        // candidates per lane in eval_cvrp_words2 (0 auto = 2; 1 A/B builds)
   int opt_words_lookahead = 0;  // VRPMS_OPT_WORDS_LOOKAHEAD (words2 gather lookahead, A/B)
   int opt_words_kernel = 0;     // VRPMS_OPT_WORDS_KERNEL (0 auto = words2/rows2, 1 = first generation)
   int opt_ga_fused = 0;          // VRPMS_OPT_GA_FUSED (0 auto, 2 = force the three-kernel GA)
@@ -66,6 +66,7 @@ struct vrpms_ctx {
   void* comm = nullptr;            // ncclComm_t of the island model (vrpms_island_init)
   int comm_rank = 0, comm_world = 1;
   int opt_island_timeout_s = 120;  // VRPMS_OPT_ISLAND_TIMEOUT_S
+  int opt_seg_waves = 0;           // VRPMS_OPT_SEG_WAVES (0 auto, 1..4 force)
 };
 
 namespace vrpms {

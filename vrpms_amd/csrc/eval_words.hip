@@ -311,7 +311,7 @@ int launch_words2(const vrpms_ctx* ctx, const WordsArgs& w, int R, hipStream_t s
   // ILP1/LA1 34.0-35.5 G evals/s.  (Before the fast split, at ~2.5 more
   // VALU per customer, ILP1/LA2 with two workgroups per CU led: 32.5 vs 31.6.)
   const bool two_wg = 2 * lds <= ctx->max_lds;
-  const int ilp = ctx->opt_words_ilp ? ctx->opt_words_ilp : 2;
+  const int ilp = ctx->opt_words_ilp ? ctx->opt_words_ilp : 2;  // 1: A/B builds only
   const int la = ctx->opt_words_lookahead ? ctx->opt_words_lookahead : (two_wg ? 2 : 1);
   // ILP >= 2 needs > 64 VGPRs: one 1024-lane workgroup per CU; ILP1 fits two
   const int per_cu = ilp >= 2 ? 1 : (two_wg ? 2 : 1);
@@ -335,8 +335,16 @@ int launch_words2(const vrpms_ctx* ctx, const WordsArgs& w, int R, hipStream_t s
   using one = std::integral_constant<int, 1>;
   using two = std::integral_constant<int, 2>;
   const bool la2 = la == 2;
-  if (ilp == 2) la2 ? pick(two{}, two{}) : pick(two{}, one{});
-  else la2 ? pick(one{}, two{}) : pick(one{}, one{});
+#ifdef VRPMS_AB
+  // one candidate per lane: measured slower, built only for A/B runs
+  // (VRPMS_OPT_WORDS_ILP = 1 is refused by the shipped library)
+  if (ilp == 1) {
+    la2 ? pick(one{}, two{}) : pick(one{}, one{});
+    VRPMS_HIP(hipGetLastError());
+    return VRPMS_OK;
+  }
+#endif
+  la2 ? pick(two{}, two{}) : pick(two{}, one{});
   VRPMS_HIP(hipGetLastError());
   return VRPMS_OK;
 }

@@ -317,6 +317,22 @@ static ncclResult_t wait_comm(ncclComm_t comm, std::chrono::steady_clock::time_p
   }
 }
 
+// Tear down the context's communicator: a non-blocking one is finalized and
+// polled to completion before it is destroyed (aborted if that fails or does
+// not finish within the deadline).
+static void release_comm(vrpms_ctx* ctx) {
+  if (!ctx->comm) return;
+  ncclComm_t comm = static_cast<ncclComm_t>(ctx->comm);
+  ctx->comm = nullptr;
+  ctx->comm_world = 1;
+  ncclResult_t r = ncclCommFinalize(comm);
+  if (r == ncclSuccess || r == ncclInProgress)
+    r = wait_comm(comm, std::chrono::steady_clock::now() +
+                            std::chrono::seconds(ctx->opt_island_timeout_s));
+  if (r == ncclSuccess) (void)ncclCommDestroy(comm);
+  else (void)ncclCommAbort(comm);
+}
+
 // The pool scratch is grown with a plain hipFree + hipMalloc: hipFree
 // synchronises the device, so work still queued on the caller's stream that
 // reads the old buffer (RCCL receive area, top-E levels) completes first.
@@ -610,8 +626,7 @@ int vrpms_island_init(vrpms_ctx* ctx, const void* unique_id, int32_t rank, int32
     return fail(VRPMS_EINVAL, "vrpms_island_init: need 0 <= rank < world");
   VRPMS_HIP(hipSetDevice(ctx->device));
   if (ctx->comm) {
-    (void)ncclCommDestroy(static_cast<ncclComm_t>(ctx->comm));
-    ctx->comm = nullptr;
+    release_comm(ctx);
   }
   ncclUniqueId id;
   std::memcpy(&id, unique_id, sizeof(id));
@@ -679,9 +694,16 @@ int vrpms_island_exchange(vrpms_ctx* ctx, const vrpms_pool* src, const vrpms_poo
     if (r == ncclInProgress)
       r = wait_comm(comm, std::chrono::steady_clock::now() +
                               std::chrono::seconds(ctx->opt_island_timeout_s));
-    if (r != ncclSuccess)
+    if (r != ncclSuccess) {
+      // a communicator left with an operation pending (or in error) is never
+      // used again: abort it, so later exchanges fall back to the local copy
+      // (world 1) and vrpms_island_world reports 0
+      (void)ncclCommAbort(comm);
+      ctx->comm = nullptr;
+      ctx->comm_world = 1;
       return fail(r == ncclInProgress ? VRPMS_ETIMEOUT : VRPMS_EHIP,
                   std::string("ncclAllGather: ") + ncclGetErrorString(r));
+    }
   } else {
     VRPMS_HIP(hipMemcpyAsync(recv, send, mb, hipMemcpyDeviceToDevice, s));
   }
@@ -695,8 +717,7 @@ int vrpms_island_exchange(vrpms_ctx* ctx, const vrpms_pool* src, const vrpms_poo
 namespace vrpms {
 // called by vrpms_ctx_destroy
 void island_release(vrpms_ctx* ctx) {
-  if (ctx->comm) (void)ncclCommDestroy(static_cast<ncclComm_t>(ctx->comm));
-  ctx->comm = nullptr;
+  release_comm(ctx);
   (void)hipFree(ctx->pool_scratch);
   ctx->pool_scratch = nullptr;
   ctx->pool_scratch_bytes = 0;

@@ -31,7 +31,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdlib>
 
 #include "common.hpp"
 #include "ctx.hpp"
@@ -725,6 +724,20 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
           }
         }
         const uint32_t dspa = T.dsp[ra], dspz = T.dsp[rz], pmxa = T.pmx[ra], smxz = T.smx[rz];
+        // Cut budget (one capacity, the tail after the last changed segment
+        // keeps its customers, the unserved shortcut on): the moved tour has
+        // S + 1 + cuts routes (a cut = a route closed by a customer that did
+        // not fit) and Tt trailing separators, so it serves everyone iff its
+        // cuts <= K - 1 - S + Tt.  Segments outside s0..sH keep their splits
+        // (their cuts: (ra - s0) + (R - rz) - (S - sH)); once the composed
+        // segments' cuts exceed what is left the move's key is the largest
+        // (exactly what the fleet count below would give), so an overflowing
+        // run stops there instead of binary-searching its cuts.  In a tour of
+        // full routes (the cold phase) almost every overflow ends here.
+        const bool tail_kept = en < n && lneS - 1 > sH;
+        const int bud = (!HET && shortcut && tail_kept)
+                            ? (K - 1 - S + Tt) - ((ra - s0) + (R - rz) - (S - sH))
+                            : 0x7fffffff;
 
         SEG_PT(15);
         // the open route and what the composition has closed
@@ -732,8 +745,8 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
         bool c_has = false;
         int c_cnt = 0;
         uint32_t isum = 0, imax = 0;
-        int icnt = 0, seps = 0;
-        bool cust = false;
+        int icnt = 0, seps = 0, cutc = 0;
+        bool cust = false, dead = false;  // dead: the cuts exceeded the budget
         int vo = ra;  // (heterogeneous) the open route's vehicle
         auto close = [&]() __attribute__((always_inline)) {
           const uint32_t d = c_dur + c_pl;
@@ -750,7 +763,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
         // holds a customer
         auto run = [&](const RunP& p, bool rev, uint32_t jv) __attribute__((always_inline)) {
           int x = p.x, y = p.y;
-          if (x > y) return;
+          if (x > y || dead) return;
           seps = 0;
           cust = true;
           if (p.pdy - p.pdx <= capv(vo) - c_load) {  // fits: from the round-3 values
@@ -768,6 +781,11 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
             const bool fits = pdy - pdx <= room;
             int pa = x, pb = y;
             if (!fits) {
+              if (cutc >= bud) {  // one cut more than the fleet allows: no search
+                dead = true;
+                return;
+              }
+              ++cutc;
               // first q in [x - 1, y + 1] with PD[q + 1] > thr, on the monotone
               // PD (one customer: it does not fit, q = x)
               const int thr = rev ? (int)(pdy - room) - 1 : (int)(pdx + room);
@@ -918,10 +936,11 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
         }
         const int Rb = ra + c_cnt + icnt + tcnt;
         int Tb = Tt;
-        const bool tail_kept = en < n && lneS - 1 > sH;
         if (!tail_kept && cust) Tb = seps + (en < n ? n - 1 - en : 0);
         if (full) {
           // (heterogeneous) the tail moved by more than kSegShift vehicles
+        } else if (dead) {
+          k = ~0ull;  // over the cut budget: serves fewer (shortcut on)
         } else if (Rb - Tb <= K) {
           const uint32_t dsum = dspa + c_sum + isum + tsum;
           const uint32_t dmax = max(max(pmxa, tmax), max(imax, c_max));
@@ -1078,6 +1097,10 @@ int launch_sa_seg(const vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* d_cu
       in.K > 65535 || n < 2 || n >= 64 * kSegRegs || n > 65535 || moves % 64 != 0 ||
       moves / 64 > kSegMaxMoves)
     return 1;
+  // the prefix demands PD are u32 and the capacity cuts compare them (and
+  // PD + a capacity) as int32: the total demand plus a capacity must stay
+  // below 2^31, else the full re-evaluation kernels price the moves
+  if ((int64_t)(in.N - 1) * (int64_t)in.max_dem + (int64_t)in.max_cap >= (int64_t)1 << 31) return 1;
   const bool het = !in.uniform_cap;
   SearchInst si = search_inst(ctx);
   si.mat_lds = 0;  // the matrix stays in L2: a move gathers <= 4 entries
@@ -1093,7 +1116,7 @@ int launch_sa_seg(const vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* d_cu
   // chains' wavefronts stay resident (two per SIMD at this kernel's VGPRs)
   int W = std::min(moves / 64, kSegMaxWaves);
   while (W > 1 && (int64_t)p->chains * W > 8 * (int64_t)ctx->num_cus) W >>= 1;
-  if (const char* e = std::getenv("VRPMS_SEG_WAVES")) W = std::max(1, std::min(atoi(e), kSegMaxWaves));
+  if (ctx->opt_seg_waves > 0) W = std::min(ctx->opt_seg_waves, kSegMaxWaves);  // A/B
   while (W > 1 && (moves / 64) % W != 0) --W;
   int cpw = 4;
   // fewer chains than 4 per CU: spread them, one wavefront per workgroup

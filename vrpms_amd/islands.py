@@ -61,13 +61,26 @@ def init_comm(ctx, group=None, timeout_s: int | None = None) -> int:
     if timeout_s is not None:
         ctx.set_island_timeout(timeout_s)
     err = None
-    try:
-        obj = [ctx.island_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0, group=group)
-        ctx.island_init(obj[0], rank, world)
-        ok = int(ctx.island_world() == world)
-    except Exception as e:  # noqa: BLE001 -- reported after the agreement
-        ok, err = 0, e
+    # rank 0 always reaches the broadcast: a failed unique id travels as None
+    # (every rank then skips island_init), so no rank is left waiting in a
+    # collective the others never enter before the agreement below
+    uid = None
+    if rank == 0:
+        try:
+            uid = ctx.island_unique_id()
+        except Exception as e:  # noqa: BLE001 -- reported after the agreement
+            err = e
+    obj = [uid]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    ok = 0
+    if obj[0] is None:
+        err = err or RuntimeError("rank 0 could not create the RCCL unique id")
+    else:
+        try:
+            ctx.island_init(obj[0], rank, world)
+            ok = int(ctx.island_world() == world)
+        except Exception as e:  # noqa: BLE001 -- reported after the agreement
+            ok, err = 0, e
     if not _agree(ok, group, getattr(ctx, "dev", None)):
         ctx.island_comm_group = None
         raise RuntimeError(f"vrpms_island_init failed on at least one rank "

@@ -41,23 +41,43 @@ def _post(base: str, problem: str, algorithm: str, body: dict, timeout: float) -
     return out["message"]
 
 
+# knobs the GPU box's /solve route honours (App.solve_inline); anything else
+# would be silently ignored there, so it is refused here instead
+_FORWARDED = {"random_permutation_count": "randomPermutationCount",
+              "iteration_count": "iterationCount"}
+
+
+def _options(body: dict, seed, time_limit, knobs: dict, objective=None):
+    extra = sorted(k for k in knobs if k not in _FORWARDED)
+    if extra:
+        raise ValueError(f"remote solve: unsupported argument(s) {extra} "
+                         f"(forwarded: seed, time_limit, objective, {sorted(_FORWARDED)})")
+    for k, name in _FORWARDED.items():
+        if knobs.get(k):
+            body[name] = int(knobs[k])
+    body["seed"] = int(seed)
+    if time_limit is not None:
+        body["timeLimit"] = float(time_limit)
+    if objective is not None:
+        body["objective"] = str(objective)
+    return body
+
+
 def solve_tsp(algorithm, durations, customers, start_node, start_time=0, *, base=None,
-              timeout: float = 600.0, **_):
+              timeout: float = 600.0, seed: int = 0, time_limit=None, **knobs):
     """solver.solve_tsp on the GPU box -> {'duration', 'vehicle'}."""
-    return _post(base or url(), "tsp", algorithm,
-                 {"durations": durations, "customers": list(customers or []),
-                  "startNode": start_node, "startTime": start_time}, timeout)
+    body = {"durations": durations, "customers": list(customers or []),
+            "startNode": start_node, "startTime": start_time}
+    return _post(base or url(), "tsp", algorithm, _options(body, seed, time_limit, knobs), timeout)
 
 
 def solve_vrp(algorithm, durations, locations, capacities, start_times, ignored_customers=(),
-              completed_customers=(), *, base=None, timeout: float = 600.0, **knobs):
+              completed_customers=(), *, base=None, timeout: float = 600.0, seed: int = 0,
+              objective: str = "sum", time_limit=None, **knobs):
     """solver.solve_vrp on the GPU box -> {'durationMax', 'durationSum', 'vehicles'}."""
     body = {"durations": durations, "locations": list(locations or []),
             "capacities": list(capacities), "startTimes": list(start_times),
             "ignoredCustomers": list(ignored_customers or []),
             "completedCustomers": list(completed_customers or [])}
-    if knobs.get("random_permutation_count"):
-        body["randomPermutationCount"] = int(knobs["random_permutation_count"])
-    if knobs.get("iteration_count"):
-        body["iterationCount"] = int(knobs["iteration_count"])
-    return _post(base or url(), "vrp", algorithm, body, timeout)
+    return _post(base or url(), "vrp", algorithm,
+                 _options(body, seed, time_limit, knobs, objective), timeout)

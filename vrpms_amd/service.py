@@ -288,12 +288,15 @@ class App:
         return ci if TspBatcher.accepts(ci) else None
 
     def _gpu_solve(self, problem, algorithm, params, knobs, locations, durations):
+        """knobs may carry "seed", "time_limit" and "objective" (the /solve
+        route's options, vrpms_amd.remote); the endpoints use the app's."""
         from . import solver
+        seed = int(knobs.get("seed", self.seed))
+        tl = knobs.get("time_limit", self.max_seconds)
         if problem == "tsp":
             return solver.solve_tsp(algorithm, durations, params["customers"],
                                     params["start_node"], params["start_time"] or 0,
-                                    seed=self.seed, time_limit=self.max_seconds,
-                                    device=self.device)
+                                    seed=seed, time_limit=tl, device=self.device)
         extra = {}
         if knobs.get("random_permutationCount"):
             extra["random_permutation_count"] = int(knobs["random_permutationCount"])
@@ -301,8 +304,9 @@ class App:
             extra["iteration_count"] = int(knobs["iteration_count"])
         return solver.solve_vrp(algorithm, durations, locations, params["capacities"],
                                 params["start_times"], params["ignored_customers"],
-                                params["completed_customers"], seed=self.seed,
-                                time_limit=self.max_seconds, device=self.device, **extra)
+                                params["completed_customers"], seed=seed,
+                                objective=knobs.get("objective", "sum"),
+                                time_limit=tl, device=self.device, **extra)
 
     def post(self, problem: str, algorithm: str, raw: bytes):
         """-> (status, response dict) for a POST body."""
@@ -386,6 +390,21 @@ class App:
             knobs = {"random_permutationCount": content.get("randomPermutationCount"),
                      "iteration_count": content.get("iterationCount")}
             locations = vals["locations"]
+        # the remote front-end's options (vrpms_amd.remote): seed, time limit
+        # (capped by the box's own), objective
+        try:
+            if "seed" in content:
+                knobs["seed"] = int(content["seed"])
+            if content.get("timeLimit") is not None:
+                tl = float(content["timeLimit"])
+                knobs["time_limit"] = tl if self.max_seconds is None else min(tl, self.max_seconds)
+            if problem == "vrp" and "objective" in content:
+                if content["objective"] not in ("sum", "max"):
+                    raise ValueError("objective must be 'sum' or 'max'")
+                knobs["objective"] = content["objective"]
+        except (TypeError, ValueError) as e:
+            return 400, {"success": False,
+                         "errors": [{"what": "Invalid request", "reason": str(e)}]}
         try:
             with self.gpu_lock:
                 result = self._solve(problem, algorithm, params, knobs, locations,

@@ -237,7 +237,8 @@ def solve_tsp(algorithm: str, durations, customers, start_node, start_time=0, *,
     """Result dict of the TSP TODO slot (api/tsp/ga/index.py:40-44)."""
     rem = _remote()
     if rem is not None:
-        return rem.solve_tsp(algorithm, durations, customers, start_node, start_time)
+        return rem.solve_tsp(algorithm, durations, customers, start_node, start_time, seed=seed,
+                             time_limit=time_limit, **knobs)
     ci = compact_tsp(durations, customers, start_node, start_time)
     ctx = context(device)
     load(ctx, ci)
@@ -255,7 +256,8 @@ def solve_vrp(algorithm: str, durations, locations, capacities, start_times,
     rem = _remote()
     if rem is not None:
         out = rem.solve_vrp(algorithm, durations, locations, capacities, start_times,
-                            ignored_customers, completed_customers, **knobs)
+                            ignored_customers, completed_customers, seed=seed,
+                            objective=objective, time_limit=time_limit, **knobs)
         if with_unvisited:   # the served customers' complement (the remote answers the slot dict)
             served = {c for v in out["vehicles"] for c in v["tour"][1:-1]}
             nodes = [0] + active_customers(list(locations or []), ignored_customers,
