@@ -475,14 +475,40 @@ def other_configs(ctx, torch, dev, seed=0, r_lds=None):
                                            "frac": mev * 8 / r_lds if r_lds else None}}
     del mats
     try:
-        out["cfg5_api"] = cfg5_api_leg(torch, dev, R=R, steps=steps, seed=seed)
+        out["cfg5_api"] = cfg5_api_pool_leg(R=R, steps=steps)
     except Exception:
         out["cfg5_api"] = {"error": traceback.format_exc(limit=3)}
+    try:
+        out["cfg5_api_one_process"] = cfg5_api_leg(torch, dev, R=R, steps=steps, seed=seed)
+    except Exception:
+        out["cfg5_api_one_process"] = {"error": traceback.format_exc(limit=3)}
+    return out
+
+
+def cfg5_api_pool_leg(R=10000, steps=1000):
+    """Config 5 at the API across processes (vrpms_amd.frontends.FrontEndPool):
+    front-end worker processes parse / ingest / answer the R /api/tsp/sa
+    requests and feed one GPU-owner process through shared memory.  This
+    process has initialised the GPU, so the pool runs as a child program
+    (forked workers must come from a process that has not); its own clock
+    brackets the R requests, and it checks a sample of the answers'
+    durations against their tours (A4)."""
+    import subprocess
+    threads, cores = host_cores()
+    workers = max(2, threads - 2)        # the parent and the GPU owner keep a core each
+    cmd = [sys.executable, "-m", "vrpms_amd.frontends", "bench", "--requests", str(R),
+           "--workers", str(workers), "--steps", str(steps)]
+    res = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    if res.returncode != 0:
+        return {"error": f"exit {res.returncode}", "stderr": res.stderr[-2000:]}
+    out = json.loads(res.stdout.strip().splitlines()[-1])
+    out["host_cores"] = cores
     return out
 
 
 def cfg5_api_leg(torch, dev, R=10000, steps=1000, workers=256, seed=0, N=50):
-    """Config 5 at the API: R concurrent /api/tsp/sa requests (the reference's
+    """Config 5 at the API in ONE process (the GIL-bound contrast to
+    cfg5_api_pool_leg): R concurrent /api/tsp/sa requests (the reference's
     request body, api/tsp/sa/index.py:40-44; each its own random symmetric
     50-node matrix served as the DB's JSON nested lists) posted in-process
     to service.App from a `workers`-thread pool; TspBatcher coalesces them

@@ -558,9 +558,12 @@ int oracle_max_threads(void) {
  * a walk state equal to the current state at src(q) stays equal to the end
  * of the run: the walk jumps there, adding the routes the current tour
  * closes in between (prefix sums of route durations, a sparse table for
- * their maximum).  A walk that would reach the K-th vehicle, a current tour
- * that exhausts the fleet, a non-uniform fleet and TSP fall back to the full
- * walk (tour_key), so every key equals tour_key's.
+ * their maximum).  A fleet of different vehicles (per-vehicle capacities or
+ * start times, api/parameters.py:11-12) re-synchronises only on the same
+ * vehicle too (w.k == k[src(q)]): the future then runs on the same vehicles
+ * from the same state.  A walk that would reach the K-th vehicle, a current
+ * tour that exhausts the fleet and TSP fall back to the full walk
+ * (tour_key), so every key equals tour_key's.
  * ---------------------------------------------------------------------- */
 typedef struct {
   int64_t load, t, s, mx;
@@ -699,7 +702,7 @@ static inline int walk_jump(const split_t* S, walk_t* w, int a, int b, int K) {
  * counted exactly -- it cannot win over a feasible move, and a winner that
  * is infeasible is rejected either way (as on the device). */
 static uint64_t resync_key(const inst_t* I, const uint16_t* T, int n, const move_t* m,
-                           const split_t* S, int hopeless) {
+                           const split_t* S, int hopeless, int uniform) {
   int i = m->i, j = m->j;
   int lo = i < j ? i : j;
   /* runs of the moved tour that read the current tour contiguously:
@@ -734,7 +737,9 @@ static uint64_t resync_key(const inst_t* I, const uint16_t* T, int n, const move
     while (run < nr && re[run] < q) ++run;
     if (run < nr && q >= rs[run] && q < re[run] && w.k < I->K) {
       const int c = q + ro[run];
-      if (S->k[c] < I->K && w.load == S->load[c] && w.t == S->t[c] && w.prev == S->prev[c]) {
+      /* a fleet of different vehicles: the same state on the same vehicle */
+      if (S->k[c] < I->K && w.load == S->load[c] && w.t == S->t[c] && w.prev == S->prev[c] &&
+          (uniform || w.k == S->k[c])) {
         const int b = walk_jump(S, &w, c, re[run] + ro[run], I->K);
         if (b < 0) return hopeless ? ~0ull : tour_key(I, T, n, m);
         q = b - ro[run];
@@ -1010,7 +1015,7 @@ int oracle_sa_run_resync(int problem, const int32_t* D, int H, int N, const int3
                          int threads, int moves) {
   int uniform = problem == 1 && K > 0;
   for (int k = 1; uniform && k < K; ++k) uniform = cap[k] == cap[0] && st[k] == st[0];
-  if (!uniform || n < 2)
+  if (problem != 1 || K <= 0 || n < 2)
     return oracle_sa_run(problem, D, H, N, dem, cap, st, K, objective, cur, cur_key, best,
                          best_key, chains, n, steps, inv_t0, inv_alpha, seed, step0, window,
                          window_types, threads, moves);
@@ -1023,6 +1028,7 @@ int oracle_sa_run_resync(int problem, const int32_t* D, int H, int N, const int3
   for (int a = 0; sym && a < N; ++a)
     for (int b = a + 1; sym && b < N; ++b) sym = D[(int64_t)a * N + b] == D[(int64_t)b * N + a];
   for (int c = 1; sym && c < N; ++c) sym = dem[c] <= cap[0];
+  sym = sym && uniform; /* segment pricing: one capacity (seg_key reads cap[0]) */
   int clevels = 1;
   while ((1 << clevels) <= n + 2) ++clevels;
 #ifdef _OPENMP
@@ -1088,7 +1094,8 @@ int oracle_sa_run_resync(int problem, const int32_t* D, int H, int N, const int3
             kk = seg_key(&I, A, &C, &m, hopeless, &unserved);
             if (unserved) kk = hopeless ? ~0ull : tour_key(&I, A, n, &m);
           } else {
-            kk = S.alive ? resync_key(&I, A, n, &m, &S, hopeless) : tour_key(&I, A, n, &m);
+            kk = S.alive ? resync_key(&I, A, n, &m, &S, hopeless, uniform)
+                         : tour_key(&I, A, n, &m);
           }
           if (kk < kbest) {
             kbest = kk;

@@ -16,14 +16,28 @@ from . import spec
 
 class Tables:
     """Greedy-split routes of tour A with unlimited vehicles: rs (first
-    position), dur, cus (holds a customer), rid (route of each position)."""
+    position), dur, cus (holds a customer), rid (route of each position).
+
+    D: [N][N] static or [H][N][N] hour-indexed (A3).  cap / st0: one value
+    (an exchangeable fleet) or one per vehicle (api/parameters.py:11-12);
+    route r runs on vehicle min(r, K - 1) -- past the fleet the routes serve
+    no one and the fleet count (X below) rejects the tour."""
 
     def __init__(self, D, A, dem, cap, st0):
-        self.D, self.dem, self.cap, self.st0 = D, dem, cap, st0
+        D = np.asarray(D)
+        self.D = D if D.ndim == 3 else D[None]
+        self.H = self.D.shape[0]
+        self.dem = dem
+        self.caps = [int(c) for c in np.atleast_1d(cap)]
+        self.sts = [int(t) for t in np.atleast_1d(st0)]
+        K = max(len(self.caps), len(self.sts))
+        self.caps += [self.caps[-1]] * (K - len(self.caps))
+        self.sts += [self.sts[-1]] * (K - len(self.sts))
+        self.uniform = len(set(self.caps)) == 1 and len(set(self.sts)) == 1
         self.A = list(A)
         n = len(A)
         rs, dur, cus, rid = [0], [], [], [0] * n
-        w = Walk(self)
+        w = Walk(self, 0)
         for q, c in enumerate(A):
             if c == 0:
                 rid[q] = len(dur)
@@ -32,7 +46,7 @@ class Tables:
                 cus.append(cu)
                 rs.append(q + 1)
                 continue
-            if w.load + dem[c] > cap:
+            if w.load + dem[c] > w.cap:
                 cu = w.prev != 0
                 dur.append(w.close())
                 cus.append(cu)
@@ -61,33 +75,57 @@ class Tables:
         for r in range(self.R):
             self.lnb.append(r if cus[r] else self.lnb[-1])
 
+    def cap_of(self, v):
+        return self.caps[min(v, len(self.caps) - 1)]
+
+    def st_of(self, v):
+        return self.sts[min(v, len(self.sts) - 1)]
+
+    def edge(self, t, a, b):
+        return int(self.D[(t // 60) % self.H, a, b])
+
 
 class Walk:
-    def __init__(self, T):
+    """The greedy split from a route start on vehicle v (its capacity and
+    start time)."""
+
+    def __init__(self, T, v=0):
         self.T = T
-        self.load, self.t, self.prev = 0, T.st0, 0
+        self.v = v
+        self.load, self.t, self.prev = 0, T.st_of(v), 0
+        self.cap = T.cap_of(v)
         self.cnt = self.ds = self.dm = 0
         self.xs = -1
 
     def close(self):
         rd = 0
         if self.prev:
-            self.t += int(self.T.D[self.prev, 0])
-            rd = self.t - self.T.st0
+            self.t += self.T.edge(self.t, self.prev, 0)
+            rd = self.t - self.T.st_of(self.v)
             self.ds += rd
             self.dm = max(self.dm, rd)
         self.cnt += 1
-        self.load, self.t, self.prev = 0, self.T.st0, 0
+        self.v += 1
+        self.load, self.t, self.prev = 0, self.T.st_of(self.v), 0
+        self.cap = self.T.cap_of(self.v)
         return rd
 
     def closes(self, c):
-        return c == 0 or self.load + self.T.dem[c] > self.T.cap
+        return c == 0 or self.load + self.T.dem[c] > self.cap
 
-    def in_step(self, c):
-        return self.prev == 0 or (c != 0 and self.load + self.T.dem[c] > self.T.cap)
+    def in_step(self, c, r=None):
+        """Back in step with the current tour at a position where its route r
+        starts: the walk is at a route start too (fresh, or c does not fit);
+        on a fleet of different vehicles also on route r's vehicle."""
+        nofit = c != 0 and self.load + self.T.dem[c] > self.cap
+        if not (self.prev == 0 or nofit):
+            return False
+        if self.T.uniform or r is None:
+            return True
+        return (self.v + 1 if self.prev != 0 else self.v) == r
 
     def add(self, c):
-        self.t += int(self.T.D[self.prev, c])
+        self.t += self.T.edge(self.t, self.prev, c)
         self.load += self.T.dem[c]
         self.prev = c
         self.xs = self.cnt
@@ -96,7 +134,10 @@ class Walk:
 def price(T: Tables, m, K: int, objective: int = 0):
     """Composed key of tour T.A moved by m = (typ, i, j), or None when the
     moved tour leaves a customer unserved (the kernel then re-evaluates in
-    full or uses the largest key)."""
+    full or uses the largest key).  A fleet of different vehicles
+    re-synchronises only on the same vehicle (Walk.in_step), so every zone
+    that re-synchronises keeps its route count (d1 = d2 = 0) and one that
+    does not is walked to the end of the tour."""
     typ, i, j = m
     A, n = T.A, len(T.A)
     mv = _moved(A, m)
@@ -116,25 +157,25 @@ def price(T: Tables, m, K: int, objective: int = 0):
     Z2 = T.rs[r2s] + dl
     two = typ != spec.MOVE_2OPT and Z2 > bq0
     phase = 1 if two else 3
-    w, w1 = Walk(T), Walk(T)
+    w, w1 = Walk(T, r1s), Walk(T, r1s)
     r1e, r2e = 0, T.R
     q = P1
     while q < n:
         c = mv[q]
         if phase == 1 and q >= bq0:
             qo = q - dl
-            if T.rs[T.rid[qo]] == qo and w.in_step(c):
+            if T.rs[T.rid[qo]] == qo and w.in_step(c, T.rid[qo]):
                 if w.prev:
                     w.close()
                 w1, r1e = w, T.rid[qo]
-                w = Walk(T)
+                w = Walk(T, r2s + w1.cnt - (r1e - r1s))
                 phase = 2
                 q = Z2
                 continue
             if q == Z2:
                 phase = 3
         if phase >= 2 and q > hi:
-            if T.rs[T.rid[q]] == q and w.in_step(c):
+            if T.rs[T.rid[q]] == q and w.in_step(c, T.rid[q]):
                 if w.prev:
                     w.close()
                 r2e = T.rid[q]
@@ -147,7 +188,7 @@ def price(T: Tables, m, K: int, objective: int = 0):
     if q >= n:
         w.close()
     if phase != 2:
-        w1, w = w, Walk(T)
+        w1, w = w, Walk(T, T.R)
         r1e = r2s = r2e
     d1 = w1.cnt - (r1e - r1s)
     d2 = w.cnt - (r2e - r2s)

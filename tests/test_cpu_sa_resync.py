@@ -89,3 +89,30 @@ def test_resync_cold_cut_budget(n_sep_off):
     small = synth.cvrp(120, 10, seed=6)
     P = _starts(small, 6, small.K - n_sep_off, "pack", 2)
     _both(small, P, 400, 1 / 5.0, 1.0, 19)
+
+
+def _het(inst, fracs, starts=True):
+    import dataclasses
+    K = len(inst.capacities)
+    base = int(inst.capacities[0])
+    caps = np.array([max(int(base * fracs[k * len(fracs) // K]), int(inst.demand.max()))
+                     for k in range(K)], dtype=np.int64)
+    st = (np.arange(K, dtype=np.int64) * 37 % 240 + 420) if starts else inst.start_times
+    return dataclasses.replace(inst, capacities=caps, start_times=st)
+
+
+@pytest.mark.parametrize("hot", [False, True])
+def test_resync_heterogeneous_td(hot):
+    """Hour-indexed TD-200 x 24 with staggered start times and three capacity
+    classes (the reference's request shape, api/parameters.py:11-12): the walk
+    re-synchronises only on the same vehicle; same trajectories as the full
+    walk."""
+    inst = _het(synth.td_cvrp(200, 16, seed=3), (1.3, 1.0, 0.8))
+    P = _starts(inst, 4, inst.K - 1, "pack", 2)
+    _both(inst, P, 200, 1 / (1e6 if hot else 60.0), 1 / 0.99, 5, window=16, types=2)
+
+
+def test_resync_heterogeneous_static_full_range():
+    inst = _het(synth.cvrp(150, 12, seed=4, slack=1.2), (1.4, 0.9), starts=False)
+    P = _starts(inst, 4, inst.K - 1, "random", 3)
+    _both(inst, P, 300, 1 / 80.0, 1 / 0.99, 6)

@@ -1,0 +1,101 @@
+"""FrontEndPool (vrpms_amd/frontends.py, cfg 5 at the API across processes)
+on the CPU: forked front-end workers feed two stand-in GPU owners ("fake
+devices") through the shared-memory arena, round-robin; the answers follow
+App.post's contract (api/tsp/sa/index.py) request for request."""
+import json
+import multiprocessing as mp
+
+import numpy as np
+import pytest
+
+from vrpms_amd import frontends, service, synth
+
+
+def _store(R, N, seed=0):
+    rng = np.random.default_rng(seed)
+    return service.MemoryStore({0: [{"id": i} for i in range(N)]},
+                               {i: synth.random_symmetric(N, rng).tolist() for i in range(R)},
+                               {"tok": "a@b.c"})
+
+
+def _body(i, N, **kw):
+    b = {"solutionName": "n", "solutionDescription": "d", "locationsKey": 0, "durationsKey": i,
+         "customers": list(range(1, N)), "startNode": 0, "startTime": 0}
+    b.update(kw)
+    return json.dumps(b).encode()
+
+
+def _stand_in(counts):
+    """Launch factory: the identity tour of each request, its exact
+    duration; counts[dev] += requests launched on dev."""
+    def factory(dev):
+        def launch(N, host):
+            with counts.get_lock():
+                counts[dev] += host.shape[0]
+            R = host.shape[0]
+            tours = np.tile(np.arange(1, N, dtype=np.int16), (R, 1))
+            path = np.arange(N + 1) % N
+            durs = host[:, path[:-1], path[1:]].sum(axis=1).astype(np.int64)
+            return tours, durs
+        return launch
+    return factory
+
+
+def _fake_app(store):
+    def factory(dev):
+        def solve(problem, algorithm, params, knobs, locations, durations):
+            D = np.asarray(durations)
+            n = D.shape[0]
+            return {"duration": int(sum(D[i, (i + 1) % n] for i in range(n))),
+                    "vehicle": list(range(n)) + [0]}
+        return service.App(store, device=dev, solve=solve)
+    return factory
+
+
+def test_pool_round_robin_two_devices_matches_app_contract():
+    N, R = 12, 240
+    store = _store(R, N)
+    counts = mp.get_context("fork").Array("l", 2)
+    bodies = [_body(i, N) for i in range(R)]
+    bodies[5] = b"{not json"
+    bodies[6] = json.dumps({"durationsKey": 1}).encode()           # missing parameters
+    bodies[7] = _body(10**6, N)                                    # no such matrix
+    bodies[8] = _body(8, N, auth="tok")                            # saved
+    bodies[9] = _body(9, N, auth="bad")                            # not permitted
+    bodies[10] = _body(10, N, customers=[1, 2, 99])                # outside the matrix
+    ref_app = _fake_app(store)(0)
+    with frontends.FrontEndPool(store, workers=3, devices=(0, 1), slots_per_worker=32, nmax=16,
+                                chunk=16, launch_factory=_stand_in(counts),
+                                app_factory=_fake_app(store)) as pool:
+        res = pool.post_many("tsp", "sa", bodies)
+        # another endpoint: not batchable, the owners' App.post
+        ga = pool.post_many("tsp", "ga", [_body(3, N)])
+    assert len(res) == R
+    for i in (5, 6, 7, 9, 10):
+        st, body = res[i]
+        want = ref_app.post("tsp", "sa", bodies[i]) if i != 10 else None
+        assert st == 400 and not body["success"]
+        if want is not None:
+            assert (st, body) == want, i
+    assert "outside" in res[10][1]["errors"][0]["reason"]
+    path = list(range(1, N)) + [0]
+    for i, (st, body) in enumerate(res):
+        if i in (5, 6, 7, 9, 10):
+            continue
+        assert st == 200, (i, body)
+        D = np.asarray(store.durations[i])
+        assert body["message"]["vehicle"] == [0] + path
+        assert body["message"]["duration"] == int(D[[0] + path[:-1], path].sum())
+    # both fake devices launched, the batches split between them
+    c = list(counts)
+    assert c[0] > 0 and c[1] > 0 and c[0] + c[1] == R - 4   # 9 is solved, then refused a save
+    # the auth request's solution reached the parent's store, once
+    assert len(store.solutions) == 1 and store.solutions[0]["owner"] == "a@b.c"
+    assert store.solutions[0]["duration"] == res[8][1]["message"]["duration"]
+    st, body = ga[0]
+    assert st == 200 and body["message"]["vehicle"][0] == 0
+
+
+def test_pool_rejects_empty_configuration():
+    with pytest.raises(ValueError):
+        frontends.FrontEndPool(_store(1, 5), workers=0)

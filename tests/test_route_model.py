@@ -142,3 +142,44 @@ def test_segment_pricing_heterogeneous_fleet(nn, classes, shuffle, window, obj):
                 T = rmod.SegTables(D, A, dem, caps)
     assert checked > 30 and checked + none + full == 900
     assert full < 30, full
+
+
+@pytest.mark.parametrize("nn,classes,staggered,td,obj", [
+    (60, (1.3, 1.0, 0.8), True, True, 0), (80, (1.0, 1.4), False, True, 1),
+    (70, (1.2, 0.9, 1.0), True, False, 0), (50, (1.0,), True, True, 0)])
+def test_route_pricing_heterogeneous_td(nn, classes, staggered, td, obj):
+    """Route-local pricing on a fleet of different vehicles (per-vehicle
+    capacities in classes, staggered start times) and hour-indexed matrices
+    (api/parameters.py:11-12, src/solver.py:7): a walk re-synchronises only
+    on the same vehicle, so the key equals eval_cvrp's on random moves and is
+    None exactly when a customer is unserved."""
+    rng = np.random.default_rng(nn * 3 + len(classes))
+    checked = none = 0
+    for trial in range(3):
+        inst = synth.td_cvrp(nn, max(3, nn // 10), seed=trial + nn) if td else \
+            synth.cvrp(nn, max(3, nn // 10), seed=trial + nn, slack=1.3)
+        K = len(inst.capacities)
+        base = int(inst.capacities[0]) * 1.3      # room for the small class
+        dem = [int(x) for x in inst.demand]
+        caps = [max(int(base * classes[k * len(classes) // K]), max(dem)) for k in range(K)]
+        st = [int(x) for x in (np.arange(K) * 37 % 240 + 420)] if staggered else \
+            [int(inst.start_times[0])] * K
+        perm = rng.permutation(np.arange(1, nn + 1))
+        A = [int(x) for x in spec.pack_separators(perm, K - 1, dem, caps)]
+        for _ in range(150):
+            n = len(A)
+            r = [int(x) for x in rng.integers(0, 2**32, size=3, dtype=np.uint64)]
+            typ, i, j = spec.decode_move_window(r[0], r[1], r[2], n, 6 if trial else 0, 2)
+            T = rmod.Tables(inst.durations, A, dem, caps, st)
+            got = rmod.price(T, (typ, i, j), K, obj)
+            mv = rmod._moved(A, (typ, i, j))
+            ref = spec.eval_cvrp(inst.durations, mv, inst.demand, caps, st, obj)
+            if ref["unvisited"] == 0:
+                assert got == ref["key"], (trial, typ, i, j)
+                checked += 1
+            else:
+                assert got is None, (trial, typ, i, j)
+                none += 1
+            if ref["unvisited"] == 0 or rng.random() < 0.2:
+                A = mv
+    assert checked > 60, (checked, none)

@@ -206,6 +206,22 @@ ROUTE_CASES = [
      32, 0),
     ("cvrp300_asym_i32", lambda: _asym(synth.cvrp(300, 24, seed=8), 2, scale=60), "pack", 8, 120,
      1 / 18000.0, 24, 0),
+    # fleets of different vehicles (api/parameters.py:11-12): three capacity
+    # classes and staggered start times on the hour-indexed TD-200 x 24 (the
+    # reference's normal VRP request), shuffled classes hot, and static
+    # asymmetric matrices (the segment kernel needs a symmetric one): walks
+    # re-synchronise on the same vehicle only
+    ("td200_het_classes_starts", lambda: _starts(_classes(synth.td_cvrp(200, 16, seed=21),
+                                                          (1.3, 1.0, 0.8))), "pack", 8, 60,
+     1 / 200.0, 16, 2),
+    ("td200_het_shuffled_hot", lambda: _classes(synth.td_cvrp(200, 16, seed=22), (1.2, 0.9),
+                                                shuffle=True), "pack", 8, 40, 1e-7, 16, 0),
+    ("x1000_asym_het_starts", lambda: _starts(_classes(_asym(synth.x_style(1000, seed=23), 1),
+                                                       (1.4, 1.1, 0.9))), "pack", 8, 120,
+     1 / 300.0, 32, 2),
+    ("cvrp150_asym_het_random", lambda: _classes(_asym(synth.cvrp(150, 12, seed=24, slack=1.3), 2),
+                                                 (1.3, 0.8), shuffle=True), "random", 8, 60,
+     1 / 100.0, 8, 0),
 ]
 
 
@@ -258,6 +274,8 @@ MULTIWAVE_CASES = [
     ("cvrp150_hot", 128),
     ("cvrp200_no_seps", 192),
     ("x1000_asym_u16", 512),
+    ("td200_het_classes_starts", 256),
+    ("x1000_asym_het_starts", 128),
 ]
 
 

@@ -248,6 +248,8 @@ def test_remote_front_end_over_http(monkeypatch):
     seen = []
 
     def fake_solve(problem, algorithm, params, knobs, locations, durations):
+        assert knobs.get("device") == 0      # the app's one device
+        knobs = {k: v for k, v in knobs.items() if k != "device"}
         seen.append((problem, algorithm, params, knobs, locations, durations))
         if problem == "tsp":
             return {"duration": 24, "vehicle": [0, 1, 2, 3, 0]}
@@ -289,3 +291,47 @@ def test_remote_front_end_over_http(monkeypatch):
     finally:
         srv.shutdown()
         srv.server_close()
+
+
+def test_multi_device_scheduling_and_batcher_round_robin():
+    """App(devices=[0, 1]): small requests take a free device each, a large
+    SA request takes both (the island model), and TspBatcher launches go to
+    the devices round-robin (replicas only); stand-ins record where they ran."""
+    import threading
+    import time
+
+    seen = []
+    gate = threading.Event()
+
+    def fake_solve(problem, algorithm, params, knobs, locations, durations):
+        seen.append((algorithm, knobs.get("device"), knobs.get("devices")))
+        if algorithm == "ga":
+            gate.wait(5)      # hold the first device while the next request arrives
+        return {"duration": 1, "vehicle": [0, 1, 0]}
+
+    launched = []
+
+    def fake_launch(N, cis, device):
+        launched.append((device, len(cis)))
+        return [list(range(1, N)) for _ in cis]
+
+    app = service.App(store(), devices=[0, 1], solve=fake_solve, island_min_n=3,
+                      batch_tsp=True, batch_window_s=0.001, batch_launch=fake_launch)
+    body = json.dumps(FULL["tsp"]).encode()
+    th = threading.Thread(target=app.post, args=("tsp", "ga", body))
+    th.start()
+    time.sleep(0.2)
+    app.post("tsp", "aco", body)               # device 0 is busy: device 1
+    gate.set()
+    th.join()
+    assert seen[0] == ("ga", 0, None) and seen[1] == ("aco", 1, None)
+    big = dict(FULL["tsp"], customers=[1, 2, 3, 1])   # 4 > island_min_n customers
+    app.post("tsp", "bf", json.dumps(big).encode())    # brute force: one device
+    app.post("tsp", "ga", json.dumps(big).encode())    # both: islands
+    assert seen[2][2] is None and seen[3][2] == [0, 1]
+    # the batcher alternates devices launch by launch
+    for _ in range(4):
+        st, b = app.post("tsp", "sa", body)
+        assert st == 200
+    assert [d for d, _ in launched] == [0, 1, 0, 1]
+    assert app.batcher.per_device == {0: 2, 1: 2}

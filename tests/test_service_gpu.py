@@ -1,6 +1,7 @@
 """HTTP host with the GPU solver in the slot: the 8 endpoints answer the
 reference's request bodies with real solutions, and saves carry them."""
 import json
+import os
 
 import pytest
 
@@ -71,3 +72,22 @@ def test_tsp_batcher_on_gpu():
         assert status == 200
         msg = resp["message"]
         assert msg["duration"] == 24 and sorted(msg["vehicle"][1:-1]) == [1, 2, 3]
+
+
+@pytest.mark.gpu
+def test_frontend_pool_cfg5_api_on_gpu():
+    """cfg 5 at the API across processes (vrpms_amd.frontends): forked
+    front-end workers + a GPU-owner process running vrpms_tsp_batch_sa.  The
+    pool runs as a child program (this test process may already hold the
+    GPU); every answer is a 200 and a sample's durations equal their tours'
+    closed-tour costs."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = subprocess.run([sys.executable, "-m", "vrpms_amd.frontends", "bench", "--requests",
+                          "3000", "--workers", "4", "--steps", "300"], cwd=root,
+                         capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stderr[-2000:]
+    out = json.loads(res.stdout.strip().splitlines()[-1])
+    assert out["ok"] == 3000 and out["duration_mismatches"] == 0 and out["duration_checked"] > 0

@@ -5,7 +5,12 @@ start times, K - 1 first-fit separators, windowed 2-opt + swap / relocate
 anywhere.  Steps per second per chain of sa_seg_kernel's heterogeneous
 variant against the full re-evaluation kernel it replaces (sa_kernel,
 ctx.set_sa_route(2)), and whether both follow the same trajectories.
-usage: het_rate.py [chains] [steps]"""
+With --td: the reference's normal VRP request shape instead -- the
+hour-indexed TD-200 x 24 (time_of_day, src/solver.py:7) with three capacity
+classes (1.3 / 1.0 / 0.8) and staggered start times: sa_route_kernel's
+heterogeneous variant (walks re-synchronise on the same vehicle) against
+sa_kernel.
+usage: het_rate.py [chains] [steps] [--td]"""
 import os
 import sys
 import time
@@ -18,19 +23,25 @@ import torch  # noqa: E402
 from vrpms_amd import runners, synth  # noqa: E402
 from vrpms_amd.core import CVRP, Context  # noqa: E402
 
-chains = int(sys.argv[1]) if len(sys.argv) > 1 else 256
-steps = int(sys.argv[2]) if len(sys.argv) > 2 else 400
-x = synth.x_style(1000, seed=0)
+TD = "--td" in sys.argv
+argv = [a for a in sys.argv[1:] if not a.startswith("--")]
+chains = int(argv[0]) if len(argv) > 0 else 256
+steps = int(argv[1]) if len(argv) > 1 else 400
+x = synth.td_cvrp(200, 16, seed=0) if TD else synth.x_style(1000, seed=0)
 K, base = len(x.capacities), int(x.capacities[0])
-caps = np.array([max(int(base * (1.4, 1.1, 0.9)[k * 3 // K]), int(x.demand.max())) for k in range(K)])
-starts = np.arange(K, dtype=np.int64) * 37 % 240
+fr = (1.3, 1.0, 0.8) if TD else (1.4, 1.1, 0.9)
+caps = np.array([max(int(base * fr[k * 3 // K]), int(x.demand.max())) for k in range(K)])
+starts = np.arange(K, dtype=np.int64) * 37 % 240 + (420 if TD else 0)
+window = 16 if TD else 32
 ctx = Context(0)
 ctx.set_instance(CVRP, x.durations, x.demand, caps, starts)
 out = {}
-for mode, label in ((0, "sa_seg_kernel (heterogeneous)"), (2, "sa_kernel (full re-evaluation)")):
+fast = "sa_route_kernel (heterogeneous, same-vehicle resync)" if TD else \
+    "sa_seg_kernel (heterogeneous)"
+for mode, label in ((0, fast), (2, "sa_kernel (full re-evaluation)")):
     ctx.set_sa_route(mode)
     r = runners.SARunner(ctx, x.n, chains=chains, total_steps=steps + 10, durations=x.durations,
-                         n_sep=K - 1, window=32, window_types=2, start="pack", moves=64)
+                         n_sep=K - 1, window=window, window_types=2, start="pack", moves=64)
     r.epoch(10)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -38,7 +49,9 @@ for mode, label in ((0, "sa_seg_kernel (heterogeneous)"), (2, "sa_kernel (full r
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     out[mode] = (r.cur.cpu(), r.cur_key.cpu())
+    out[f"rate{mode}"] = steps / dt
     print(f"{label}: {steps / dt:,.0f} steps/s per chain ({chains} chains x 64 moves), "
           f"best {r.best()[0] >> 28 & (2**28 - 1)} (unvisited {r.best()[0] >> 56})", flush=True)
-print("same trajectories:", torch.equal(out[0][0], out[2][0]) and torch.equal(out[0][1], out[2][1]))
+print("same trajectories:", torch.equal(out[0][0], out[2][0]) and torch.equal(out[0][1], out[2][1]),
+      f"speed-up {out['rate0'] / out['rate2']:.2f}x")
 ctx.set_sa_route(0)

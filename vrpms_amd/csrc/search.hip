@@ -246,7 +246,16 @@ VRPMS_DEV uint32_t wave_scan_incl(uint32_t v) {
 __device__ unsigned long long g_route_prof[12 * 8192];
 #endif
 
-template <typename MatT, int HM>
+// HV: a fleet of different vehicles (per-vehicle capacities or start
+// times, api/parameters.py:11-12).  Route r of the split runs on vehicle
+// min(r, K - 1) (past the fleet the routes serve no one and the fleet count
+// rejects the tour), so a walk is back in step only at a route start of the
+// current tour that it reaches on the same vehicle: from there both run on
+// the same vehicles from the same state.  A zone that re-synchronises then
+// keeps its route count (d = 0); one that does not is walked to the end of
+// the tour.  The tables of a full build come from one lane's walk (a
+// segment's routes depend on the vehicles before it).
+template <typename MatT, int HM, bool HV = false>
 __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 #ifdef VRPMS_ROUTE_PROF
@@ -317,6 +326,9 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
   const uint32_t Nm1 = N - 1;
   const int cap0 = I.sp.cap[0], st0 = I.sp.start[0];
   const int32_t* dem = I.sp.dem;
+  // vehicle v's capacity and start time (HV; past the fleet: the last vehicle's)
+  auto capv = [&](int v) -> int { return HV ? I.sp.cap[v < K ? v : K - 1] : cap0; };
+  auto stv = [&](int v) -> int { return HV ? I.sp.start[v < K ? v : K - 1] : st0; };
   if (cw == 0) {  // the chain's first wavefront owns every table write outside an accept
     const uint16_t* gcur = a.cur + (int64_t)chain * n;
     for (int q = lane; q < n; q += 64) {
@@ -356,10 +368,14 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
     uint32_t prev, cnt, ds, dm;
     int xs;    // closures before the last customer (-1: none yet)
     int pret;  // return leg of prev (static matrix)
+    int v, cap, st;  // (HV) the open route's vehicle, its capacity and start time
   };
-  auto fresh = [&](Walk& w) {
+  auto fresh = [&](Walk& w, int v) {  // a route start on vehicle v (HV)
     w.load = 0;
-    w.t = st0;
+    w.v = v;
+    w.cap = capv(v);
+    w.st = stv(v);
+    w.t = HV ? w.st : st0;
     w.prev = 0;
     w.cnt = w.ds = w.dm = 0;
     w.xs = -1;
@@ -375,19 +391,25 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
   };
   auto close = [&](Walk& w) -> uint32_t {  // returns the closed route's duration
     uint32_t rd = 0;
+    const int s0 = HV ? w.st : st0;
     if constexpr (HM == 1) {  // branch-free: the return leg rides in pret
-      rd = w.prev ? (uint32_t)(w.t + w.pret - st0) : 0u;
+      rd = w.prev ? (uint32_t)(w.t + w.pret - s0) : 0u;
       w.ds += rd;
       w.dm = max(w.dm, rd);
     } else if (w.prev) {
       w.t += I.D(w.t, w.prev, 0);
-      rd = (uint32_t)(w.t - st0);
+      rd = (uint32_t)(w.t - s0);
       w.ds += rd;
       w.dm = max(w.dm, rd);
     }
     ++w.cnt;
     w.load = 0;
-    w.t = st0;
+    if (HV) {
+      ++w.v;
+      w.cap = capv(w.v);
+      w.st = stv(w.v);
+    }
+    w.t = HV ? w.st : st0;
     w.prev = 0;
     return rd;
   };
@@ -480,6 +502,47 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
   // the lanes split in parallel (two passes: route counts, then routes at
   // their global index).  Returns R, or -1 when the tables cannot hold it.
   auto full_build = [&]() -> int {
+    if constexpr (HV) {
+      // the vehicles of a segment's routes depend on every route before it:
+      // one lane walks the tour (full builds are rare: the start of a call
+      // and accepts whose routes no longer fit the incremental update)
+      int r = 0;
+      if (lane == 0) {
+        Walk w;
+        fresh(w, 0);
+        int start = 0;
+        for (int q = 0; q < n && r <= RMAX; ++q) {
+          const uint32_t at = T.at[q], c = at & 0xffffu;
+          const int d = (int)(at >> 16);
+          if (c == 0 || w.load + d > w.cap) {
+            const bool cu = w.prev != 0;
+            if (c == 0) T.rid[q] = (uint8_t)r;  // a separator belongs to the route it ends
+            T.dur[r] = close(w);
+            T.cus[r] = cu ? 1 : 0;
+            T.rs[r] = (uint16_t)start;
+            ++r;
+            start = c == 0 ? q + 1 : q;
+            if (c == 0 || r > RMAX) continue;
+          }
+          add(w, c, d, w.prev ? ein_q(q) : 0);
+          T.rid[q] = (uint8_t)r;
+        }
+        if (r <= RMAX) {
+          const bool cu = w.prev != 0;
+          T.dur[r] = close(w);
+          T.cus[r] = cu ? 1 : 0;
+          T.rs[r] = (uint16_t)start;
+          ++r;
+          if (r <= RMAX) T.rs[r] = (uint16_t)n;
+        }
+      }
+      const int R = __builtin_amdgcn_readfirstlane(r);
+      wave_sync();
+      if (R > RMAX) return -1;
+      derive(R);
+      build_bits();
+      return R;
+    }
     int S = 0;
     for (int base = 0; base < n; base += 64) {
       const int q = base + lane;
@@ -496,7 +559,7 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
     for (int s = lane; s <= S; s += 64) {
       const int from = s ? T.send[s - 1] + 1 : 0, to = T.send[s];
       Walk w;
-      fresh(w);
+      fresh(w, 0);
       for (int q = from; q < to; ++q) {
         const uint32_t at = T.at[q], c = at & 0xffffu;
         const int d = (int)(at >> 16);
@@ -523,7 +586,7 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
       const int from = s ? T.send[s - 1] + 1 : 0, to = T.send[s];
       int r = (int)T.pmx[s], start = from;
       Walk w;
-      fresh(w);
+      fresh(w, 0);
       for (int q = from; q < to; ++q) {
         const uint32_t at = T.at[q], c = at & 0xffffu;
         const int d = (int)(at >> 16);
@@ -634,8 +697,8 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
       const bool two = m.typ != kMove2Opt && Z2 > bq0;
       int phase = two ? 1 : 3;  // 1: first zone, 2: second zone, 3: one merged zone
       Walk w, w1;
-      fresh(w);
-      fresh(w1);
+      fresh(w, r1s);
+      fresh(w1, r1s);
       r2e = R;
       int q = P1;
       int zbase = P1;  // first position of the zone being walked
@@ -696,6 +759,21 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
         const uint64_t wm = bm >= 0 ? (((uint64_t)T.bits[(bm >> 5) + 1] << 32) | T.bits[bm >> 5]) >> (bm & 31)
                                     : 0ull;
         const uint64_t wa = (((uint64_t)T.bits[(q >> 5) + 1] << 32) | T.bits[q >> 5]) >> (q & 31);
+        // (HV) the current tour's routes at the window bases: the route
+        // starting at base + i is that plus the starts in (base, base + i];
+        // and the capacities / start times of the next two vehicles (a block
+        // closing a third route stops before it and resumes in the next)
+        int ridm = 0, rida = 0, cap1 = 0, st1 = 0, cap2 = 0, st2 = 0, ncl = 0;
+        if constexpr (HV) {
+          ridm = bm >= 0 && bm < n ? (int)T.rid[bm] : 0;
+          rida = (int)T.rid[q < n ? q : n - 1];
+          if (HM == 1) {
+            cap1 = capv(w.v + 1);
+            st1 = stv(w.v + 1);
+            cap2 = capv(w.v + 2);
+            st2 = stv(w.v + 2);
+          }
+        }
         int adv = kBlk;
         // Each token is straight-line predicated code: a lane that leaves the
         // block early sets `stop`, and the rare events that end a zone (back
@@ -717,29 +795,48 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
           // back in step at a route start of the current tour: the walk's
           // route is fresh there, or the customer there does not fit (a
           // separator would close the walk's route, not the tour's empty one)
-          const bool nofit = c != 0 && w.load + db[i] > cap0;
-          const bool insync = w.prev == 0 || nofit;
+          // -- and (HV) the walk's next route there is that route
+          const bool nofit = c != 0 && w.load + db[i] > (HV ? w.cap : cap0);
+          bool insm = w.prev == 0 || nofit, insa = insm;
+          if constexpr (HV) {
+            const int vw = w.prev == 0 ? w.v : w.v + 1;
+            const uint32_t below = (1u << i) - 1u;
+            insm = insm && vw == ridm + __popc((uint32_t)(wm >> 1) & below);
+            insa = insa && vw == rida + __popc((uint32_t)(wa >> 1) & below);
+          }
           const bool mid = !stop && phase == 1 && qq >= bq0;  // moved(qq) = A[qq - dl]
-          const bool sw = mid && ((wm >> i) & 1u) && insync;
+          const bool sw = mid && ((wm >> i) & 1u) && insm;
           phase = mid && !sw && qq == Z2 ? 3 : phase;  // never back in step before the second end
-          const bool done = !stop && !sw && phase >= 2 && qq > hi && ((wa >> i) & 1u) && insync;
+          const bool done = !stop && !sw && phase >= 2 && qq > hi && ((wa >> i) & 1u) && insa;
           ev = sw ? 1 : done ? 2 : ev;
           evq = sw || done ? qq : evq;
-          const bool act = !stop && !sw && !done;
-          stop = stop || sw || done;
+          // (HV, static matrix) a third closure in the block: resume there
+          const bool over = HV && HM == 1 && !stop && !sw && !done && (c == 0 || nofit) && ncl >= 2;
+          adv = over ? i : adv;
+          const bool act = !stop && !sw && !done && !over;
+          stop = stop || sw || done || over;
           // a separator ends the walk's route (the next one starts after it);
           // a customer that does not fit closes it and opens the next
           if constexpr (HM == 1) {
             const bool closing = act && (c == 0 || nofit);
-            const uint32_t rd = closing && w.prev ? (uint32_t)(w.t + w.pret - st0) : 0u;
+            const uint32_t rd =
+                closing && w.prev ? (uint32_t)(w.t + w.pret - (HV ? w.st : st0)) : 0u;
             w.ds += rd;
             w.dm = max(w.dm, rd);
             w.cnt += closing ? 1u : 0u;
+            if constexpr (HV) {  // the next vehicle opens
+              w.v += closing ? 1 : 0;
+              w.cap = closing ? cap1 : w.cap;
+              w.st = closing ? st1 : w.st;
+              cap1 = closing ? cap2 : cap1;
+              st1 = closing ? st2 : st1;
+              ncl += closing ? 1 : 0;
+            }
             // the next route starts at block offset i (i + 1 after a
             // separator); zbase and z2 are fixed inside a block, so the bits
             // go to the zone's mask once, after the block
             blk |= closing ? (c == 0 ? 2u << i : 1u << i) : 0u;
-            const int t0 = closing ? st0 : w.t, l0 = closing ? 0 : w.load;
+            const int t0 = closing ? (HV ? w.st : st0) : w.t, l0 = closing ? 0 : w.load;
             const uint32_t p0 = closing ? 0u : w.prev;
             const bool addf = act && c != 0;
             w.t = addf ? t0 + (p0 ? eb[i] : ob[i]) : t0;
@@ -773,7 +870,7 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
           w1 = w;
           r1e = T.rid[evq - dl];
           q1 = evq;
-          fresh(w);
+          fresh(w, r2s + (int)w1.cnt - (r1e - r1s));  // (HV: back in step on r1e, so r2s)
           phase = 2;
           z2 = true;
           zbase = Z2;
@@ -793,7 +890,7 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
       q2 = q;
       if (phase != 2) {  // one zone: routes r1s .. r2e - 1
         w1 = w;
-        fresh(w);
+        fresh(w, R);
         r1e = r2s = r2e;
         q1 = Z2 = q2;
       }
@@ -990,7 +1087,7 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
               int zi = 0;
               auto rec = [&](int from, int to, int r0) {
                 Walk w;
-                fresh(w);
+                fresh(w, r0);
                 int start = from, rr = r0;
                 auto put = [&](int next) {
                   const bool cu = w.prev != 0;
@@ -1009,7 +1106,7 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
                     put(q + 1);
                     continue;
                   }
-                  if (w.load + d > cap0) put(q);
+                  if (w.load + d > (HV ? w.cap : cap0)) put(q);
                   add(w, c, d, w.prev ? ein_q(q) : 0);
                   T.rid[q] = (uint8_t)rr;
                 }
@@ -1099,7 +1196,7 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
             const int rr = lane < bc1 ? br1s + lane : br2s + d1 + (lane - bc1);
             const int from = T.rs[rr], to = T.rs[rr + 1];
             Walk w;
-            fresh(w);
+            fresh(w, rr);
             for (int q = from; q < to; ++q) {
               const uint32_t at = T.at[q], c = at & 0xffffu;
               if (c == 0) break;  // a separator ends the route
@@ -2144,6 +2241,10 @@ struct RouteK {
   static auto kernel() { return sa_route_kernel<MatT, HM>; }
 };
 template <typename MatT, int HM, bool CVRP>
+struct RouteHK {  // per-vehicle capacities / start times
+  static auto kernel() { return sa_route_kernel<MatT, HM, true>; }
+};
+template <typename MatT, int HM, bool CVRP>
 struct BfK {
   static auto kernel() { return bf_kernel<MatT, HM, CVRP>; }
 };
@@ -2219,12 +2320,13 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
   SaArgs a{search_inst(ctx), p->chains, n, p->steps, p->window, wtypes, p->inv_t0, p->inv_alpha,
            (uint32_t)p->seed, (uint32_t)(p->seed >> 32), p->step0, d_cur, d_cur_key, d_best,
            d_best_key, wpc};
-  // route-local pricing (sa_route_kernel) for windowed SA on a fleet of
-  // exchangeable vehicles: one capacity, one start time, every demand fits
+  // route-local pricing (sa_route_kernel) for windowed SA, every demand
+  // fitting the smallest vehicle: an exchangeable fleet (one capacity, one
+  // start time) or not (HV: walks re-synchronise on the same vehicle only)
   const Instance& in = ctx->inst;
-  if (p->window > 0 && in.problem == VRPMS_CVRP && in.uniform_cap &&
-      in.min_start == in.max_start && in.max_dem <= in.cap0 && in.max_dem <= 65535 &&
-      route_max(in.K) <= 255 &&
+  const bool hv = !(in.uniform_cap && in.min_start == in.max_start);
+  if (p->window > 0 && in.problem == VRPMS_CVRP && in.max_dem <= in.min_cap &&
+      in.max_dem <= 65535 && route_max(in.K) <= 255 &&
       n <= 65535 && ctx->opt_sa_route != 2) {  // (0 auto, 3 force this kernel)
     const size_t npad = ((size_t)n + 7) & ~(size_t)7;
     const size_t wbytes = ((size_t)route_wave_bytes((int)npad, in.K) + 15) & ~(size_t)15;
@@ -2242,13 +2344,14 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
       const int per_cu = ctx->opt_route_wg_per_cu ? ctx->opt_route_wg_per_cu : (wpc > 1 ? 1 : 2);
       if (per_cu == 1) lds = std::max(lds, ctx->max_lds / 2 + 16);
       const dim3 grid(wpc > 1 ? p->chains : (p->chains + 3) / 4), block(wpc > 1 ? 64 * wpc : 256);
+      if (hv) return launch_inst<RouteHK>(ctx, grid, block, lds, (hipStream_t)stream, a);
       return launch_inst<RouteK>(ctx, grid, block, lds, (hipStream_t)stream, a);
     }
   }
   if (wpc > 1)
     return fail(VRPMS_EINVAL,
-                "vrpms_sa_run: moves > 64 needs the route-local kernel (window > 0, CVRP, one "
-                "capacity and start time, every demand fits a vehicle)");
+                "vrpms_sa_run: moves > 64 needs the route-local kernel (window > 0, CVRP, every "
+                "demand fits the smallest vehicle, at most 126 vehicles)");
   const size_t npad = ((size_t)n + 7) & ~(size_t)7;
   size_t lds = inst_lds_bytes_host(a.si) + 4 * 3 * npad * 2;
   if (lds > ctx->max_lds) {

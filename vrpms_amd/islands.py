@@ -119,6 +119,50 @@ def exchange(runner, E: int, group=None):
     ctx.pool_inject(*runner.dst(), runner.inject_mode, tours, keys, runner.groups)
 
 
+def exchange_local(runners, E: int):
+    """One migration among islands held by ONE process on several devices
+    (the service's multi-GPU path): each runner's E elites are
+    packed on its device, every message is copied device to device (xGMI
+    peer copies), and each device merges the same gathered messages and
+    injects the global E best -- the all-gather exchange without a
+    communicator.  Messages go in runner order, so every island receives the
+    same migrants as vrpms_island_exchange would give ranks in that order."""
+    torch = _torch()
+    msgs = [r.ctx.island_pack(*r.src(), E) for r in runners]
+    world = len(runners)
+    for r in runners:
+        allm = torch.cat([m.to(r.ctx.dev) for m in msgs])
+        tours, keys = r.ctx.island_merge(allm, world, E, r.n)
+        r.ctx.pool_inject(*r.dst(), r.inject_mode, tours, keys, r.groups)
+
+
+def run_local(runners, epochs: int, exchange_every: int = 5, E: int = 8, time_limit=None,
+              sync=None):
+    """Islands on several devices of one process: every epoch is enqueued on
+    each device in turn (the launches are asynchronous, so the devices run
+    together), a migration every `exchange_every` epochs.  Stops after
+    `epochs`, or when `time_limit` seconds have passed (checked after each
+    epoch, as the single-device search does).  Returns the global best
+    (key, tour) by (key, island)."""
+    import time
+    t0 = time.perf_counter()
+    for e in range(1, epochs + 1):
+        for r in runners:
+            r.epoch()
+        if e % exchange_every == 0 and len(runners) > 1:
+            exchange_local(runners, E)
+        if sync is not None:
+            sync()
+        if time_limit is not None and time.perf_counter() - t0 >= time_limit:
+            break
+    best = None
+    for r in runners:
+        k, t = r.best()
+        if best is None or k < best[0]:
+            best = (k, t)
+    return best
+
+
 def run_islands(runner, epochs: int, exchange_every: int = 5, E: int = 8, group=None):
     """Advance `runner` for `epochs`, migrating every `exchange_every` epochs."""
     for e in range(1, epochs + 1):

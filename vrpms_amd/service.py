@@ -7,8 +7,9 @@ set and duration matrix from Supabase, run the algorithm (the
 module keeps that request/response contract byte for byte -- banners,
 preflight headers, error lists, status lines, the save payload -- and fills
 the slot with the GPU solver (vrpms_amd.solver).  One process owns one GPU
-context; requests are served by a threading HTTP server and reach the GPU
-one at a time (the solver's context is per process).
+context per served device; requests are served by a threading HTTP server,
+one at a time per device (App.devices; large requests as an island model
+across all of them).  Throughput mode across processes: vrpms_amd.frontends.
 
 Storage is pluggable: anything with the three calls of the reference's
 Database classes (api/database.py) works.  `MemoryStore` (JSON-backed, the
@@ -161,7 +162,9 @@ class TspBatcher:
     5 of BASELINE.json).  A request waits at most `window_s` for company.
     Requests in one launch share its seed and temperature schedule (scaled
     to the batch's mean edge), so a batched answer depends on the batch it
-    rode in; the unbatched path is deterministic per request."""
+    rode in; the unbatched path is deterministic per request.  With several
+    devices the launches go to them round-robin (SURVEY.md §8e cfg 5:
+    replicas only), one launch thread per device, so they run together."""
 
     MIN_N, MAX_N = 4, 190        # compact nodes; N*N int32 must fit the LDS
 
@@ -176,6 +179,13 @@ class TspBatcher:
         self._launch = launch or self._gpu_launch
         self._q = []
         self._cv = threading.Condition()
+        self.devices = list(getattr(app, "devices", None) or [getattr(app, "device", 0)])
+        self.per_device = {d: 0 for d in self.devices}
+        self._rr = 0
+        self._pool = None
+        if len(self.devices) > 1:
+            from concurrent.futures import ThreadPoolExecutor
+            self._pool = ThreadPoolExecutor(len(self.devices), thread_name_prefix="tsp-launch")
         threading.Thread(target=self._loop, daemon=True, name="tsp-batcher").start()
 
     @classmethod
@@ -218,25 +228,39 @@ class TspBatcher:
             for job in batch:
                 groups.setdefault(job["ci"].N, []).append(job)
             for N, jobs in groups.items():
-                try:
-                    res = self._launch(N, [j["ci"] for j in jobs])
-                    tours, durs = res if isinstance(res, tuple) else (res, None)
-                    self.launches += 1
-                    self.requests += len(jobs)
-                    for x, (j, t) in enumerate(zip(jobs, tours)):
-                        j["tour"] = t
-                        if durs is not None and durs[x] is not None:
-                            j["duration"] = durs[x]
-                except Exception as e:         # every waiter of the group sees it
-                    for j in jobs:
-                        j["error"] = e
-                for j in jobs:
-                    j["done"].set()
+                dev = self.devices[self._rr % len(self.devices)]
+                self._rr += 1
+                if self._pool is None:
+                    self._run(N, jobs, dev)
+                else:
+                    self._pool.submit(self._run, N, jobs, dev)
 
-    def _gpu_launch(self, N, cis):
-        """-> (tours, durations): the durations are the kernel's keys'
-        primary term (A8: a TSP key is duration << 28), exact below the
-        2^28 - 1 clamp; a clamped one is summed on the host."""
+    def _run(self, N, jobs, dev):
+        try:
+            if len(self.devices) > 1:
+                res = self._launch(N, [j["ci"] for j in jobs], dev)
+            else:
+                res = self._launch(N, [j["ci"] for j in jobs])
+            tours, durs = res if isinstance(res, tuple) else (res, None)
+            with self._cv:
+                self.launches += 1
+                self.requests += len(jobs)
+                self.per_device[dev] += len(jobs)
+            for x, (j, t) in enumerate(zip(jobs, tours)):
+                j["tour"] = t
+                if durs is not None and durs[x] is not None:
+                    j["duration"] = durs[x]
+        except Exception as e:         # every waiter of the group sees it
+            for j in jobs:
+                j["error"] = e
+        for j in jobs:
+            j["done"].set()
+
+    def _gpu_launch(self, N, cis, device=None):
+        """-> (tours, durations) on `device` (default: the app's first): the
+        durations are the kernel's keys' primary term (A8: a TSP key is
+        duration << 28), exact below the 2^28 - 1 clamp; a clamped one is
+        summed on the host."""
         import numpy as np
         import torch
         from . import solver
@@ -249,8 +273,9 @@ class TspBatcher:
         edge = float(nz.mean()) if nz.size else 1.0
         inv_t0 = 1.0 / (0.5 * edge)
         inv_alpha = (0.5 / 0.002) ** (1.0 / max(1, self.steps))
-        with self.app.gpu_lock:
-            ctx = solver.context(self.app.device)
+        dev = self.devices[0] if device is None else device
+        with self.app.locks[dev]:
+            ctx = solver.context(dev)
             mats = torch.from_numpy(host).to(ctx.dev)
             tours, keys = ctx.tsp_batch_sa(mats, self.steps, inv_t0, inv_alpha, self.app.seed)
             tours, keys = tours.cpu().tolist(), keys.cpu().tolist()
@@ -264,19 +289,62 @@ class TspBatcher:
 # ---------------------------------------------------------------------------
 class App:
     """Parse -> fetch -> solve -> save -> respond for one endpoint call.
-    `solve` is injectable (tests); by default it is the GPU solver."""
+    `solve` is injectable (tests); by default it is the GPU solver.
+
+    `devices` (default [device]): the GPUs this process serves.  Each has
+    its own context and lock; a request takes the first free device (one
+    request per device at a time), and a large SA / GA / ACO request (more
+    than `island_min_n` customers) with two or more devices takes them all
+    and runs as an island model across them (solver.search_islands)."""
 
     def __init__(self, store, device: int = 0, seed: int = 0, max_seconds: float | None = None,
                  solve=None, batch_tsp: bool = False, batch_window_s: float = 0.005,
-                 batch_steps: int = 2000, batch_launch=None):
+                 batch_steps: int = 2000, batch_launch=None, devices=None,
+                 island_min_n: int = 150):
         self.store = store
-        self.device = device
+        self.devices = list(devices) if devices else [device]
+        self.device = self.devices[0]
         self.seed = seed
         self.max_seconds = max_seconds
-        self.gpu_lock = threading.Lock()
+        self.island_min_n = island_min_n
+        self.locks = {d: threading.Lock() for d in self.devices}
+        self.gpu_lock = self.locks[self.device]
+        self._rr = 0
+        self._rr_lock = threading.Lock()
         self._solve = solve or self._gpu_solve
         self.batcher = TspBatcher(self, batch_window_s, batch_steps, launch=batch_launch) \
             if batch_tsp else None
+
+    def _scheduled(self, problem, algorithm, params, knobs, locations, durations):
+        """Run the solve on a device: all of them (in order, as an island
+        model) for a large SA / GA / ACO request when there are several, else
+        the first free one (round-robin start), waiting for one if all are
+        busy."""
+        n = len(params.get("customers") or []) if problem == "tsp" else \
+            max(0, len(locations or []) - 1)
+        knobs = dict(knobs)
+        if len(self.devices) > 1 and algorithm != "bf" and n > self.island_min_n:
+            for d in self.devices:
+                self.locks[d].acquire()
+            try:
+                knobs["devices"] = list(self.devices)
+                return self._solve(problem, algorithm, params, knobs, locations, durations)
+            finally:
+                for d in reversed(self.devices):
+                    self.locks[d].release()
+        with self._rr_lock:
+            start = self._rr
+            self._rr = (self._rr + 1) % len(self.devices)
+        order = self.devices[start:] + self.devices[:start]
+        dev = next((d for d in order if self.locks[d].acquire(blocking=False)), None)
+        if dev is None:
+            dev = order[0]
+            self.locks[dev].acquire()
+        try:
+            knobs["device"] = dev
+            return self._solve(problem, algorithm, params, knobs, locations, durations)
+        finally:
+            self.locks[dev].release()
 
     def _batched_tsp(self, params, durations):
         """The compact instance when this request rides the batcher, else None."""
@@ -293,10 +361,12 @@ class App:
         from . import solver
         seed = int(knobs.get("seed", self.seed))
         tl = knobs.get("time_limit", self.max_seconds)
+        devs = knobs.get("devices") or [knobs.get("device", self.device)]
+        dv = dict(device=devs[0], devices=devs if len(devs) > 1 else None)
         if problem == "tsp":
             return solver.solve_tsp(algorithm, durations, params["customers"],
                                     params["start_node"], params["start_time"] or 0,
-                                    seed=seed, time_limit=tl, device=self.device)
+                                    seed=seed, time_limit=tl, **dv)
         extra = {}
         if knobs.get("random_permutationCount"):
             extra["random_permutation_count"] = int(knobs["random_permutationCount"])
@@ -306,7 +376,7 @@ class App:
                                 params["start_times"], params["ignored_customers"],
                                 params["completed_customers"], seed=seed,
                                 objective=knobs.get("objective", "sum"),
-                                time_limit=tl, device=self.device, **extra)
+                                time_limit=tl, **dv, **extra)
 
     def post(self, problem: str, algorithm: str, raw: bytes):
         """-> (status, response dict) for a POST body."""
@@ -334,8 +404,7 @@ class App:
             if ci is not None:
                 result = self.batcher.solve(ci)
             else:
-                with self.gpu_lock:
-                    result = self._solve(problem, algorithm, params, knobs, locations, durations)
+                result = self._scheduled(problem, algorithm, params, knobs, locations, durations)
         except Exception as e:   # bad instance shape, GPU unavailable, ...
             return 400, {"success": False,
                          "errors": [{"what": "Solver error", "reason": str(e)}]}
@@ -406,8 +475,7 @@ class App:
             return 400, {"success": False,
                          "errors": [{"what": "Invalid request", "reason": str(e)}]}
         try:
-            with self.gpu_lock:
-                result = self._solve(problem, algorithm, params, knobs, locations,
+            result = self._scheduled(problem, algorithm, params, knobs, locations,
                                      vals["durations"])
         except Exception as e:
             return 400, {"success": False,
@@ -506,6 +574,9 @@ def main(argv=None):
     ap.add_argument("--port", type=int, default=8000)
     ap.add_argument("--data", help="MemoryStore JSON (locations / durations / users)")
     ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--devices", default=None,
+                    help="comma-separated GPUs to serve (default: --device); large SA / GA / ACO "
+                         "requests run as an island model across them")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--max-seconds", type=float, default=None,
                     help="wall-time cap per solve (default: the algorithm's own budget)")
@@ -515,9 +586,10 @@ def main(argv=None):
     ap.add_argument("--batch-steps", type=int, default=2000)
     args = ap.parse_args(argv)
     store = MemoryStore.from_json(args.data) if args.data else MemoryStore()
+    devices = [int(x) for x in args.devices.split(",")] if args.devices else None
     app = App(store, device=args.device, seed=args.seed, max_seconds=args.max_seconds,
               batch_tsp=args.batch_tsp, batch_window_s=args.batch_window_ms * 1e-3,
-              batch_steps=args.batch_steps)
+              batch_steps=args.batch_steps, devices=devices)
     srv = serve(app, args.host, args.port)
     print(f"vrpms_amd service on http://{args.host}:{args.port}/api", flush=True)
     try:

@@ -137,19 +137,20 @@ def compact_vrp(durations, locations, capacities, start_times, ignored_customers
 # ---------------------------------------------------------------------------
 # device context (one per process; the handlers call in sequentially)
 # ---------------------------------------------------------------------------
-_CTX: Context | None = None
+_CTX: dict = {}
 _CTX_LOCK = threading.Lock()
 
 
 def context(device: int = 0) -> Context:
-    """The process-wide context on `device` (created once; the check and the
-    creation are one critical section, so concurrent first calls from the
-    request threads and the batcher share a single vrpms_ctx)."""
-    global _CTX
+    """The process-wide context on `device`, one per device (created once;
+    the check and the creation are one critical section, so concurrent first
+    calls from the request threads and the batcher share a single vrpms_ctx
+    per device)."""
     with _CTX_LOCK:
-        if _CTX is None or _CTX.device != device:
-            _CTX = Context(device)
-        return _CTX
+        ctx = _CTX.get(device)
+        if ctx is None:
+            ctx = _CTX[device] = Context(device)
+        return ctx
 
 
 def load(ctx: Context, ci: CompactInstance, objective: int = OBJ_SUM):
@@ -158,6 +159,65 @@ def load(ctx: Context, ci: CompactInstance, objective: int = OBJ_SUM):
     else:
         ctx.set_instance(CVRP, ci.durations, ci.demand, ci.capacities, ci.start_times,
                          objective=objective)
+
+
+def _runner(ctx: Context, ci: CompactInstance, algorithm: str, seed: int, knobs: dict):
+    """(runner, epochs) for SA / GA / ACO on the loaded instance."""
+    n = ci.n
+    iters = knobs.get("iteration_count")
+    if algorithm == "sa":
+        steps = int(iters or knobs.get("steps", 4000))
+        # VRP: K - 1 route separators (A10) let the moves place route
+        # boundaries instead of leaving them to the greedy split alone
+        n_sep = int(knobs.get("separators", len(ci.capacities) - 1 if ci.problem == CVRP else 0))
+        # large tours: A11/A12 windowed 2-opt, swap / relocate anywhere
+        # (priced in O(1) / route-locally); separators start where first-fit
+        # routes end (a feasible start on a tight fleet, where random
+        # separator positions would leave customers unserved)
+        window = int(knobs.get("window", SA_WINDOW if n > SA_WINDOW_MIN_N else 0))
+        r = runners.SARunner(ctx, n, chains=int(knobs.get("chains", 1024)), seed=seed,
+                             total_steps=steps, durations=ci.durations, n_sep=n_sep,
+                             window=window, window_types=int(knobs.get("window_types", 2)),
+                             start="pack" if n_sep > 0 else "random")
+        return r, max(1, steps // r.steps_per_epoch)
+    if algorithm == "ga":
+        pop = int(knobs.get("random_permutation_count") or knobs.get("pop", 256))
+        gens = int(iters or 400)
+        r = runners.GARunner(ctx, n, islands=int(knobs.get("islands", 8)), pop=max(2, min(pop, 4096)),
+                             seed=seed)
+        return r, max(1, gens // r.gens_per_epoch)
+    if algorithm == "aco":
+        its = int(iters or 100)
+        r = runners.ACORunner(ctx, n, colonies=int(knobs.get("colonies", 4)),
+                              ants=int(knobs.get("ants", 64)), seed=seed)
+        return r, max(1, its // r.iters_per_epoch)
+    raise ValueError(f"unknown algorithm {algorithm!r}; expected one of {ALGORITHMS}")
+
+
+def search_islands(ci: CompactInstance, algorithm: str, devices, seed: int = 0,
+                   time_limit: float | None = None, objective: int = OBJ_SUM, **knobs):
+    """The island model inside one process: one SA / GA / ACO
+    island per device (seed + 1000 d), the same epochs enqueued on every
+    device, the E best migrating every 5 epochs device to device
+    (islands.exchange_local).  -> (key, compact giant tour) of the best
+    island."""
+    import torch
+    from . import islands
+    if ci.n <= 1 or algorithm == "bf":
+        raise ValueError("search_islands: SA / GA / ACO on two or more customers")
+    rs, epochs = [], 1
+    for d, dev in enumerate(devices):
+        ctx = context(dev)
+        load(ctx, ci, objective)
+        r, epochs = _runner(ctx, ci, algorithm, seed + 1000 * d, knobs)
+        rs.append(r)
+
+    def sync():
+        for dev in devices:
+            torch.cuda.synchronize(dev)
+    key, tour = islands.run_local(rs, epochs, exchange_every=5, E=min(8, rs[0].src()[1].numel()),
+                                  time_limit=time_limit, sync=sync if time_limit else None)
+    return key, [int(x) for x in tour.cpu().tolist()]
 
 
 def search(ctx: Context, ci: CompactInstance, algorithm: str, seed: int = 0,
@@ -174,35 +234,7 @@ def search(ctx: Context, ci: CompactInstance, algorithm: str, seed: int = 0,
             raise ValueError(f"brute force supports at most {cap} customers "
                              f"({n} given)")
         return runners.brute_force(ctx, n)
-    iters = knobs.get("iteration_count")
-    if algorithm == "sa":
-        steps = int(iters or knobs.get("steps", 4000))
-        # VRP: K - 1 route separators (A10) let the moves place route
-        # boundaries instead of leaving them to the greedy split alone
-        n_sep = int(knobs.get("separators", len(ci.capacities) - 1 if ci.problem == CVRP else 0))
-        # large tours: A11/A12 windowed 2-opt, swap / relocate anywhere
-        # (priced in O(1) / route-locally); separators start where first-fit
-        # routes end (a feasible start on a tight fleet, where random
-        # separator positions would leave customers unserved)
-        window = int(knobs.get("window", SA_WINDOW if n > SA_WINDOW_MIN_N else 0))
-        r = runners.SARunner(ctx, n, chains=int(knobs.get("chains", 1024)), seed=seed,
-                             total_steps=steps, durations=ci.durations, n_sep=n_sep,
-                             window=window, window_types=int(knobs.get("window_types", 2)),
-                             start="pack" if n_sep > 0 else "random")
-        epochs = max(1, steps // r.steps_per_epoch)
-    elif algorithm == "ga":
-        pop = int(knobs.get("random_permutation_count") or knobs.get("pop", 256))
-        gens = int(iters or 400)
-        r = runners.GARunner(ctx, n, islands=int(knobs.get("islands", 8)), pop=max(2, min(pop, 4096)),
-                             seed=seed)
-        epochs = max(1, gens // r.gens_per_epoch)
-    elif algorithm == "aco":
-        its = int(iters or 100)
-        r = runners.ACORunner(ctx, n, colonies=int(knobs.get("colonies", 4)),
-                              ants=int(knobs.get("ants", 64)), seed=seed)
-        epochs = max(1, its // r.iters_per_epoch)
-    else:
-        raise ValueError(f"unknown algorithm {algorithm!r}; expected one of {ALGORITHMS}")
+    r, epochs = _runner(ctx, ci, algorithm, seed, knobs)
     t0 = time.perf_counter()
     e = 0
     while True:
@@ -232,17 +264,29 @@ def _remote():
     return None if torch.cuda.is_available() else remote
 
 
+def _searched(ci, algorithm, seed, time_limit, device, devices, objective, knobs):
+    """(context holding the instance, compact tour): one device, or the
+    island model across `devices` (two or more) for SA / GA / ACO."""
+    if devices is not None and len(devices) > 1 and algorithm != "bf" and ci.n > 1:
+        _, tour = search_islands(ci, algorithm, list(devices), seed=seed, time_limit=time_limit,
+                                 objective=objective, **knobs)
+        return context(devices[0]), tour
+    ctx = context(device)
+    load(ctx, ci, objective)
+    _, tour = search(ctx, ci, algorithm, seed=seed, time_limit=time_limit, **knobs)
+    return ctx, tour
+
+
 def solve_tsp(algorithm: str, durations, customers, start_node, start_time=0, *, seed: int = 0,
-              time_limit: float | None = None, device: int = 0, **knobs) -> dict:
-    """Result dict of the TSP TODO slot (api/tsp/ga/index.py:40-44)."""
+              time_limit: float | None = None, device: int = 0, devices=None, **knobs) -> dict:
+    """Result dict of the TSP TODO slot (api/tsp/ga/index.py:40-44).
+    `devices` (two or more): SA / GA / ACO as an island model across them."""
     rem = _remote()
     if rem is not None:
         return rem.solve_tsp(algorithm, durations, customers, start_node, start_time, seed=seed,
                              time_limit=time_limit, **knobs)
     ci = compact_tsp(durations, customers, start_node, start_time)
-    ctx = context(device)
-    load(ctx, ci)
-    _, tour = search(ctx, ci, algorithm, seed=seed, time_limit=time_limit, **knobs)
+    ctx, tour = _searched(ci, algorithm, seed, time_limit, device, devices, OBJ_SUM, knobs)
     _, dur = _decode(ctx, tour)
     vehicle = [ci.nodes[0]] + [ci.nodes[c] for c in tour] + [ci.nodes[0]]
     return {"duration": int(dur[0]), "vehicle": vehicle}
@@ -251,8 +295,9 @@ def solve_tsp(algorithm: str, durations, customers, start_node, start_time=0, *,
 def solve_vrp(algorithm: str, durations, locations, capacities, start_times,
               ignored_customers=(), completed_customers=(), *, seed: int = 0,
               objective: str = "sum", time_limit: float | None = None, device: int = 0,
-              with_unvisited: bool = False, **knobs) -> dict:
-    """Result dict of the VRP TODO slot (api/vrp/ga/index.py:48-53); A7 shapes."""
+              devices=None, with_unvisited: bool = False, **knobs) -> dict:
+    """Result dict of the VRP TODO slot (api/vrp/ga/index.py:48-53); A7 shapes.
+    `devices` (two or more): SA / GA / ACO as an island model across them."""
     rem = _remote()
     if rem is not None:
         out = rem.solve_vrp(algorithm, durations, locations, capacities, start_times,
@@ -266,9 +311,8 @@ def solve_vrp(algorithm: str, durations, locations, capacities, start_times,
         return out
     ci = compact_vrp(durations, locations, capacities, start_times, ignored_customers,
                      completed_customers)
-    ctx = context(device)
-    load(ctx, ci, OBJ_MAX if objective == "max" else OBJ_SUM)
-    _, tour = search(ctx, ci, algorithm, seed=seed, time_limit=time_limit, **knobs)
+    ctx, tour = _searched(ci, algorithm, seed, time_limit, device, devices,
+                          OBJ_MAX if objective == "max" else OBJ_SUM, knobs)
     K = len(ci.capacities)
     routes = [[] for _ in range(K)]
     unvisited = []
