@@ -303,38 +303,58 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
     return out
 
 
-def algo_quality(ctx, inst, seconds, seed=0):
+def algo_quality(ctx, inst, seconds, seed=0, polish_steps=50, polish_top=4):
     """The GA and ACO endpoints' best cost at the same wall time as the SA
     quality leg (cfg 2, api/vrp/{ga,aco}/index.py): each runs on the GPU for
     `seconds` of wall time -- GA 256 islands x 256 (randomPermutationCount),
     20 fused generations per epoch; ACO 64 colonies x 64 ants, 5 iterations
     per epoch, best-so-far deposit every 5th -- with elite migration every 5
-    epochs (inject(elites(16)), as the SA leg).  Their giant tours carry no
-    separators: the A3 greedy split places the route boundaries."""
+    epochs (inject(elites(16)), as the SA leg).  Both are memetic: after each
+    epoch the GA's `polish_top` best members of every island and ACO's colony
+    bests take `polish_steps` SA steps (runners.Polish, the SA endpoint's
+    moves), cooled from 0.05 to 0.002 x the mean edge over the wall-time
+    budget (_TimedCooling).  Their giant tours carry no separators: the A3
+    greedy split places the routes."""
     import torch
     from vrpms_amd import runners
     out = {}
+    edge = runners.typical_edge(inst.durations)
     for name in ("ga", "aco"):
+        pol = runners.Polish(polish_steps, inst.durations, seed=seed + 17) if polish_steps else None
         if name == "ga":
-            r = runners.GARunner(ctx, inst.n, islands=256, pop=256, seed=seed, gens_per_epoch=20)
+            r = runners.GARunner(ctx, inst.n, islands=256, pop=256, seed=seed, gens_per_epoch=20,
+                                 polish=pol, polish_top=polish_top)
             unit, per = "generations", 20
         else:
             r = runners.ACORunner(ctx, inst.n, colonies=64, ants=64, seed=seed,
-                                  iters_per_epoch=5, bsf_period=5)
+                                  iters_per_epoch=5, bsf_period=5, polish=pol)
             unit, per = "iterations", 5
         r.epoch()                              # first launch: code object load
         torch.cuda.synchronize(ctx.dev)
-        t0 = time.perf_counter()
-        e = 0
-        while time.perf_counter() - t0 < seconds:
+        cool = _TimedCooling(seconds, 0.05 * edge, 0.002 * edge)
+        e = done = 0
+        while True:
+            _, inv_a = cool.plan(done, min_steps=polish_steps or 1)
+            if inv_a is None:
+                break
+            if pol is not None:
+                pol.inv_t, pol.inv_alpha = cool.inv_t, inv_a
             r.epoch()
+            if pol is not None:
+                cool.advance(polish_steps, inv_a)
+                done += polish_steps
+            else:
+                done += 1
             e += 1
             if e % 5 == 0:
                 r.inject(*r.elites(16))
             torch.cuda.synchronize(ctx.dev)
-        wall = time.perf_counter() - t0
+        wall = cool.elapsed()
         key, _ = r.best()
         out[name] = {unit: (e + 1) * per, "epochs": e, "wall_s": wall,
+                     "memetic": {"polish_steps_per_epoch": polish_steps,
+                                 "polished": f"top {polish_top} per island" if name == "ga"
+                                 else "colony bests"} if pol is not None else None,
                      "unvisited": key >> 56, "duration_sum": (key >> 28) & (2**28 - 1)}
         del r
     return out

@@ -610,3 +610,48 @@ def test_aco_best_so_far_deposit_matches_oracle(ctx, name, maker):
         got_tau = tau.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
         assert all((got_tau[c] == rtau[c]).all() for c in range(colonies)), it
         assert bt.cpu().numpy().tolist() == rbest[0] and u64(bk) == rbest[1]
+
+
+@pytest.mark.parametrize("algo", ["ga", "aco"])
+def test_memetic_polish_matches_c_restatement(ctx, coracle, algo):
+    """The memetic step of the GA / ACO endpoints (runners.Polish): after an
+    epoch, the GA's top-T members of every island / ACO's colony bests are
+    the C restatement's SA best-so-far from the un-polished epoch's rows
+    (same Philox stream, temperature and step counter); every other GA slot
+    is the plain generation's."""
+    from vrpms_amd import runners
+    inst = synth.cvrp(60, 5, seed=21, slack=1.2)
+    load(ctx, inst)
+    pol = runners.Polish(25, inst.durations, seed=9)
+    inv_t, inv_a, pseed = float(pol.inv_t), float(pol.inv_alpha), pol.seed
+    if algo == "ga":
+        T = 3
+        r = runners.GARunner(ctx, inst.n, islands=4, pop=32, seed=5, gens_per_epoch=3,
+                             polish=pol, polish_top=T)
+        plain = runners.GARunner(ctx, inst.n, islands=4, pop=32, seed=5, gens_per_epoch=3)
+        r.epoch()
+        plain.epoch()
+        rows = plain.tours[:, :T, :].reshape(-1, inst.n).cpu().numpy().view(np.uint16).copy()
+        keys = u64(plain.keys[:, :T].reshape(-1))
+        got_t = r.tours[:, :T, :].reshape(-1, inst.n).cpu().numpy().view(np.uint16)
+        got_k = u64(r.keys[:, :T].reshape(-1))
+        assert torch_().equal(r.tours[:, T:], plain.tours[:, T:])
+        assert torch_().equal(r.keys[:, T:], plain.keys[:, T:])
+    else:
+        r = runners.ACORunner(ctx, inst.n, colonies=3, ants=16, seed=5, iters_per_epoch=2,
+                              polish=pol)
+        plain = runners.ACORunner(ctx, inst.n, colonies=3, ants=16, seed=5, iters_per_epoch=2)
+        r.epoch()
+        plain.epoch()
+        rows = plain.best_t.cpu().numpy().view(np.uint16).copy()
+        keys = u64(plain.best_key)
+        got_t = r.best_t.cpu().numpy().view(np.uint16)
+        got_k = u64(r.best_key)
+    cur, best = rows.copy(), rows.copy()
+    bk = np.array(keys, dtype=np.uint64)
+    coracle.sa_run(inst.durations, cur, best, bk, 25, inv_t, inv_a, pseed, 0, inst.demand,
+                   inst.capacities, inst.start_times)
+    assert (got_t == best).all()
+    assert got_k == [int(x) for x in bk]
+    assert all(g <= k for g, k in zip(got_k, keys))
+    assert any(g < k for g, k in zip(got_k, keys))      # the polish improved something

@@ -48,7 +48,7 @@ def run(chains, moves):
                          for k in range(K)])
     ctx.set_instance(CVRP, x.durations, x.demand, caps, x.start_times)
     edge = runners.typical_edge(x.durations)
-    NP = 18
+    NP = 22
     buf = (ctypes.c_ulonglong * (NP * 8192))()
     r = runners.SARunner(ctx, x.n, chains=chains, total_steps=1000, durations=x.durations,
                          n_sep=x.K - 1, window=32, window_types=2, start="pack", moves=moves)
@@ -71,7 +71,9 @@ def run(chains, moves):
               f"routes {a[10] / max(a[7], 1) * 10:.0f}, sparse {a[11] / max(a[7], 1) * 10:.0f}), "
               f"pricing parts per move (draw {a[12] / mv:.0f}, r1 {a[13] / mv:.0f}, r2 {a[14] / mv:.0f}, "
               f"r3 {a[15] / mv:.0f}, compose {a[16] / mv:.0f}, full {a[17] / mv:.0f}), "
-              f"accept rate {a[3] / st:.3f}, "
+              f"accept rate {a[3] / st:.3f}, cuts per step wave-max {a[18] / st:.2f} "
+              f"(lanes {a[19] / st:.1f} of 64), search steps wave-max {a[20] / st:.1f}, "
+              f"over-budget lanes {a[21] / st:.1f}, "
               f"exchange {a[4] / st * 10:.0f} ns, setup {a[5] / chains * 10 / 1e3:.1f} us, "
               f"kernel {a[6] / chains * 10 / 1e3:.1f} us/chain | best "
               f"{r.best()[0] >> 28 & (2**28 - 1)}", flush=True)

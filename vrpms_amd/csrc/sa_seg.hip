@@ -160,7 +160,7 @@ struct SegTabs {
 // outstanding load, so only roughly the kernel's own schedule): draw and
 // junction tokens, round 1, round 2, round 3, composition, full
 // re-evaluation (wall_clock64, 100 MHz)
-constexpr int kSegProf = 18;
+constexpr int kSegProf = 22;  // + cut iterations (wave max, lane sum), search steps (wave max), dead lanes
 __device__ unsigned long long g_seg_prof[kSegProf * 8192];
 #endif
 
@@ -608,6 +608,9 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
     const bool shortcut = (ck >> 56) == 0 && invT >= 0x1p-20f;
     uint64_t bkey = ~0ull;
     uint32_t bidx = 0xffffffffu, bw = 0;
+#ifdef VRPMS_SEG_PROF
+    int p_cut = 0, p_bs = 0, p_dead = 0;
+#endif
     Move bmv{0, 0, 0};
     uint32_t bj0 = 0, bj1 = 0, bj2 = 0, bj3 = 0;
 #pragma unroll 1
@@ -783,9 +786,15 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
             if (!fits) {
               if (cutc >= bud) {  // one cut more than the fleet allows: no search
                 dead = true;
+#ifdef VRPMS_SEG_PROF
+                ++p_dead;
+#endif
                 return;
               }
               ++cutc;
+#ifdef VRPMS_SEG_PROF
+              ++p_cut;
+#endif
               // first q in [x - 1, y + 1] with PD[q + 1] > thr, on the monotone
               // PD (one customer: it does not fit, q = x)
               const int thr = rev ? (int)(pdy - room) - 1 : (int)(pdx + room);
@@ -797,6 +806,9 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
               while (l < h) {
                 const int md = (l + h) >> 1;
                 if ((int)T.PD[md + 1] > thr) h = md; else l = md + 1;
+#ifdef VRPMS_SEG_PROF
+                ++p_bs;
+#endif
               }
               if (rev) pa = l + 1; else pb = l - 1;
             }
@@ -984,6 +996,19 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
 #ifdef VRPMS_SEG_PROF
     const unsigned long long px0 = wall_clock64();
     pf[0] += px0 - pt0;
+    {
+      int mc = p_cut, sc = p_cut, mb = p_bs, sd = p_dead;
+      for (int off = 32; off > 0; off >>= 1) {
+        mc = max(mc, __shfl_xor(mc, off, 64));
+        sc += __shfl_xor(sc, off, 64);
+        mb = max(mb, __shfl_xor(mb, off, 64));
+        sd += __shfl_xor(sd, off, 64);
+      }
+      pf[18] += (unsigned long long)mc;
+      pf[19] += (unsigned long long)sc;
+      pf[20] += (unsigned long long)mb;
+      pf[21] += (unsigned long long)sd;
+    }
 #endif
     if (W > 1) {
       SegXSlot* xb = xs + (st & 1) * kSegMaxWaves;

@@ -104,16 +104,20 @@ def gpu_launch(device: int, steps: int, seed: int):
     return launch
 
 
-def _owner_main(dev, arena, submit_q, done_qs, post_resp_q, make_launch, make_app, window_s,
+def _owner_main(dev, arena, submit_q, done_qs, stats_q, make_launch, make_app, window_s,
                 max_batch):
     """GPU owner of one device: coalesce the workers' slot lists, one launch
     per node count, answers into the arena, then each worker's done queue."""
     launch = make_launch(dev)
     app = None
+    st = {"device": dev, "batches": 0, "requests": 0, "stage_s": 0.0, "launch_s": 0.0,
+          "collect_s": 0.0, "max_batch": 0}
     while True:
         msg = submit_q.get()
         if msg is _STOP:
+            stats_q.put(("owner", st))
             return
+        tc = time.perf_counter()
         batch = [msg]
         deadline = time.perf_counter() + window_s
         n_slots = len(msg[2]) if msg[0] == "slots" else 0
@@ -132,46 +136,64 @@ def _owner_main(dev, arena, submit_q, done_qs, post_resp_q, make_launch, make_ap
             if m[0] == "slots":
                 n_slots += len(m[2])
         slots = [s for m in batch if m[0] == "slots" for s in m[2]]
+        t0 = time.perf_counter()
+        st["collect_s"] += t0 - tc
         if slots:
             sl = np.asarray(slots, dtype=np.int64)
             Ns = arena.N[sl]
+            st["batches"] += 1
+            st["requests"] += len(slots)
+            st["max_batch"] = max(st["max_batch"], len(slots))
             for N in np.unique(Ns):
                 grp = sl[Ns == N]
                 try:
+                    t1 = time.perf_counter()
                     host = np.ascontiguousarray(arena.mats[grp, :N, :N])
+                    t2 = time.perf_counter()
                     tours, durs = launch(int(N), host)
+                    t3 = time.perf_counter()
                     arena.tours[grp, :N - 1] = tours[:, :N - 1]
                     arena.dur[grp] = durs
                     arena.status[grp] = 0
+                    st["stage_s"] += t2 - t1
+                    st["launch_s"] += t3 - t2
                 except Exception as e:  # noqa: BLE001 -- every waiter of the group sees it
                     arena.status[grp] = 1
                     sys.stderr.write(f"owner {dev}: launch failed: {e}\n")
         for m in batch:
             if m[0] == "slots":
-                done_qs[m[1]].put(m[2])
+                done_qs[m[1]].put(("slots", m[3]))
             else:                        # ("post", worker, token, problem, algorithm, body)
                 _, w, token, problem, algorithm, body = m
                 if app is None:
                     app = make_app(dev)
                 before = len(app.store.solutions)
                 status, resp = app.post(problem, algorithm, body)
-                rows = app.store.solutions[before:]
+                rows = list(app.store.solutions[before:])
+                del app.store.solutions[before:]
                 done_qs[w].put(("post", token, status, resp, rows))
 
 
-def _worker_main(w, arena, lo, hi, req_q, resp_q, submit_qs, done_q, store, batchable_nmax):
+def _worker_main(w, arena, lo, hi, req_q, resp_q, submit_qs, done_q, store, batchable_nmax,
+                 stats_q, inflight=2):
     """Front-end worker: the request contract on the CPU, batchable TSP SA
-    requests through the arena and an owner (round-robin over owners)."""
+    requests through the arena and an owner (round-robin over owners).  Up
+    to `inflight` jobs at a time: the next chunk is parsed while the owner
+    runs the previous one."""
     from . import service, solver
     rr = w % len(submit_qs)
     free = list(range(lo, hi))
-    while True:
-        job = req_q.get()
-        if job is _STOP:
-            return
+    jobs = {}          # token -> job state
+    st = {"worker": w, "jobs": 0, "requests": 0, "parse_s": 0.0, "answer_s": 0.0, "idle_s": 0.0}
+    stop = False
+    token = 0
+
+    def start(job):
+        nonlocal rr, token
+        t0 = time.perf_counter()
         job_id, problem, algorithm, bodies = job
         out = [None] * len(bodies)
-        pending = []   # (index, slot, compact instance, params)
+        pending = []   # (index, slot, compact instance, params, locations, db)
         posts = {}
         before = len(store.solutions)
         for i, raw in enumerate(bodies):
@@ -215,29 +237,35 @@ def _worker_main(w, arena, lo, hi, req_q, resp_q, submit_qs, done_q, store, batc
             arena.mats[s, :N, :N] = ci.durations[0]
             arena.N[s] = N
             pending.append((i, s, ci, params, locations, db))
+        token += 1
+        waiting = (1 if pending else 0) + len(posts)
+        jobs[token] = {"id": job_id, "out": out, "pending": pending, "waiting": waiting,
+                       "rows": list(store.solutions[before:])}
+        del store.solutions[before:]
         if pending:
-            submit_qs[rr].put(("slots", w, [p[1] for p in pending]))
+            submit_qs[rr].put(("slots", w, [p[1] for p in pending], token))
             rr = (rr + 1) % len(submit_qs)
         for i, raw in posts.items():   # the unbatched path on an owner
-            submit_qs[rr].put(("post", w, i, problem, algorithm, raw))
+            submit_qs[rr].put(("post", w, (token, i), problem, algorithm, raw))
             rr = (rr + 1) % len(submit_qs)
-        rows = []
-        waiting = 1 if pending else 0
-        waiting += len(posts)
-        while waiting:
-            m = done_q.get()
-            waiting -= 1
-            if isinstance(m, tuple) and m and m[0] == "post":
-                _, i, status, resp, saved = m
-                out[i] = (status, resp)
-                rows += saved
-        for i, s, ci, params, locations, db in pending:
+        st["jobs"] += 1
+        st["requests"] += len(bodies)
+        st["parse_s"] += time.perf_counter() - t0
+        if waiting == 0:
+            finish(token)
+
+    def finish(tk):
+        t0 = time.perf_counter()
+        j = jobs.pop(tk)
+        out = j["out"]
+        before = len(store.solutions)
+        for i, s, ci, params, locations, db in j["pending"]:
             if arena.status[s] != 0:
                 out[i] = (400, {"success": False, "errors": [
                     {"what": "Solver error", "reason": "batched launch failed"}]})
             else:
                 N = ci.N
-                path = [0] + [int(c) for c in arena.tours[s, :N - 1]] + [0]
+                path = [0] + arena.tours[s, :N - 1].tolist() + [0]
                 result = {"duration": int(arena.dur[s]), "vehicle": [ci.nodes[c] for c in path]}
                 errors = []
                 if params["auth"]:
@@ -248,9 +276,39 @@ def _worker_main(w, arena, lo, hi, req_q, resp_q, submit_qs, done_q, store, batc
                 out[i] = (400, {"success": False, "errors": errors}) if errors else \
                     (200, {"success": True, "message": result})
             free.append(s)
-        rows = list(store.solutions[before:]) + rows
+        rows = j["rows"] + list(store.solutions[before:])
         del store.solutions[before:]
-        resp_q.put((job_id, out, rows))
+        resp_q.put((j["id"], out, rows))
+        st["answer_s"] += time.perf_counter() - t0
+
+    while not (stop and not jobs):
+        if not stop and len(jobs) < inflight:
+            try:
+                job = req_q.get() if not jobs else req_q.get_nowait()
+            except queue.Empty:
+                pass            # jobs in flight, none waiting: wait for an answer below
+            else:
+                if job is _STOP:
+                    stop = True
+                else:
+                    start(job)
+                continue
+        if not jobs:
+            continue
+        t0 = time.perf_counter()
+        m = done_q.get()
+        st["idle_s"] += time.perf_counter() - t0
+        if m[0] == "slots":
+            tk = m[1]
+            jobs[tk]["waiting"] -= 1
+        else:                                   # ("post", (token, index), status, resp, rows)
+            _, (tk, i), status, resp, saved = m
+            jobs[tk]["out"][i] = (status, resp)
+            jobs[tk]["rows"] += saved
+            jobs[tk]["waiting"] -= 1
+        if jobs[tk]["waiting"] == 0:
+            finish(tk)
+    stats_q.put(("worker", st))
 
 
 def _default_app(store, seed, steps):
@@ -278,20 +336,22 @@ class FrontEndPool:
         self._req_qs = [ctx.Queue() for _ in range(self.workers)]
         self._done_qs = [ctx.Queue() for _ in range(self.workers)]
         self._submit_qs = [ctx.Queue() for _ in self.devices]
+        self._stats_q = ctx.Queue()
+        self.stats = []
         make_launch = launch_factory or (lambda dev: gpu_launch(dev, steps, seed))
         make_app = app_factory or _default_app(store, seed, steps)
         self._procs = []
         for d, dev in enumerate(self.devices):
             p = ctx.Process(target=_owner_main, daemon=True, name=f"vrpms-owner{dev}",
-                            args=(dev, self.arena, self._submit_qs[d], self._done_qs, None,
-                                  make_launch, make_app, window_s, max_batch))
+                            args=(dev, self.arena, self._submit_qs[d], self._done_qs,
+                                  self._stats_q, make_launch, make_app, window_s, max_batch))
             p.start()
             self._procs.append(p)
         for w in range(self.workers):
             p = ctx.Process(target=_worker_main, daemon=True, name=f"vrpms-front{w}",
                             args=(w, self.arena, w * slots_per_worker, (w + 1) * slots_per_worker,
                                   self._req_qs[w], self._resp_q, self._submit_qs,
-                                  self._done_qs[w], store, nmax))
+                                  self._done_qs[w], store, nmax, self._stats_q))
             p.start()
             self._procs.append(p)
         self._next_job = 0
@@ -319,8 +379,20 @@ class FrontEndPool:
             return out
 
     def close(self):
-        for q in self._req_qs + self._submit_qs:
+        for q in self._req_qs:
             q.put(_STOP)
+        for _ in range(self.workers):           # workers drain before the owners stop
+            try:
+                self.stats.append(self._stats_q.get(timeout=30))
+            except queue.Empty:
+                break
+        for q in self._submit_qs:
+            q.put(_STOP)
+        for _ in self.devices:
+            try:
+                self.stats.append(self._stats_q.get(timeout=30))
+            except queue.Empty:
+                break
         for p in self._procs:
             p.join(timeout=10)
             if p.is_alive():
@@ -354,6 +426,9 @@ def bench_api(R: int = 10000, N: int = 50, workers: int = 16, steps: int = 1000,
         res = pool.post_many("tsp", "sa", bodies)
         dt = time.perf_counter() - t0
     ok = sum(1 for st, _ in res if st == 200)
+    owners = [x for kind, x in pool.stats if kind == "owner"]
+    wk = [x for kind, x in pool.stats if kind == "worker"]
+    agg = {k: sum(x[k] for x in wk) for k in ("parse_s", "answer_s", "idle_s", "requests")}
     # each sampled answer's duration is its closed tour's cost (A4: a static
     # matrix, start time 0 -- the sum of the tour's edges) and its tour visits
     # every customer once
@@ -370,7 +445,11 @@ def bench_api(R: int = 10000, N: int = 50, workers: int = 16, steps: int = 1000,
                         f"+ 1 GPU-owner process (vrpms_amd.frontends.FrontEndPool)",
             "requests_per_s": R / dt, "wall_s": dt, "ok": ok, "workers": workers,
             "batch_window_ms": window_ms, "sa_steps_per_chain": steps,
-            "duration_checked": int(len(idx)), "duration_mismatches": bad}
+            "duration_checked": int(len(idx)), "duration_mismatches": bad,
+            "owners": owners,
+            "workers_total": {k: round(v, 4) if isinstance(v, float) else v
+                              for k, v in agg.items()},
+            "note": "owner/worker times include the warm-up batch"}
 
 
 def main(argv=None):

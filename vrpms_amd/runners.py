@@ -120,19 +120,61 @@ class SARunner(_Base):
         return self.cur, self.cur_key
 
 
+class Polish:
+    """The memetic step of the GA / ACO endpoints (api/vrp/{ga,aco}/index.py):
+    `steps` SA steps (vrpms_sa_run: the same moves, Philox streams and
+    acceptance as the SA endpoint) on some rows of a pool, whose best-so-far
+    tours and keys then replace those rows.  The temperature cools
+    geometrically from t0 to t_end over `total_steps` polish steps (or by
+    whatever inv_t / inv_alpha the caller sets, e.g. a wall-time schedule);
+    the Philox stream is the pool's seed ^ 0x9E3779B9 with the step counter
+    running across calls."""
+
+    def __init__(self, steps: int, durations=None, t0: float | None = None,
+                 t_end: float | None = None, total_steps: int = 20000, seed: int = 0):
+        edge = typical_edge(durations) if durations is not None else 100.0
+        t0 = t0 if t0 is not None else 0.05 * edge
+        t_end = t_end if t_end is not None else 0.002 * edge
+        self.steps = int(steps)
+        self.inv_t = np.float32(1.0 / t0)
+        self.inv_alpha = np.float32((t0 / t_end) ** (1.0 / max(total_steps, 1)))
+        self.seed = (int(seed) ^ 0x9E3779B9) & (2**64 - 1)
+        self.step = 0
+
+    def run(self, ctx: Context, rows, keys):
+        """SA from each row of `rows` (int16 [R][n], contiguous); returns the
+        chains' best (tours, keys) -- never worse than the rows' own keys."""
+        torch = _torch()
+        cur = rows.clone()
+        best = rows.clone()
+        ck = torch.empty(rows.shape[0], dtype=torch.int64, device=rows.device)
+        bk = keys.clone()
+        ctx.sa_run(cur, ck, best, bk, self.steps, float(self.inv_t), float(self.inv_alpha),
+                   self.seed, self.step)
+        for _ in range(self.steps):       # the kernel's float32 recurrence
+            self.inv_t = np.float32(self.inv_t * self.inv_alpha)
+        self.step += self.steps
+        return best, bk
+
+
 class GARunner(_Base):
     """Island GA: `islands` populations of `pop` members, each kept sorted by
-    (key, index); migrants take the worst slots of the islands round robin."""
+    (key, index); migrants take the worst slots of the islands round robin.
+    `polish` (a Polish): after each epoch's generations the `polish_top`
+    best members of every island are improved by SA (memetic GA) and put
+    back in their slots (the next generation re-sorts the islands)."""
 
     inject_mode = INJECT_SORTED
 
     def __init__(self, ctx: Context, n: int, islands: int = 8, pop: int = 256, seed: int = 0,
-                 pmut: float = 0.2, gens_per_epoch: int = 20):
+                 pmut: float = 0.2, gens_per_epoch: int = 20, polish: Polish | None = None,
+                 polish_top: int = 4):
         self.ctx, self.n, self.seed = ctx, n, seed
         self.islands, self.pop, self.pmut = islands, pop, pmut
         self.gens_per_epoch = gens_per_epoch
         self.gen = 0
         self.groups = islands
+        self.polish, self.polish_top = polish, max(1, min(polish_top, pop))
         self.tours = random_tours(ctx, islands * pop, n, seed).view(islands, pop, n).contiguous()
         self.keys = ctx.eval(self.tours.view(-1, n)).view(islands, pop)
 
@@ -140,6 +182,13 @@ class GARunner(_Base):
         g = self.gens_per_epoch if gens is None else gens
         self.ctx.ga_generation(self.tours, self.keys, g, self.pmut, self.seed, self.gen)
         self.gen += g
+        if self.polish is not None and self.n >= 2:
+            T = self.polish_top
+            rows = self.tours[:, :T, :].reshape(-1, self.n).contiguous()
+            keys = self.keys[:, :T].reshape(-1).contiguous()
+            best, bk = self.polish.run(self.ctx, rows, keys)
+            self.tours[:, :T, :] = best.view(self.islands, T, self.n)
+            self.keys[:, :T] = bk.view(self.islands, T)
 
     def src(self):
         return self.tours, self.keys
@@ -157,7 +206,8 @@ class ACORunner(_Base):
     inject_mode = INJECT_BETTER
 
     def __init__(self, ctx: Context, n: int, colonies: int = 4, ants: int = 64, seed: int = 0,
-                 iters_per_epoch: int = 5, evap_shift: int = 3, bsf_period: int = 5):
+                 iters_per_epoch: int = 5, evap_shift: int = 3, bsf_period: int = 5,
+                 polish: Polish | None = None):
         torch = _torch()
         if n != ctx.N - 1:
             raise ValueError("ACO builds complete giant tours: n must be N - 1")
@@ -170,14 +220,22 @@ class ACORunner(_Base):
         self.it = 0
         self.best_key = torch.full((colonies,), -1, dtype=torch.int64, device=ctx.dev)
         self.best_t = torch.zeros((colonies, n), dtype=torch.int16, device=ctx.dev)
+        self.polish = polish
 
     def epoch(self, iters: int | None = None):
+        """`polish` (a Polish): after the epoch's iterations every colony's
+        best-so-far is improved by SA (ACO with local search), so the next
+        best-so-far deposit lays pheromone on the improved tour."""
         for _ in range(self.iters_per_epoch if iters is None else iters):
             self.ctx.aco_iteration(self.tau, self.eta, self.ants, self.seed, self.it,
                                    self.evap_shift, self.tau_min, self.tau_max,
                                    best_tours=self.best_t, best_keys=self.best_key,
                                    bsf_period=self.bsf_period)
             self.it += 1
+        if self.polish is not None and self.n >= 2:
+            best, bk = self.polish.run(self.ctx, self.best_t.contiguous(), self.best_key)
+            self.best_t.copy_(best)
+            self.best_key.copy_(bk)
 
     # migrant e replaces colony e's best-so-far when better
     def src(self):
