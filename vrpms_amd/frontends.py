@@ -74,96 +74,148 @@ class Arena:
             pass
 
 
-def gpu_launch(device: int, steps: int, seed: int):
-    """The owner's default launch: (N, int32 [R][N][N]) -> (tours int16
-    [R][N-1], durations int64 [R]) through vrpms_tsp_batch_sa on `device`,
-    the temperature schedule scaled to the batch's mean edge (as
+def gpu_launch(device: int, steps: int, seed: int, streams: int = 3):
+    """The owner's default launch: (N, int32 [R][N][N]) -> a finish() that
+    returns (tours int16 [R][N-1], durations int64 [R]) once
+    vrpms_tsp_batch_sa on `device` has run.  The launch is asynchronous: the
+    matrices go up from a pinned buffer and the answers come back into
+    pinned buffers on one of `streams` streams (round-robin), so the owner
+    stages and launches the next batch while this one runs, and a small
+    batch (fewer workgroups than the chip holds) runs beside the previous
+    one.  The temperature schedule is scaled to the batch's mean edge (as
     service.TspBatcher)."""
-    state = {}
+    state = {"k": 0}
 
     def launch(N, host):
         import torch
         from . import solver
         if "ctx" not in state:
             state["ctx"] = solver.context(device)
+            state["streams"] = [torch.cuda.Stream(device=device) for _ in range(streams)]
         ctx = state["ctx"]
+        stream = state["streams"][state["k"] % streams]
+        state["k"] += 1
+        R = host.shape[0]
         nz = host[host > 0]
         edge = float(nz.mean()) if nz.size else 1.0
         inv_t0 = 1.0 / (0.5 * edge)
         inv_alpha = (0.5 / 0.002) ** (1.0 / max(1, steps))
-        mats = torch.from_numpy(host).to(ctx.dev, non_blocking=False)
-        tours, keys = ctx.tsp_batch_sa(mats, steps, inv_t0, inv_alpha, seed)
-        tours, keys = tours.cpu().numpy(), keys.cpu().numpy().view(np.uint64)
-        clamp = (1 << 28) - 1
-        durs = ((keys >> np.uint64(28)) & np.uint64(clamp)).astype(np.int64)
-        # a clamped key (2^28 - 1) is summed on the host from the tour
-        for x in np.flatnonzero(durs == clamp):
-            path = [0] + [int(c) for c in tours[x]] + [0]
-            durs[x] = int(sum(int(host[x, a, b]) for a, b in zip(path, path[1:])))
-        return tours, durs
+        pin = torch.from_numpy(host).pin_memory()
+        tours_h = torch.empty((R, max(N - 1, 1)), dtype=torch.int16, pin_memory=True)
+        keys_h = torch.empty(R, dtype=torch.int64, pin_memory=True)
+        with torch.cuda.stream(stream):
+            mats = pin.to(ctx.dev, non_blocking=True)
+            tours, keys = ctx.tsp_batch_sa(mats, steps, inv_t0, inv_alpha, seed)
+            tours_h.copy_(tours, non_blocking=True)
+            keys_h.copy_(keys, non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(stream)
+        keep = (pin, mats, tours, keys)   # alive until the stream is done with them
+
+        def finish():
+            done.synchronize()
+            del keep
+            t = tours_h.numpy()
+            k = keys_h.numpy().view(np.uint64)
+            clamp = (1 << 28) - 1
+            durs = ((k >> np.uint64(28)) & np.uint64(clamp)).astype(np.int64)
+            # a clamped key (2^28 - 1) is summed on the host from the tour
+            for x in np.flatnonzero(durs == clamp):
+                path = [0] + [int(c) for c in t[x]] + [0]
+                durs[x] = int(sum(int(host[x, a, b]) for a, b in zip(path, path[1:])))
+            return t, durs
+        return finish
     return launch
 
 
 def _owner_main(dev, arena, submit_q, done_qs, stats_q, make_launch, make_app, window_s,
-                max_batch):
+                max_batch, max_inflight=2):
     """GPU owner of one device: coalesce the workers' slot lists, one launch
-    per node count, answers into the arena, then each worker's done queue."""
+    per node count, answers into the arena, then each worker's done queue.
+    A launch may return its answers at once or a finish() (asynchronous
+    launches): up to `max_inflight` batches are then on the device while the
+    next one is collected and staged."""
+    from collections import deque
     launch = make_launch(dev)
     app = None
     st = {"device": dev, "batches": 0, "requests": 0, "stage_s": 0.0, "launch_s": 0.0,
-          "collect_s": 0.0, "max_batch": 0}
-    while True:
-        msg = submit_q.get()
-        if msg is _STOP:
-            stats_q.put(("owner", st))
-            return
-        tc = time.perf_counter()
-        batch = [msg]
-        deadline = time.perf_counter() + window_s
-        n_slots = len(msg[2]) if msg[0] == "slots" else 0
-        while n_slots < max_batch:
-            left = deadline - time.perf_counter()
-            if left <= 0:
-                break
+          "wait_s": 0.0, "collect_s": 0.0, "max_batch": 0}
+    pending = deque()          # (messages, [(group slots, N, answers or finish)])
+    stopping = False
+
+    def complete():
+        msgs, groups = pending.popleft()
+        for grp, N, res in groups:
             try:
-                m = submit_q.get(timeout=left)
-            except queue.Empty:
-                break
-            if m is _STOP:
-                submit_q.put(_STOP)      # finish this batch, stop on the next get
-                break
-            batch.append(m)
-            if m[0] == "slots":
-                n_slots += len(m[2])
-        slots = [s for m in batch if m[0] == "slots" for s in m[2]]
-        t0 = time.perf_counter()
-        st["collect_s"] += t0 - tc
-        if slots:
-            sl = np.asarray(slots, dtype=np.int64)
+                t0 = time.perf_counter()
+                tours, durs = res() if callable(res) else res
+                st["wait_s"] += time.perf_counter() - t0
+                arena.tours[grp, :N - 1] = tours[:, :N - 1]
+                arena.dur[grp] = durs
+                arena.status[grp] = 0
+            except Exception as e:  # noqa: BLE001 -- every waiter of the group sees it
+                arena.status[grp] = 1
+                sys.stderr.write(f"owner {dev}: launch failed: {e}\n")
+        for m in msgs:
+            done_qs[m[1]].put(("slots", m[3]))
+
+    while not (stopping and not pending):
+        batch = []
+        n_slots = 0
+        tc = time.perf_counter()
+        if not stopping:
+            if not pending:              # idle: wait for work, then a short window for company
+                msg = submit_q.get()
+                batch.append(msg)
+                deadline = time.perf_counter() + window_s
+            else:                        # busy: take what is queued, no window
+                deadline = None
+            while True:
+                try:
+                    if deadline is None:
+                        m = submit_q.get_nowait()
+                    else:
+                        left = deadline - time.perf_counter()
+                        if left <= 0:
+                            break
+                        m = submit_q.get(timeout=left)
+                except queue.Empty:
+                    break
+                batch.append(m)
+                if m is not _STOP and m[0] == "slots":
+                    n_slots += len(m[2])
+                    if n_slots >= max_batch:
+                        break
+            if batch and batch[0] is _STOP or any(m is _STOP for m in batch):
+                stopping = True
+                batch = [m for m in batch if m is not _STOP]
+        st["collect_s"] += time.perf_counter() - tc
+        slot_msgs = [m for m in batch if m[0] == "slots"]
+        if slot_msgs:
+            sl = np.asarray([x for m in slot_msgs for x in m[2]], dtype=np.int64)
             Ns = arena.N[sl]
             st["batches"] += 1
-            st["requests"] += len(slots)
-            st["max_batch"] = max(st["max_batch"], len(slots))
+            st["requests"] += len(sl)
+            st["max_batch"] = max(st["max_batch"], len(sl))
+            groups = []
             for N in np.unique(Ns):
                 grp = sl[Ns == N]
+                t1 = time.perf_counter()
+                host = np.ascontiguousarray(arena.mats[grp, :N, :N])
+                t2 = time.perf_counter()
                 try:
-                    t1 = time.perf_counter()
-                    host = np.ascontiguousarray(arena.mats[grp, :N, :N])
-                    t2 = time.perf_counter()
-                    tours, durs = launch(int(N), host)
-                    t3 = time.perf_counter()
-                    arena.tours[grp, :N - 1] = tours[:, :N - 1]
-                    arena.dur[grp] = durs
-                    arena.status[grp] = 0
-                    st["stage_s"] += t2 - t1
-                    st["launch_s"] += t3 - t2
-                except Exception as e:  # noqa: BLE001 -- every waiter of the group sees it
-                    arena.status[grp] = 1
+                    res = launch(int(N), host)
+                except Exception as e:  # noqa: BLE001
                     sys.stderr.write(f"owner {dev}: launch failed: {e}\n")
+
+                    def res(e=e):
+                        raise e
+                st["stage_s"] += t2 - t1
+                st["launch_s"] += time.perf_counter() - t2
+                groups.append((grp, int(N), res))
+            pending.append((slot_msgs, groups))
         for m in batch:
-            if m[0] == "slots":
-                done_qs[m[1]].put(("slots", m[3]))
-            else:                        # ("post", worker, token, problem, algorithm, body)
+            if m[0] == "post":           # ("post", worker, token, problem, algorithm, body)
                 _, w, token, problem, algorithm, body = m
                 if app is None:
                     app = make_app(dev)
@@ -172,10 +224,16 @@ def _owner_main(dev, arena, submit_q, done_qs, stats_q, make_launch, make_app, w
                 rows = list(app.store.solutions[before:])
                 del app.store.solutions[before:]
                 done_qs[w].put(("post", token, status, resp, rows))
+        # answer the oldest batch when the device holds enough, or nothing new came
+        while pending and (len(pending) > max_inflight or not slot_msgs or stopping):
+            complete()
+            if slot_msgs and not stopping:
+                break
+    stats_q.put(("owner", st))
 
 
 def _worker_main(w, arena, lo, hi, req_q, resp_q, submit_qs, done_q, store, batchable_nmax,
-                 stats_q, inflight=2):
+                 stats_q, inflight=3):
     """Front-end worker: the request contract on the CPU, batchable TSP SA
     requests through the arena and an owner (round-robin over owners).  Up
     to `inflight` jobs at a time: the next chunk is parsed while the owner
@@ -323,6 +381,8 @@ class FrontEndPool:
     the module docstring).  post_many() answers a list of request bodies for
     one endpoint with the (status, response dict) pairs App.post would give."""
 
+    INFLIGHT = 3   # jobs a worker keeps in flight
+
     def __init__(self, store, workers: int = 16, devices=(0,), steps: int = 1000, seed: int = 0,
                  window_s: float = 0.002, slots_per_worker: int = 1024, nmax: int = 64,
                  chunk: int = 64, max_batch: int = 16384, launch_factory=None, app_factory=None):
@@ -331,6 +391,9 @@ class FrontEndPool:
         if not self.devices or self.workers < 1:
             raise ValueError("FrontEndPool needs at least one worker and one device")
         ctx = mp.get_context("fork")
+        # every job a worker has in flight needs its slots (else its requests
+        # take the unbatched path)
+        slots_per_worker = max(int(slots_per_worker), self.INFLIGHT * self.chunk)
         self.arena = Arena(self.workers * slots_per_worker, nmax)
         self._resp_q = ctx.Queue()
         self._req_qs = [ctx.Queue() for _ in range(self.workers)]
@@ -351,7 +414,7 @@ class FrontEndPool:
             p = ctx.Process(target=_worker_main, daemon=True, name=f"vrpms-front{w}",
                             args=(w, self.arena, w * slots_per_worker, (w + 1) * slots_per_worker,
                                   self._req_qs[w], self._resp_q, self._submit_qs,
-                                  self._done_qs[w], store, nmax, self._stats_q))
+                                  self._done_qs[w], store, nmax, self._stats_q, self.INFLIGHT))
             p.start()
             self._procs.append(p)
         self._next_job = 0

@@ -91,11 +91,13 @@ def compact_tsp(durations, customers, start_node, start_time=0) -> CompactInstan
     if not 0 <= start < N:
         raise ValueError(f"startNode {start} outside the {N}-node matrix")
     nodes = [start]
+    seen = {start}
     for c in customers or []:
         c = int(c)
         if not 0 <= c < N:
             raise ValueError(f"customer {c} outside the {N}-node matrix")
-        if c not in nodes:
+        if c not in seen:
+            seen.add(c)
             nodes.append(c)
     # every node in matrix order (the common request): no copy
     sub = D if nodes == list(range(N)) else D[:, nodes][:, :, nodes]
