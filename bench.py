@@ -198,7 +198,7 @@ class _TimedCooling:
 
 def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label="cvrp100_k8 seed 0",
             gpu_seed=None, n_sep=None, window=0, window_types=0, start="random", moves=64,
-            cpu_moves=64, gpu=True):
+            cpu_moves=64, gpu=True, mig_every=5, mig_E=16):
     """Best-cost gap at fixed wall time (the metric's second half): the same SA
     (Philox streams, 64 sampled moves per step, geometric cooling from
     0.5 to 0.002 x the mean edge spread over the wall-time budget by
@@ -248,17 +248,18 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
             r.epoch(steps)
             cool.advance(steps, inv_a)
             e += 1
-            if e % 5 == 0:
+            if e % mig_every == 0:
                 if world > 1:
-                    islands.exchange(r, 16)
+                    islands.exchange(r, mig_E)
                 else:
-                    r.inject(*r.elites(16))
+                    r.inject(*r.elites(mig_E))
             torch.cuda.synchronize(dev)
         gpu_wall = cool.elapsed()
         key, tour = r.best()
         if world > 1:
             key, _ = islands.global_best(r)
         out["gpu"] = {"chains_per_gpu": chains, "moves_per_step": moves, "steps_per_chain": r.step,
+                      "migration": {"every_epochs": mig_every, "elites": mig_E},
                       "epochs": e, "wall_s": gpu_wall, "unvisited": key >> 56,
                       "duration_sum": (key >> 28) & (2**28 - 1)}
     if with_cpu:

@@ -1,0 +1,5 @@
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+timeout -k 10 200 python -m vrpms_amd.frontends bench --workers 14 > gpurun_out/fe_bench3.log 2>&1 || exit $?
+TSEL="segment or route_local or sa_with_sep" bash tools/gpu_run.sh tsel || exit $?

@@ -1,0 +1,24 @@
+#!/usr/bin/env python3
+"""GPU SA leg on X-1000 (cfg 4) at T seconds for several elite-migration
+settings (every k epochs, E elites into the worst chains); GPU only.
+usage: migration_scan.py T seed every:E [every:E ...]"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from vrpms_amd import synth  # noqa: E402
+from vrpms_amd.core import CVRP, Context  # noqa: E402
+
+T, seed = float(sys.argv[1]), int(sys.argv[2])
+ctx = Context(0)
+x = synth.x_style(1000, seed=seed)
+ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
+for spec in sys.argv[3:]:
+    every, E = (int(v) for v in spec.split(":"))
+    q = bench.quality(ctx, x, T, 1, 0, None, with_cpu=False, chains=256, moves=128, window=32,
+                      window_types=2, start="pack", mig_every=every, mig_E=E)
+    print(json.dumps({"every": every, "E": E, "gpu": q["gpu"]["duration_sum"],
+                      "steps": q["gpu"]["steps_per_chain"], "epochs": q["gpu"]["epochs"]}),
+          flush=True)

@@ -77,13 +77,13 @@ constexpr uint32_t kSegXBytes = 2 * kSegMaxWaves * sizeof(SegXSlot) + 32;
 
 // per-chain LDS: u32 [PE n+2 | PD n+2 | LG n+2 | dur rm+1 | dsp, pmx, smx rm+1
 // each | sparse (lv-1) x rm | (het) need, allow rm+1 each], then u16 [tok n+2 |
-// SC n+2 | SP, RB, FNE, LNE1 segs+2 | (het) NB 2 kSegShift x (rm+1) | SEGR rm+1 |
-// cend K]
+// SC n+2 | SP, RB, FNE, LNE1 segs+2 | RS rm+1 | (het) NB 2 kSegShift x (rm+1) |
+// SEGR rm+1 | cend K]
 __host__ __device__ inline uint32_t seg_chain_bytes(int n, int segs, int rm, int lv, bool het, int K) {
   const uint32_t np2 = ((uint32_t)n + 2u + 1u) & ~1u;
   const uint32_t u32s = 3u * np2 + 4u * (uint32_t)(rm + 1) + (uint32_t)(lv - 1) * (uint32_t)rm +
                         (het ? 2u * (uint32_t)(rm + 1) : 0u);
-  const uint32_t u16s = 2u * np2 + 4u * (uint32_t)(segs + 2) +
+  const uint32_t u16s = 2u * np2 + 4u * (uint32_t)(segs + 2) + (uint32_t)(rm + 1) +
                         (het ? (2u * kSegShift + 1u) * (uint32_t)(rm + 1) + (uint32_t)K : 0u);
   return ((4u * u32s + 2u * u16s + 15u) & ~15u) + kSegXBytes;
 }
@@ -142,6 +142,7 @@ VRPMS_DEV uint32_t dpp_rscan_max(uint32_t v, uint32_t& total) {
 struct SegTabs {
   uint32_t *PE, *PD, *LG, *dur, *dsp, *pmx, *smx, *sp;  // LG[q] = leg of the token at q
   uint16_t *tok, *SC, *SP, *RB, *FNE, *LNE1;
+  uint16_t* RS;  // RS[r] = the first position of route r
   // heterogeneous fleets: per route its load (need) and the largest capacity
   // that splits it the same (allow); NB[d][r] = the first route >= r that
   // would split differently on vehicle r + delta(d) (R: none), delta =
@@ -217,6 +218,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
     T.RB = T.SP + (SEGS + 2);
     T.FNE = T.RB + (SEGS + 2);
     T.LNE1 = T.FNE + (SEGS + 2);
+    T.RS = T.LNE1 + (SEGS + 2);
     T.need = T.allow = nullptr;
     T.NB = T.SEGR = T.cend = nullptr;
     if (HET) {
@@ -229,7 +231,8 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
       T.RB = T.SP + (SEGS + 2);
       T.FNE = T.RB + (SEGS + 2);
       T.LNE1 = T.FNE + (SEGS + 2);
-      T.NB = T.LNE1 + (SEGS + 2);
+      T.RS = T.LNE1 + (SEGS + 2);
+      T.NB = T.RS + (RM + 1);
       T.SEGR = T.NB + 2 * kSegShift * (RM + 1);
       T.cend = T.SEGR + (RM + 1);
       // cend[v] = the first u >= v whose successor's capacity differs: a
@@ -443,6 +446,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
     for (int g = lane; g <= S; g += 64) {
       const int s0 = SPX(g - 1) + 1, s1 = SPX(g) - 1;
       int r = T.RB[g], x = s0;
+      T.RS[r] = (uint16_t)s0;
       while (x <= s1 && T.PD[s1 + 1] - T.PD[x] > capv(r)) {
         const uint32_t thr = T.PD[x] + capv(r);
         int l = x, h = s1;
@@ -458,6 +462,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
         // route: depot -> A[x..l-1] -> depot
         T.dur[r++] = leg[T.tok[x]] + T.PE[l] - T.PE[x + 1] + leg[T.tok[l - 1]];
         x = l;
+        T.RS[r] = (uint16_t)l;
       }
       // the last (or only) route: A[x..s1], closed by the separator (or the end)
       if (HET) {
@@ -678,7 +683,8 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
         // round 2: separator positions, route indices
         const int stp = SPX(s0 - 1) + 1, en = SPX(sH);
         const int ra = T.RB[s0], rz = T.RB[sH + 1];  // sH = the last changed segment
-        int SMIN[3], SMAX[3], R0[3], R1[3], GF[3];
+        const int ra1 = T.RB[s0 + 1];                // routes ra .. ra1 - 1 hold segment s0
+        int SMIN[3], SMAX[3], R0[3], R1[3], GF[3], RG0[3], RG1[3];
 #pragma unroll
         for (int s = 0; s < 3; ++s) {
           const bool hs = SA[s] != SB[s], rev = opt && s == 0;
@@ -689,6 +695,9 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
           const bool mid = SB[s] - SA[s] >= 2;
           R0[s] = mid ? (int)T.RB[SA[s] + 1] : 0;
           R1[s] = mid ? (int)T.RB[SB[s]] : 0;
+          // (forward) the segment after the piece's last separator: its routes
+          RG0[s] = hs && !rev ? (int)T.RB[SB[s]] : 0;
+          RG1[s] = hs && !rev ? (int)T.RB[SB[s] + 1] : 0;
           GF[s] = mid ? (rev ? (int)T.FNE[SA[s] + 1] : (int)T.LNE1[SB[s] - 1] - 1) : 0;
         }
         SEG_PT(14);
@@ -735,8 +744,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
         // (their cuts: (ra - s0) + (R - rz) - (S - sH)); once the composed
         // segments' cuts exceed what is left the move's key is the largest
         // (exactly what the fleet count below would give), so an overflowing
-        // run stops there instead of binary-searching its cuts.  In a tour of
-        // full routes (the cold phase) almost every overflow ends here.
+        // run stops there instead of binary-searching its cuts.
         const bool tail_kept = en < n && lneS - 1 > sH;
         const int bud = (!HET && shortcut && tail_kept)
                             ? (K - 1 - S + Tt) - ((ra - s0) + (R - rz) - (S - sH))
@@ -835,6 +843,34 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
             }
           }
         };
+        // A fresh vehicle at the start of segment g (routes g_r0 .. g_r1 - 1)
+        // taking its customers up to y in the current order, on the current
+        // vehicles: the current tour's split.  Its routes before the one
+        // holding y are closed from the tables, that route's part up to y is
+        // the open route -- no capacity cut is searched.  (Segments of one
+        // route go through run(): their prefix never cuts.)
+        auto aligned = [&](const RunP& p, int g_r0, int g_r1) __attribute__((always_inline)) {
+          if (p.x > p.y || dead) return;
+          seps = 0;
+          cust = true;
+          int l = g_r0, h = g_r1 - 1;  // the last route starting at or before y
+          while (l < h) {
+            const int md = (l + h + 1) >> 1;
+            if ((int)T.RS[md] <= p.y) l = md; else h = md - 1;
+          }
+          if (l > g_r0) {
+            c_sum += T.dsp[l] - T.dsp[g_r0];
+            c_max = max(c_max, rmaxq(g_r0, l - 1));
+            c_cnt += l - g_r0;
+            vo += l - g_r0;
+            cutc += l - g_r0;  // each route after a segment's first is a cut
+          }
+          const int xs = T.RS[l];
+          c_dur = T.LG[xs] + p.pey - T.PE[xs + 1];
+          c_load = p.pdy - T.PD[xs];
+          c_pl = p.lgy;
+          c_has = true;
+        };
         // (heterogeneous) routes r..rend-1 of the current tour, the first on
         // vehicle vo: every route keeps its split on vehicle r + delta (delta =
         // vo - r) up to the first that does not (NB), whose segment is walked
@@ -862,8 +898,9 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
           }
           return true;
         };
-        // the start of the first changed segment, up to lo
-        run(p_start, false, 0u);
+        // the start of the first changed segment, up to lo: the current split
+        if (ra1 - ra > 1) aligned(p_start, ra, ra1);
+        else run(p_start, false, 0u);
 #pragma unroll
         for (int s = 0; s < 3; ++s) {
           const bool hs = SA[s] != SB[s], rev = opt && s == 0;
@@ -922,8 +959,11 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
               }
             }
           }
-          // (D) the part after the last separator opens the next route
-          run(PDn[s], rev, 0u);
+          // (D) the part after the last separator opens the next route: read
+          // forward, the current split of that segment's start (on the same
+          // vehicles)
+          if (hs && !rev && RG1[s] - RG0[s] > 1 && (!HET || vo == RG0[s])) aligned(PDn[s], RG0[s], RG1[s]);
+          else run(PDn[s], rev, 0u);
         }
         // the rest of the last changed segment, closed by its separator (or
         // the tour's end)
