@@ -198,7 +198,7 @@ class _TimedCooling:
 
 def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label="cvrp100_k8 seed 0",
             gpu_seed=None, n_sep=None, window=0, window_types=0, start="random", moves=64,
-            cpu_moves=64, gpu=True, mig_every=5, mig_E=16):
+            cpu_moves=64, gpu=True, mig_every=1, mig_E=None, epochs=40):
     """Best-cost gap at fixed wall time (the metric's second half): the same SA
     (Philox streams, 64 sampled moves per step, geometric cooling from
     0.5 to 0.002 x the mean edge spread over the wall-time budget by
@@ -220,6 +220,7 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
     from vrpms_amd import islands, runners
     n = inst.n
     n_sep = inst.K - 1 if n_sep is None else n_sep
+    mig_E = chains // 2 if mig_E is None else mig_E
     dev = ctx.dev
     edge = runners.typical_edge(inst.durations)
     t0, t_end = 0.5 * edge, 0.002 * edge
@@ -238,7 +239,7 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
                              window=window, window_types=window_types, start=start, moves=moves)
         if world > 1:
             dist.barrier()
-        cool = _TimedCooling(seconds, t0, t_end)
+        cool = _TimedCooling(seconds, t0, t_end, epochs=epochs)
         e = 0
         while True:
             steps, inv_a = cool.plan(r.step)
@@ -275,22 +276,32 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
         cur = cur.copy()
         best = cur.copy()
         bk = np.full(threads, 2**64 - 1, dtype=np.uint64)
-        cool = _TimedCooling(seconds, t0, t_end)
-        step = 0
+        cool = _TimedCooling(seconds, t0, t_end, epochs=epochs)
+        # the GPU leg's migration scaled to the host's chains: every mig_every
+        # epochs the same fraction of chains restarts from the best-so-far
+        # tours (the E best by key replace the E worst current tours)
+        e_host = max(1, int(round(threads * mig_E / chains))) if mig_every else 0
+        step = e = 0
         while True:
             steps, inv_a = cool.plan(step)
             if steps == 0:
                 break
-            coracle.sa_run(inst.durations, cur, best, bk, steps, float(cool.inv_t), float(inv_a),
-                           1, step, inst.demand, inst.capacities, inst.start_times,
-                           threads=threads, window=window, window_types=window_types,
-                           resync=True, moves=cpu_moves)
+            ck = coracle.sa_run(inst.durations, cur, best, bk, steps, float(cool.inv_t),
+                                float(inv_a), 1, step, inst.demand, inst.capacities,
+                                inst.start_times, threads=threads, window=window,
+                                window_types=window_types, resync=True, moves=cpu_moves)
             cool.advance(steps, inv_a)
             step += steps
+            e += 1
+            if e_host and e % mig_every == 0 and threads > 1:
+                top = np.argsort(bk, kind="stable")[:e_host]
+                worst = np.argsort(-np.asarray(ck, dtype=np.float64), kind="stable")[:e_host]
+                cur[worst] = best[top]
         cpu_wall = cool.elapsed()
         ck = int(bk.min())
         out["cpu"] = {"chains": threads, "cores": threads, "host_cores": cores,
                       "moves_per_step": cpu_moves,
+                      "migration": {"every_epochs": mig_every, "elites": e_host},
                       "steps_per_chain": step,
                       "wall_s": cpu_wall, "unvisited": ck >> 56,
                       "duration_sum": (ck >> 28) & (2**28 - 1),

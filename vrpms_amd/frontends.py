@@ -110,11 +110,11 @@ def gpu_launch(device: int, steps: int, seed: int, streams: int = 3):
             keys_h.copy_(keys, non_blocking=True)
             done = torch.cuda.Event()
             done.record(stream)
-        keep = (pin, mats, tours, keys)   # alive until the stream is done with them
+        keep = [pin, mats, tours, keys]   # alive until the stream is done with them
 
         def finish():
             done.synchronize()
-            del keep
+            keep.clear()
             t = tours_h.numpy()
             k = keys_h.numpy().view(np.uint64)
             clamp = (1 << 28) - 1
