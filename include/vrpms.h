@@ -112,7 +112,9 @@ int vrpms_eval_path(vrpms_ctx* ctx, int32_t perm_bytes, int64_t ld, const void* 
 
 /* Context options (kernel-variant overrides for A/B tests and profiling).
  *   VRPMS_OPT_SPLIT_MODE: 0 = auto (branch-free prefix-ret split whenever its
- *   packed layout fits), 2 = force the branchy split in eval_cvrp_packed. */
+ *   packed layout fits), 2 = force the branchy split in eval_cvrp_packed,
+ *   3 = the words kernel's compare form of the fit test instead of the
+ *   add's carry (the two give identical keys; tests check both). */
 #define VRPMS_OPT_SPLIT_MODE 1
 /*   VRPMS_OPT_STAGED_M: candidates interleaved per lane in eval_staged
  *   (0 = auto: 2 for hour-indexed matrices, 1 for static; 1 or 2 force). */

@@ -184,6 +184,25 @@ static move_t decode_move(uint32_t r0, uint32_t r1, uint32_t r2, int n) {
   return m;
 }
 
+/* A13 (oracle/spec.py decode_move1): one word split by successive
+ * fixed-point multiplications (type, then i, then j') */
+static move_t decode_move1(uint32_t x, int n) {
+  move_t m;
+  uint64_t p = 3ull * x;
+  m.typ = (int)(p >> 32);
+  p = (uint64_t)(uint32_t)n * (uint32_t)p;
+  m.i = (int)(p >> 32);
+  p = (uint64_t)(uint32_t)(n - 1) * (uint32_t)p;
+  m.j = (int)(p >> 32);
+  if (m.j >= m.i) ++m.j;
+  if (m.typ != 2 && m.i > m.j) {
+    int t = m.i;
+    m.i = m.j;
+    m.j = t;
+  }
+  return m;
+}
+
 /* A11 (oracle/spec.py decode_move_window): j within `window` of i, for the
  * move types in `types` (A12; 0 = all) */
 static move_t decode_move_window(uint32_t r0, uint32_t r1, uint32_t r2, int n, int window,
@@ -377,7 +396,9 @@ int oracle_sa_run(int problem, const int32_t* D, int H, int N, const int32_t* de
 /* Throughput-mode restatement (oracle/search.py tsp_batch_sa, the C-ABI's
  * vrpms_tsp_batch_sa): R static TSP requests, int32 [R][N][N]; per request 4
  * chains from Philox Fisher-Yates starts (counters (~0, ~0, 4r + w, i)), SA
- * steps with counters (s, 0, 4r + w, lane), every candidate priced by a full
+ * steps drawing from one Philox block per two steps (counters (s >> 1, 0,
+ * 4r + w, lane); words 0, 1 on even steps, 2, 3 on odd: the move by
+ * decode_move1 (spec.py A13), the acceptance draw), every candidate priced by a full
  * re-evaluation (the device prices by O(1) deltas, so equality checks them);
  * the answer is the best (key, chain).  Out: tours [R][N-1], keys [R]. */
 int oracle_tsp_batch_sa(const int32_t* mats, int R, int N, int steps, float inv_t0,
@@ -412,13 +433,13 @@ int oracle_tsp_batch_sa(const int32_t* mats, int R, int N, int steps, float inv_
         move_t mbest = {0, 0, 0};
         uint32_t wbest = 0;
         for (int lane = 0; lane < 64; ++lane) {
-          u32x4 rr = philox((uint32_t)s, 0u, cid, (uint32_t)lane, k0, k1);
-          move_t m = decode_move(rr.x, rr.y, rr.z, n);
+          u32x4 rr = philox((uint32_t)(s >> 1), 0u, cid, (uint32_t)lane, k0, k1);
+          move_t m = decode_move1((s & 1) ? rr.z : rr.x, n);
           uint64_t kk = tour_key(&I, A, n, &m);
           if (kk < kbest) {
             kbest = kk;
             mbest = m;
-            wbest = rr.w;
+            wbest = (s & 1) ? rr.w : rr.y;
           }
         }
         int acc = kbest <= ck;

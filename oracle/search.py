@@ -122,9 +122,12 @@ def sa_run(score: Scorer, cur_tours, best_tours, best_keys, seed: int, step0: in
 
 def tsp_batch_sa(mats, steps: int, inv_t0: float, inv_alpha: float, seed: int):
     """vrpms_tsp_batch_sa: per request 4 chains (Philox Fisher-Yates starts,
-    counters (0xffffffff, 0xffffffff, 4r + w, i)), SA steps with counters
-    (s, 0, 4r + w, lane); best (key, wave).  Costs by full re-evaluation --
-    the device prices moves by O(1) deltas, so equality checks the deltas."""
+    counters (0xffffffff, 0xffffffff, 4r + w, i)); one Philox block with
+    counters (s >> 1, 0, 4r + w, lane) serves two SA steps (A13): step s uses
+    words (0, 1) when s is even, (2, 3) when odd -- the move from the first
+    (spec.decode_move1), the acceptance draw from the second; best (key,
+    wave).  Costs by full re-evaluation -- the device prices moves by O(1)
+    deltas, so equality checks the deltas."""
     key = spec.seed_key(seed)
     out_t, out_k = [], []
     for r, D in enumerate(mats):
@@ -146,9 +149,10 @@ def tsp_batch_sa(mats, steps: int, inv_t0: float, inv_alpha: float, seed: int):
                 for s in range(steps):
                     cands = []
                     for lane in range(64):
-                        rr = spec.philox4x32_10((s, 0, cid, lane), key)
-                        m = spec.decode_move(rr[0], rr[1], rr[2], n)
-                        cands.append((score(spec.apply_move(t, *m)), lane, m, rr[3]))
+                        rr = spec.philox4x32_10((s >> 1, 0, cid, lane), key)
+                        h = 2 * (s & 1)
+                        m = spec.decode_move1(rr[h], n)
+                        cands.append((score(spec.apply_move(t, *m)), lane, m, rr[h + 1]))
                     kk, lane, m, r3 = min(cands, key=lambda c: (c[0], c[1]))
                     acc = kk <= ck
                     if not acc:

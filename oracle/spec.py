@@ -330,6 +330,25 @@ def decode_move(r0: int, r1: int, r2: int, n: int):
     return typ, i, j
 
 
+def decode_move1(x: int, n: int):
+    """A13: one Philox word -> (type, i, j), the throughput kernel's move
+    (vrpms_tsp_batch_sa, two SA steps per Philox block).  The word is split
+    by successive fixed-point multiplications: type = hi(3x), i = hi(n * f1)
+    with f1 = lo(3x), j' = hi((n - 1) * f2) with f2 = lo(n * f1); j = j' + 1
+    when j' >= i; swap / 2-opt canonicalised i < j."""
+    x = int(x) & MASK32
+    p = 3 * x
+    typ, f1 = p >> 32, p & MASK32
+    p = n * f1
+    i, f2 = p >> 32, p & MASK32
+    j = ((n - 1) * f2) >> 32
+    if j >= i:
+        j += 1
+    if typ != MOVE_RELOCATE and i > j:
+        i, j = j, i
+    return typ, i, j
+
+
 def decode_move_window(r0: int, r1: int, r2: int, n: int, window: int, types: int = 0):
     """A11: a move whose second position lies within `window` of the first
     (the neighbourhood SA samples on large tours).  window <= 0 or

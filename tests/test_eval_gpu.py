@@ -59,7 +59,9 @@ def check_batch(ctx, coracle, inst, P, n=None, objective=0, expect_path=None):
     return got_k
 
 
-@pytest.fixture(params=[0, 2], ids=["prefix_ret", "branchy"])
+# 0: auto (the words kernel tests fits by the add's carry when every demand
+# is >= 1), 2: the branchy split, 3: the words kernel's sign-compare form
+@pytest.fixture(params=[0, 2, 3], ids=["prefix_ret", "branchy", "prefix_ret_compare"])
 def split_mode(request, ctx):
     ctx.set_split_mode(request.param)
     yield request.param
@@ -176,6 +178,27 @@ def test_words_layout_ragged_and_tight(ctx, coracle, n, K, slack, split_mode):
     inst = synth.cvrp(n, K, seed=n, slack=slack)
     P = synth.random_perms(20000, inst.n, seed=1)
     check_words(ctx, coracle, inst, P, inst.n, objective=n % 2)
+
+
+def test_words_layout_zero_demands_asymmetric(ctx, coracle, split_mode):
+    """Zero-demand customers on an asymmetric matrix: an edge term
+    dur(a,b) + ret(b) - ret(a) below 0 with no demand above it would carry
+    on a fit, so the carry form is not used (FastSplit::carry); keys still
+    equal the oracle's, with and without zero demands."""
+    rng = np.random.default_rng(12)
+    N = 90
+    D = rng.integers(0, 3000, size=(N, N))
+    np.fill_diagonal(D, 0)
+    D[:, 0] = rng.integers(2000, 3000, size=N)
+    D[0, 0] = 0
+    dem = np.concatenate([[0], rng.integers(1, 30, N - 1)])
+    for zeros in (False, True):
+        d = dem.copy()
+        if zeros:
+            d[1::5] = 0
+        inst = synth.Instance("asym0", D[None], d, np.full(7, 180), np.zeros(7, dtype=np.int64),
+                              "cvrp")
+        check_words(ctx, coracle, inst, synth.random_perms(12000, inst.n, seed=5), inst.n)
 
 
 def test_words_layout_oversize_and_fallbacks(ctx, coracle):

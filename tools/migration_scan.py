@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """GPU SA leg on X-1000 (cfg 4) at T seconds for several elite-migration
-settings (every k epochs, E elites into the worst chains); GPU only.
-usage: migration_scan.py T seed every:E [every:E ...]"""
+settings (every k epochs, E elites into the worst chains) and chain /
+move / epoch counts; GPU only.
+usage: migration_scan.py T seed every:E[:chains[:moves[:epochs]]] ..."""
 import json
 import os
 import sys
@@ -13,12 +14,16 @@ from vrpms_amd.core import CVRP, Context  # noqa: E402
 
 T, seed = float(sys.argv[1]), int(sys.argv[2])
 ctx = Context(0)
-x = synth.x_style(1000, seed=seed)
+# INSTANCE=td: cfg 3's TD-200 x 24 (sa_route_kernel) instead of X-1000
+td = os.environ.get("INSTANCE") == "td"
+x = synth.td_cvrp(200, 16, seed=seed) if td else synth.x_style(1000, seed=seed)
 ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
 for spec in sys.argv[3:]:
-    every, E = (int(v) for v in spec.split(":"))
-    q = bench.quality(ctx, x, T, 1, 0, None, with_cpu=False, chains=256, moves=128, window=32,
-                      window_types=2, start="pack", mig_every=every, mig_E=E)
-    print(json.dumps({"every": every, "E": E, "gpu": q["gpu"]["duration_sum"],
+    v = [int(t) for t in spec.split(":")] + [256, 128, 40][len(spec.split(":")) - 2:]
+    every, E, chains, moves, epochs = v[:5]
+    q = bench.quality(ctx, x, T, 1, 0, None, with_cpu=False, chains=chains, moves=moves, window=32,
+                      window_types=2, start="pack", mig_every=every, mig_E=E, epochs=epochs)
+    print(json.dumps({"every": every, "E": E, "chains": chains, "moves": moves, "epochs_planned": epochs,
+                      "gpu": q["gpu"]["duration_sum"],
                       "steps": q["gpu"]["steps_per_chain"], "epochs": q["gpu"]["epochs"]}),
           flush=True)

@@ -211,8 +211,9 @@ int vrpms_ctx_destroy(vrpms_ctx* ctx) {
 int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value) {
   if (!ctx) return fail(VRPMS_EINVAL, "vrpms_set_option: ctx is NULL");
   if (option == VRPMS_OPT_SPLIT_MODE) {
-    if (value != 0 && value != 2)
-      return fail(VRPMS_EINVAL, "vrpms_set_option: split mode must be 0 (auto) or 2 (branchy)");
+    if (value != 0 && value != 2 && value != 3)
+      return fail(VRPMS_EINVAL,
+                  "vrpms_set_option: split mode must be 0 (auto), 2 (branchy) or 3 (no carry form)");
     ctx->opt_split_mode = value;
     return VRPMS_OK;
   }
@@ -352,6 +353,7 @@ int vrpms_set_instance(vrpms_ctx* ctx, int32_t problem, const int32_t* d_dur, in
   if (st[6] < 0) return fail(VRPMS_EINVAL, "vrpms_set_instance: negative start time");
   in.max_dur = st[1];
   in.max_dem = problem == VRPMS_CVRP && N > 1 ? st[3] : 0;
+  in.min_dem = problem == VRPMS_CVRP && N > 1 ? st[2] : 0;
   in.min_cap = problem == VRPMS_CVRP ? st[4] : INT_MAX;
   in.max_cap = problem == VRPMS_CVRP ? st[5] : INT_MAX;
   in.max_start = st[7];

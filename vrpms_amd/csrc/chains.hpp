@@ -61,6 +61,25 @@ VRPMS_DEV void split_step_fast(SplitAcc& s, uint64_t e, uint32_t vsmask, uint32_
   s.acc = fits ? t : hi;
 }
 
+// split_step_fast with the fit test read from the add's carry (no compare):
+// acc = (load - cap - 1) << S + low lies in [2^31, 2^32) and lo = dem << S +
+// (low' - low) mod 2^32, so when dem >= 1 the second term is a positive
+// number below 2^31 and acc + lo overflows 32 bits exactly when load + dem >
+// cap -- the same test as the sign of t (fast_split_params bounds
+// (cap + max_dem + 3) << S by 2^31).  A zero demand can make lo wrap (an edge
+// term below 0) and carry on a fit: FastSplit::carry is set only when every
+// customer demand is >= 1.  A separator (column 0, lo = 2^31 - 1) always
+// carries.
+VRPMS_DEV void split_step_carry(SplitAcc& s, uint64_t e, uint32_t vsmask, uint32_t kinc) {
+  const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
+  uint32_t t;
+  const bool over = __builtin_add_overflow(s.acc, lo, &t);
+  const uint32_t rdm = over ? ((s.acc & vsmask) | kinc) : 0u;
+  s.dsum += rdm;
+  s.dmax = max(s.dmax, rdm);
+  s.acc = over ? hi : t;
+}
+
 // Copy the packed matrix E into LDS (16-byte vectors + an 8-byte tail).
 VRPMS_DEV void stage_table(const uint64_t* pack, int N, unsigned char* smem) {
   const uint32_t ebytes = (uint32_t)N * N * 8;
@@ -73,8 +92,8 @@ VRPMS_DEV void stage_table(const uint64_t* pack, int N, unsigned char* smem) {
 }
 
 // ILP independent split chains of one lane, fed four customers (one word)
-// at a time.
-template <int ILP>
+// at a time (CY: the carry form of the step, FastSplit::carry).
+template <int ILP, bool CY = false>
 struct WordChains {
   SplitAcc sa[ILP];
   uint32_t wprev[ILP];  // previous word (its byte 3 is the depot before the first word)
@@ -116,7 +135,10 @@ struct WordChains {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int i = 0; i < ILP; ++i) split_step_fast(sa[i], g[i][q], vsmask, kinc);
+      for (int i = 0; i < ILP; ++i) {
+        if constexpr (CY) split_step_carry(sa[i], g[i][q], vsmask, kinc);
+        else split_step_fast(sa[i], g[i][q], vsmask, kinc);
+      }
   }
   // The exact split of one tour (fleet limit, A10 separators), word by word
   // (word(w) returns tour word w): the slow path for a chain whose fast walk

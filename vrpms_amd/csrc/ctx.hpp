@@ -18,7 +18,7 @@ enum MatTier : int {
 struct Instance {
   int problem = VRPMS_TSP;
   int H = 1, N = 0, K = 1, objective = VRPMS_OBJ_SUM;
-  int max_dur = 0, max_dem = 0, max_start = 0, min_start = 0, min_cap = 0, max_cap = 0;
+  int max_dur = 0, max_dem = 0, min_dem = 0, max_start = 0, min_start = 0, min_cap = 0, max_cap = 0;
   bool uniform_cap = true;
   bool symmetric = false;      // hour slice 0 is symmetric (O(1) 2-opt delta for static TSP)
   int cap0 = 0;
@@ -48,7 +48,7 @@ struct vrpms_ctx {
   vrpms::Instance inst;
   int num_cus = 256;
   size_t max_lds = 160 * 1024;
-  int opt_split_mode = 0;       // VRPMS_OPT_SPLIT_MODE (0 auto, 2 force branchy)
+  int opt_split_mode = 0;       // VRPMS_OPT_SPLIT_MODE (0 auto, 2 force branchy, 3 no carry form)
   int opt_staged_m = 0;         // VRPMS_OPT_STAGED_M (0 auto, 1, 2 or 3)
   int opt_route_wg_per_cu = 0;  // sa_route_kernel workgroups per CU (0 auto, 1, 2)
   int opt_words_ilp = 0;        // candidates per lane in eval_cvrp_words2 (0 auto = 2; 1 A/B builds)

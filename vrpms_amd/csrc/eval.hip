@@ -618,6 +618,7 @@ bool fast_split_params(const vrpms_ctx* ctx, int n, FastSplit* out) {
   out->ks = (uint32_t)ks;
   out->klim = (uint32_t)((((int64_t)1 << B) - in.K) << ks);
   out->dead = (uint32_t)1u << in.pref_S;
+  out->carry = in.min_dem >= 1;
   return true;
 }
 

@@ -40,11 +40,11 @@
 
 namespace vrpms {
 
-template <int R, int ILP, int LA>
+template <int R, int ILP, int LA, bool CY>
 __global__ __launch_bounds__(1024) void eval_cvrp_words2(WordsArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   stage_table(a.f.pack, a.f.N, smem);
-  WordChains<ILP> ch;
+  WordChains<ILP, CY> ch;
   ch.setup(a.f, smem);
   const int64_t C = a.C;
   const int n = a.n, nw = (n + 3) >> 2, nfull = n >> 2;
@@ -67,14 +67,22 @@ __global__ __launch_bounds__(1024) void eval_cvrp_words2(WordsArgs a) {
     if (!live[0]) continue;
     const uint32_t* row = a.words + c0 * a.cstride;
     const int64_t wstride = a.wstride;
+    // the lane's byte offset from the uniform row pointer: a buffer load
+    // with the row in an SGPR descriptor (advanced by SALU) and a constant
+    // 32-bit VGPR offset, so a load costs no address VALU
     uint32_t loff[ILP];
 #pragma unroll
-    for (int i = 0; i < ILP; ++i) loff[i] = lane[i] * a.cstride;
+    for (int i = 0; i < ILP; ++i) loff[i] = lane[i] * a.cstride * 4u;
+    auto ld = [&](const uint32_t* r, int i) {
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint32_t*>(r), (short)0, 0x7fffffff, 0x00020000);
+      return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, loff[i], 0, 0);
+    };
     uint32_t ring[ILP][R];
 #pragma unroll
     for (int u = 0; u < R; ++u) {
 #pragma unroll
-      for (int i = 0; i < ILP; ++i) ring[i][u] = u < nw ? row[loff[i]] : 0u;
+      for (int i = 0; i < ILP; ++i) ring[i][u] = u < nw ? ld(row, i) : 0u;
       row += wstride;
     }
     ch.reset(a.f);
@@ -97,7 +105,7 @@ __global__ __launch_bounds__(1024) void eval_cvrp_words2(WordsArgs a) {
 #pragma unroll
       for (int i = 0; i < ILP; ++i) {
         wd[i] = ring[i][u];
-        if (refill) ring[i][u] = row[loff[i]];  // word w + R
+        if (refill) ring[i][u] = ld(row, i);  // word w + R
       }
       if (refill) row += wstride;
       uint64_t f[ILP][4];
@@ -139,7 +147,7 @@ __global__ __launch_bounds__(1024) void eval_cvrp_words2(WordsArgs a) {
       const uint32_t* rw = a.words + c0 * a.cstride + (int64_t)w * wstride;
       uint32_t x[ILP];
 #pragma unroll
-      for (int i = 0; i < ILP; ++i) x[i] = rw[loff[i]];
+      for (int i = 0; i < ILP; ++i) x[i] = ld(rw, i);
       if (rem == 4) {
         ch.issue(e, x, ch.wprev);
         ch.steps(e);
@@ -322,15 +330,22 @@ int launch_words2(const vrpms_ctx* ctx, const WordsArgs& w, int R, hipStream_t s
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     kern<<<grid, 1024, lds, s>>>(w);
   };
-  auto pick = [&](auto ilp_c, auto la_c) {
+  // every customer demand >= 1: the fit test rides in the add's carry
+  const bool cy = w.f.carry && ctx->opt_split_mode != 3;
+  auto pick2 = [&](auto ilp_c, auto la_c, auto cy_c) {
     constexpr int I = decltype(ilp_c)::value, L = decltype(la_c)::value;
+    constexpr bool C = decltype(cy_c)::value;
     switch (R) {
-      case 4: go(eval_cvrp_words2<4, I, L>); break;
-      case 5: go(eval_cvrp_words2<5, I, L>); break;
-      case 6: go(eval_cvrp_words2<6, I, L>); break;
-      case 7: go(eval_cvrp_words2<7, I, L>); break;
-      default: go(eval_cvrp_words2<8, I, L>); break;
+      case 4: go(eval_cvrp_words2<4, I, L, C>); break;
+      case 5: go(eval_cvrp_words2<5, I, L, C>); break;
+      case 6: go(eval_cvrp_words2<6, I, L, C>); break;
+      case 7: go(eval_cvrp_words2<7, I, L, C>); break;
+      default: go(eval_cvrp_words2<8, I, L, C>); break;
     }
+  };
+  auto pick = [&](auto ilp_c, auto la_c) {
+    if (cy) pick2(ilp_c, la_c, std::true_type{});
+    else pick2(ilp_c, la_c, std::false_type{});
   };
   using one = std::integral_constant<int, 1>;
   using two = std::integral_constant<int, 2>;

@@ -768,40 +768,11 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
           c_dur = c_load = c_pl = 0u;
           c_has = false;
         };
-        // A fresh vehicle at the start of route g_r0 of the current tour
-        // (routes g_r0 .. g_r1 - 1 hold the rest of its segment) taking the
-        // customers up to y in the current order, on the current vehicles:
-        // the current tour's split from there.  Its routes before the one
-        // holding y are closed from the tables, that route's part up to y is
-        // the open route -- no capacity cut is searched.
-        auto aligned = [&](const RunP& p, int g_r0, int g_r1) __attribute__((always_inline)) {
-          if (p.x > p.y || dead) return;
-          seps = 0;
-          cust = true;
-          int l = g_r0, h = g_r1 - 1;  // the last route starting at or before y
-          while (l < h) {
-            const int md = (l + h + 1) >> 1;
-            if ((int)T.RS[md] <= p.y) l = md; else h = md - 1;
-          }
-          if (l > g_r0) {
-            c_sum += T.dsp[l] - T.dsp[g_r0];
-            c_max = max(c_max, rmaxq(g_r0, l - 1));
-            c_cnt += l - g_r0;
-            vo += l - g_r0;
-            cutc += l - g_r0;  // each route after a segment's first is a cut
-          }
-          const int xs = T.RS[l];
-          c_dur = T.LG[xs] + p.pey - T.PE[xs + 1];
-          c_load = p.pdy - T.PD[xs];
-          c_pl = p.lgy;
-          c_has = true;
-        };
         // customers A[x..y] joined to the open route in the moved order (rev:
         // A[y] first), cut where the greedy split's next customer does not
         // fit; jv = the junction edge into the first one when the open route
         // holds a customer
-        auto run = [&](const RunP& p, bool rev, uint32_t jv, int g = -1)
-                       __attribute__((always_inline)) {
+        auto run = [&](const RunP& p, bool rev, uint32_t jv) __attribute__((always_inline)) {
           int x = p.x, y = p.y;
           if (x > y || dead) return;
           seps = 0;
@@ -869,25 +840,36 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
             } else {
               x = pb + 1;
               if (pa <= pb) pdx = pdb;  // PD[x] = PD[pb + 1]
-              // (g >= 0: forward on current positions of segment g) back in
-              // step: the fresh route starts where a route of the current tour
-              // does, on that route's vehicle -- the rest is the current split
-              if (g >= 0 && x <= y) {
-                const int r0 = T.RB[g], r1 = T.RB[g + 1];
-                int l = r0, h = r1 - 1;  // the last route starting at or before x
-                while (l < h) {
-                  const int md = (l + h + 1) >> 1;
-                  if ((int)T.RS[md] <= x) l = md; else h = md - 1;
-                }
-                if ((int)T.RS[l] == x && (!HET || vo == l)) {
-                  RunP q = p;
-                  q.x = x;
-                  aligned(q, l, r1);
-                  return;
-                }
-              }
             }
           }
+        };
+        // A fresh vehicle at the start of segment g (routes g_r0 .. g_r1 - 1)
+        // taking its customers up to y in the current order, on the current
+        // vehicles: the current tour's split.  Its routes before the one
+        // holding y are closed from the tables, that route's part up to y is
+        // the open route -- no capacity cut is searched.  (Segments of one
+        // route go through run(): their prefix never cuts.)
+        auto aligned = [&](const RunP& p, int g_r0, int g_r1) __attribute__((always_inline)) {
+          if (p.x > p.y || dead) return;
+          seps = 0;
+          cust = true;
+          int l = g_r0, h = g_r1 - 1;  // the last route starting at or before y
+          while (l < h) {
+            const int md = (l + h + 1) >> 1;
+            if ((int)T.RS[md] <= p.y) l = md; else h = md - 1;
+          }
+          if (l > g_r0) {
+            c_sum += T.dsp[l] - T.dsp[g_r0];
+            c_max = max(c_max, rmaxq(g_r0, l - 1));
+            c_cnt += l - g_r0;
+            vo += l - g_r0;
+            cutc += l - g_r0;  // each route after a segment's first is a cut
+          }
+          const int xs = T.RS[l];
+          c_dur = T.LG[xs] + p.pey - T.PE[xs + 1];
+          c_load = p.pdy - T.PD[xs];
+          c_pl = p.lgy;
+          c_has = true;
         };
         // (heterogeneous) routes r..rend-1 of the current tour, the first on
         // vehicle vo: every route keeps its split on vehicle r + delta (delta =
@@ -923,7 +905,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
         for (int s = 0; s < 3; ++s) {
           const bool hs = SA[s] != SB[s], rev = opt && s == 0;
           // (A) up to the first separator in the moved order
-          run(PA[s], rev, JV[s], rev ? -1 : SA[s]);
+          run(PA[s], rev, JV[s]);
           if (hs) {
             // (B) the separator closes the open route
             close();
@@ -985,7 +967,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
         }
         // the rest of the last changed segment, closed by its separator (or
         // the tour's end)
-        run(p_tail, false, jx3, sH);
+        run(p_tail, false, jx3);
         close();
         if (en < n) ++seps;
         // the unchanged tail: routes rz.. of the current tour.  A

@@ -238,6 +238,13 @@ VRPMS_DEV uint32_t wave_scan_incl(uint32_t v) {
   return v;
 }
 
+#ifdef VRPMS_ROUTE_DUMP
+// (debug builds only: tools/route_dump.py) each chain's route tables at the
+// end of a call: R, route_ok, then dur / rs / dsp [RM] and rid [n]
+constexpr int kRouteDumpInts = 4096;
+__device__ int g_route_dump[kRouteDumpInts * 64];
+#endif
+
 #ifdef VRPMS_ROUTE_PROF
 // per-chain counters (A/B builds only: tools/route_prof.py): pricing and
 // accept ticks (wall_clock64, 100 MHz), steps, accepts, walked tokens (wave
@@ -1229,6 +1236,21 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
     invT = invT * a.inv_alpha;
   }
   if (cw != 0) return;
+#ifdef VRPMS_ROUTE_DUMP
+  if (chain < 64 && 2 + 3 * RM + n <= kRouteDumpInts) {
+    int* d = g_route_dump + chain * kRouteDumpInts;
+    if (lane == 0) {
+      d[0] = R;
+      d[1] = route_ok ? 1 : 0;
+    }
+    for (int r = lane; r < RM; r += 64) {
+      d[2 + r] = (int)T.dur[r];
+      d[2 + RM + r] = (int)T.rs[r];
+      d[2 + 2 * RM + r] = (int)T.dsp[r];
+    }
+    for (int q = lane; q < n; q += 64) d[2 + 3 * RM + q] = (int)T.rid[q];
+  }
+#endif
   uint16_t* gout = a.cur + (int64_t)chain * n;
   for (int q = lane; q < n; q += 64) gout[q] = (uint16_t)tokA(q);
   if (lane == 0) {
@@ -2096,9 +2118,13 @@ VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, unsigned cha
   uint64_t ck = pack_key(0, (uint32_t)dur, 0), bk = ck;
   for (int q = lane; q < n; q += 64) Best[q] = A[q];
   float invT = a.inv_t0;
+  // A13: one Philox block per lane serves two steps -- words (x, y) on an
+  // even step, (z, w) on the odd one: the move, then the acceptance draw
+  u32x4 rb = {0u, 0u, 0u, 0u};
   for (int s = 0; s < a.steps && n >= 2; ++s) {
-    const u32x4 rr = philox((uint32_t)s, 0u, cid, (uint32_t)lane, a.seed_lo, a.seed_hi);
-    const Move m = decode_move(rr.x, rr.y, rr.z, n);
+    if ((s & 1) == 0) rb = philox((uint32_t)(s >> 1), 0u, cid, (uint32_t)lane, a.seed_lo, a.seed_hi);
+    const uint32_t xm = (s & 1) ? rb.z : rb.x, xa = (s & 1) ? rb.w : rb.y;
+    const Move m = decode_move1(xm, n);
     auto tourA = [&](int q) { return (uint32_t)A[q]; };
     int delta;
     if constexpr (symmetric) delta = tsp_move_delta_sym(dist, tourA, n, m);
@@ -2117,7 +2143,7 @@ VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, unsigned cha
     if (!accept) {
       const uint64_t d = (k >> 28) - (ck >> 28);
       const uint32_t dp = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
-      accept = ((uint32_t)wave_bcast((int)rr.w, bl) >> 8) < accept_threshold(dp, invT);
+      accept = ((uint32_t)wave_bcast((int)xa, bl) >> 8) < accept_threshold(dp, invT);
     }
     if (accept) {  // bl is wave-uniform: the winner's move by v_readlane
       Move mb;
@@ -2603,6 +2629,13 @@ extern "C" int vrpms_tsp_batch_sa(vrpms_ctx* ctx, const int32_t* d_mats, int32_t
   VRPMS_HIP(hipGetLastError());
   return VRPMS_OK;
 }
+
+#ifdef VRPMS_ROUTE_DUMP
+extern "C" int vrpms_debug_route_dump(int* out, int count) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(vrpms::g_route_dump), sizeof(int) * count) ==
+                 hipSuccess ? 0 : -2;
+}
+#endif
 
 #ifdef VRPMS_ROUTE_PROF
 extern "C" int vrpms_debug_route_prof(unsigned long long* out, int count, int reset) {

@@ -32,6 +32,7 @@ struct FastSplit {
   int N, K, objective;
   uint32_t lim, smask;
   uint32_t ks, klim, dead;  // 1 << ks counts vehicles; klim = initial dsum; dead = biased DEAD
+  bool carry;               // every customer demand >= 1: the fit test is acc + lo's carry
 };
 
 // Host: constants of the branch-free split for tours of n customers, or

@@ -147,6 +147,26 @@ VRPMS_DEV Move decode_move(uint32_t r0, uint32_t r1, uint32_t r2, int n) {
   return m;
 }
 
+// A13 (oracle/spec.py decode_move1): one word split by successive fixed-point
+// multiplications -- type = hi(3x), i = hi(n lo(3x)), j' = hi((n-1) lo(n lo(3x)))
+// -- six multiplies instead of three divisions by run-time moduli
+VRPMS_DEV Move decode_move1(uint32_t x, int n) {
+  Move m;
+  const uint32_t f1 = x * 3u;
+  m.typ = __umulhi(x, 3u);
+  m.i = (int)__umulhi(f1, (uint32_t)n);
+  const uint32_t f2 = f1 * (uint32_t)n;
+  int j = (int)__umulhi(f2, (uint32_t)(n - 1));
+  if (j >= m.i) ++j;
+  m.j = j;
+  if (m.typ != kMoveRelocate && m.i > m.j) {
+    const int t = m.i;
+    m.i = m.j;
+    m.j = t;
+  }
+  return m;
+}
+
 // A11 (oracle/spec.py decode_move_window): the second position within
 // `window` of the first; window <= 0 or 2 window + 1 >= n: decode_move.
 // A12: only for the move types whose bit is set in `types` (7 = all).

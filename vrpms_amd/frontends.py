@@ -336,7 +336,10 @@ def _worker_main(w, arena, lo, hi, req_q, resp_q, submit_qs, done_q, store, batc
             free.append(s)
         rows = j["rows"] + list(store.solutions[before:])
         del store.solutions[before:]
-        resp_q.put((j["id"], out, rows))
+        # the response bytes as the HTTP handler writes them (service.py
+        # do_POST): encoding is part of serving, so it runs here, in parallel
+        enc = [(st, json.dumps(body).encode("utf-8")) for st, body in out]
+        resp_q.put((j["id"], enc, rows))
         st["answer_s"] += time.perf_counter() - t0
 
     while not (stop and not jobs):
@@ -420,9 +423,11 @@ class FrontEndPool:
         self._next_job = 0
         self._lock = threading.Lock()
 
-    def post_many(self, problem: str, algorithm: str, bodies):
+    def post_many(self, problem: str, algorithm: str, bodies, raw: bool = False):
         """(status, body) per request, in order; chunks go to the workers
-        round-robin and are answered as they complete."""
+        round-robin and are answered as they complete.  The workers send each
+        response as the HTTP handler's JSON bytes; raw=True returns those
+        bytes, else the decoded dicts (App.post's contract)."""
         with self._lock:
             bodies = list(bodies)
             jobs = {}
@@ -436,7 +441,7 @@ class FrontEndPool:
             for _ in range(len(jobs)):
                 jid, res, rows = self._resp_q.get()
                 s = jobs[jid]
-                out[s:s + len(res)] = res
+                out[s:s + len(res)] = res if raw else [(st, json.loads(b)) for st, b in res]
                 if rows:
                     self.store.solutions.extend(rows)
             return out
@@ -486,7 +491,7 @@ def bench_api(R: int = 10000, N: int = 50, workers: int = 16, steps: int = 1000,
                       window_s=window_ms * 1e-3) as pool:
         pool.post_many("tsp", "sa", bodies[:2 * workers * pool.chunk])   # warm: GPU context
         t0 = time.perf_counter()
-        res = pool.post_many("tsp", "sa", bodies)
+        res = pool.post_many("tsp", "sa", bodies, raw=True)   # the response bytes, as served
         dt = time.perf_counter() - t0
     ok = sum(1 for st, _ in res if st == 200)
     owners = [x for kind, x in pool.stats if kind == "owner"]
@@ -498,7 +503,7 @@ def bench_api(R: int = 10000, N: int = 50, workers: int = 16, steps: int = 1000,
     bad = 0
     idx = np.random.default_rng(1).choice(R, size=min(check, R), replace=False)
     for i in idx:
-        st, body = res[i]
+        st, body = res[i][0], json.loads(res[i][1])
         D = np.asarray(store.durations[int(i)])
         v = body["message"]["vehicle"] if st == 200 else None
         if v is None or sorted(v[1:-1]) != list(range(1, N)) or v[0] != 0 or v[-1] != 0 or \
