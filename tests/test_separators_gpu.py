@@ -191,6 +191,11 @@ ROUTE_CASES = [
     ("td200_random", lambda: synth.td_cvrp(200, 16, seed=2), "random", 8, 30, 1 / 200.0, 16, 0),
     ("td200_random_2opt", lambda: synth.td_cvrp(200, 16, seed=4), "random", 8, 30, 1 / 200.0, 16,
      2),
+    # first-fit start (trailing separators): an accepted move whose second
+    # zone walks to the tour end closes an empty last route there -- its
+    # start is the zone's end (the table update once left it stale)
+    ("td200_pack_uniform", lambda: synth.td_cvrp(200, 16, seed=21), "pack", 8, 60, 1 / 200.0, 16,
+     2),
     # hot chains: the unserved-move shortcut is off (invT < 2^-20)
     ("cvrp150_hot", lambda: synth.cvrp(150, 12, seed=3), "greedy", 8, 30, 1e-7, 8, 0),
     ("cvrp150_pack_hot", lambda: synth.cvrp(150, 12, seed=5, slack=1.02), "pack", 8, 40, 1e-7, 6,

@@ -1191,6 +1191,11 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
               if (off < len && ((bm[2 * z + h] >> lane) & 1ull))
                 T.rs[r0 + starts_upto(z, off) - 1] = (uint16_t)(base + off);
             }
+            // routes of the zone past its set bits start at its end: the
+            // empty route a walk that reaches the tour end closes after a
+            // trailing separator (its start bit is the zone's length)
+            const int cz = z ? bc2 : bc1, nb = len > 0 ? starts_upto(z, len - 1) : 0;
+            if (lane < cz - nb) T.rs[r0 + nb + lane] = (uint16_t)(base + len);
           }
         }
         if (lane == 0) T.rs[R2] = (uint16_t)n;
