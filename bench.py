@@ -198,7 +198,8 @@ class _TimedCooling:
 
 def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label="cvrp100_k8 seed 0",
             gpu_seed=None, n_sep=None, window=0, window_types=0, start="random", moves=64,
-            cpu_moves=64, gpu=True, mig_every=1, mig_E=None, epochs=40):
+            cpu_moves=64, gpu=True, mig_every=1, mig_E=None, epochs=40, t0_frac=0.5,
+            tend_frac=0.002):
     """Best-cost gap at fixed wall time (the metric's second half): the same SA
     (Philox streams, 64 sampled moves per step, geometric cooling from
     0.5 to 0.002 x the mean edge spread over the wall-time budget by
@@ -223,7 +224,7 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
     mig_E = chains // 2 if mig_E is None else mig_E
     dev = ctx.dev
     edge = runners.typical_edge(inst.durations)
-    t0, t_end = 0.5 * edge, 0.002 * edge
+    t0, t_end = t0_frac * edge, tend_frac * edge
     out = {"T_s": seconds, "algorithm": "sa", "instance": label, "cooling": "wall-time geometric",
            "separators": n_sep, "window": window, "window_types": window_types, "start": start}
     if gpu:
@@ -258,11 +259,15 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
         gpu_wall = cool.elapsed()
         key, tour = r.best()
         if world > 1:
-            key, _ = islands.global_best(r)
+            key, tour = islands.global_best(r)
+        # the search's own key for its best tour against a fresh exact score
+        # of that tour (the library's scoring kernel, parity-tested)
+        rescored = _rescore(ctx, tour)
         out["gpu"] = {"chains_per_gpu": chains, "moves_per_step": moves, "steps_per_chain": r.step,
                       "migration": {"every_epochs": mig_every, "elites": mig_E},
                       "epochs": e, "wall_s": gpu_wall, "unvisited": key >> 56,
-                      "duration_sum": (key >> 28) & (2**28 - 1)}
+                      "duration_sum": (key >> 28) & (2**28 - 1),
+                      "rescored_equal": rescored == key}
     if with_cpu:
         from oracle import coracle
         threads, cores = host_cores()
@@ -299,12 +304,14 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
                 cur[worst] = best[top]
         cpu_wall = cool.elapsed()
         ck = int(bk.min())
+        cpu_rescored = _rescore(ctx, best[int(np.argmin(bk))].tolist())
         out["cpu"] = {"chains": threads, "cores": threads, "host_cores": cores,
                       "moves_per_step": cpu_moves,
                       "migration": {"every_epochs": mig_every, "elites": e_host},
                       "steps_per_chain": step,
                       "wall_s": cpu_wall, "unvisited": ck >> 56,
                       "duration_sum": (ck >> 28) & (2**28 - 1),
+                      "rescored_equal": cpu_rescored == ck,
                       "kind": "port (oracle/oracle_c.c oracle_sa_run_resync: "
                               "candidates priced by walking only what the move changes)"}
         if gpu:
@@ -387,6 +394,14 @@ def _gap(g, c):
     return None
 
 
+def _rescore(ctx, tour):
+    """Exact key of one tour (a list of tokens) by the library's scoring
+    kernel, as an unsigned int."""
+    import torch
+    t = torch.tensor([list(tour)], dtype=torch.int16, device=ctx.dev)
+    return int(ctx.eval(t)[0]) & (2**64 - 1)
+
+
 def equal_time_cells(ctx, seconds, dist, with_cpu, instance="x1000", seeds=(0, 1, 2),
                      cpu_moves=(32, 64), repeat_host=True):
     """The metric's second half, several seeds: per seed the GPU
@@ -404,7 +419,13 @@ def equal_time_cells(ctx, seconds, dist, with_cpu, instance="x1000", seeds=(0, 1
     from vrpms_amd.core import CVRP
     make = {"x1000": lambda sd: synth.x_style(1000, seed=sd),
             "tdvrp200": lambda sd: synth.td_cvrp(200, 16, seed=sd)}[instance]
-    kw = dict(chains=256, moves=128, window=32, window_types=2, start="pack")
+    # GPU shapes from tools/migration_scan.py (10 s, seeds 0-2): X-1000 at 512
+    # chains x 128 moves (W = 2: one wavefront per SIMD), a migration every
+    # epoch of 80 with the 128 best replacing the 128 worst; TD-200 at 256 x
+    # 128 (its shapes were within run-to-run noise of each other)
+    kw = dict(chains=512, moves=128, window=32, window_types=2, start="pack", epochs=80,
+              mig_E=128) if instance == "x1000" else \
+        dict(chains=256, moves=128, window=32, window_types=2, start="pack")
     cells = []
     spread = None
     for sd in seeds:
@@ -428,7 +449,7 @@ def equal_time_cells(ctx, seconds, dist, with_cpu, instance="x1000", seeds=(0, 1
                           "runs": [a, b], "rel": abs(a - b) / min(a, b)}
         cells.append(cell)
     out = {"instance": instance, "T_s": seconds, "seeds": list(seeds),
-           "gpu_shape": "256 chains x 128 moves per step (W = 2)",
+           "gpu_shape": f"{kw['chains']} chains x {kw['moves']} moves per step (W = 2)",
            "host": f"oracle_sa_run_resync, better of {list(cpu_moves)} moves per step",
            "window": 32, "window_types": 2, "start": "pack", "cells": cells,
            "gap_sign": "negative = GPU better"}

@@ -14,14 +14,21 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-LIB = os.path.join(ROOT, "build_ab", "gaprof", "libvrpms.so")
+# GA_PROF_TAG=x: build_ab/gaprof_x (A/B); GA_PROF_SRC=<file>: that ga_fused.hip
+# instead of the tree's (e.g. an older revision written out by git show)
+TAG = os.environ.get("GA_PROF_TAG", "")
+LIB = os.path.join(ROOT, "build_ab", "gaprof" + (f"_{TAG}" if TAG else ""), "libvrpms.so")
 
 
 def build():
     from vrpms_amd import build as b
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    cmd = [b.HIPCC, *b.FLAGS, "-shared", "-DVRPMS_GA_PROF", "-o", LIB, *b.sources(), "-L/opt/rocm/lib",
-           "-lrccl"]
+    srcs = b.sources()
+    alt = os.environ.get("GA_PROF_SRC")
+    if alt:
+        srcs = [alt if os.path.basename(x) == "ga_fused.hip" else x for x in srcs]
+    cmd = [b.HIPCC, *b.FLAGS, "-shared", "-DVRPMS_GA_PROF", f"-I{b.CSRC}", "-o", LIB, *srcs,
+           "-L/opt/rocm/lib", "-lrccl"]
     subprocess.run(cmd, check=True)
 
 

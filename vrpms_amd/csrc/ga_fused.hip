@@ -91,7 +91,7 @@ static GaFusedLayout ga_fused_layout(int N, int n, int P) {
   a.off_crow = (uint32_t)off;   off = al16(off + (size_t)P * 2);
   a.off_sk = (uint32_t)off;     off = al16(off + (size_t)M * 8);
   a.off_si = (uint32_t)off;     off = al16(off + (size_t)M * 4);
-  a.off_used = (uint32_t)off;   off = al16(off + (size_t)32 * N * 4);  // 2 stamp arrays per wave
+  a.off_used = (uint32_t)off;   off = al16(off + (size_t)32 * N);  // 2 u8 stamp arrays per wave
   a.off_bits = (uint32_t)off;   off = al16(off + ((size_t)2 * P / 32 + 1) * 4);
   const size_t runs = (size_t)64 * ((P + 63) / 64);
   a.off_rk = (uint32_t)off;     off = al16(off + runs * 8);
@@ -119,8 +119,11 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
   uint16_t* crow = reinterpret_cast<uint16_t*>(smem + a.off_crow);
   uint64_t* sk = reinterpret_cast<uint64_t*>(smem + a.off_sk);
   uint32_t* si = reinterpret_cast<uint32_t*>(smem + a.off_si);
-  // mk[g] == the current child's stamp: gene g is in the child's A[lo..hi]
-  uint32_t* mk = reinterpret_cast<uint32_t*>(smem + a.off_used) + wave * (uint32_t)a.f.N;
+  // mk[g] == the current child's stamp: gene g is in the child's A[lo..hi].
+  // u8 stamps: an array spans N / 4 dwords, so a wave's 64 lookups at random
+  // genes fall in at most 64 distinct dwords -- distinct banks or one
+  // address, no bank conflicts; the arrays are cleared before the stamps wrap
+  uint8_t* mk = smem + a.off_used + wave * (uint32_t)a.f.N;
   uint32_t* bits = reinterpret_cast<uint32_t*>(smem + a.off_bits);
   uint16_t* gpop = a.pop_tours + (int64_t)island * P * n;
   uint64_t* gkeys = a.pop_keys + (int64_t)island * P;
@@ -138,8 +141,11 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
     crow[i] = (uint16_t)(P + i);
     pk[i] = gkeys[i];
   }
-  for (int i = threadIdx.x; i < 32 * a.f.N; i += blockDim.x)
-    reinterpret_cast<uint32_t*>(smem + a.off_used)[i] = 0u;
+  auto clear_stamps = [&]() {
+    for (int i = threadIdx.x; i < 8 * a.f.N; i += blockDim.x)  // 32 N bytes
+      reinterpret_cast<uint32_t*>(smem + a.off_used)[i] = 0u;
+  };
+  clear_stamps();
   __syncthreads();
   // survivors leave every generation ascending by (key, slot); the parents
   // handed in usually are too (the previous call's output), and then the
@@ -151,6 +157,7 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
     sorted_parents = __syncthreads_or(bad) == 0;
   }
   const int cpw = (P + 15) / 16;  // children per wavefront per generation
+  int gclr = 0;                   // generation of the last stamp clear
 
   WordChains<1> ch;
   ch.setup(a.f, smem);
@@ -160,6 +167,12 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
 #endif
   for (int g = 0; g < a.gens; ++g) {
     const uint64_t gen = a.gen0 + (uint64_t)g;
+    if ((g - gclr + 1) * cpw > 255) {  // this generation's stamps would pass 255
+      __syncthreads();
+      clear_stamps();
+      __syncthreads();
+      gclr = g;
+    }
     // ---- breed: one child per wavefront at a time --------------------------
     // Lane k of wave w first draws everything random about child w + 16k in
     // parallel (two Philox blocks, both tournaments, the OX1 cut points, the
@@ -198,7 +211,7 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
       const uint8_t* A[NC];
       const uint8_t* B[NC];
       uint8_t* out[NC];
-      uint32_t* m[NC];
+      uint8_t* m[NC];
       int lo[NC], hi[NC], mi[NC], mj[NC], rest[NC], filled[NC];
       bool mut[NC];
       uint32_t mtyp[NC], stamp[NC];
@@ -217,7 +230,7 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
         mtyp[c] = (uint32_t)wave_bcast(v_mtyp, k + c);
         mi[c] = wave_bcast(v_mi, k + c);
         mj[c] = wave_bcast(v_mj, k + c);
-        stamp[c] = 1u + (uint32_t)(g * cpw + k + c);
+        stamp[c] = 1u + (uint32_t)((g - gclr) * cpw + k + c);
         rest[c] = n - (hi[c] - lo[c] + 1);
         filled[c] = 0;
       }
@@ -238,7 +251,7 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
         for (int q = lo[c] + lane; q <= hi[c]; q += 64) {
           const uint32_t gq = A[c][q];
           out[c][dst_of(c, q)] = (uint8_t)gq;
-          m[c][gq] = stamp[c];
+          m[c][gq] = (uint8_t)stamp[c];
         }
       wave_sync();
       for (int base = 0; base < n; base += 128) {
