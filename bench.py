@@ -199,13 +199,15 @@ class _TimedCooling:
 def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label="cvrp100_k8 seed 0",
             gpu_seed=None, n_sep=None, window=0, window_types=0, start="random", moves=64,
             cpu_moves=64, gpu=True, mig_every=1, mig_E=None, epochs=40, t0_frac=0.5,
-            tend_frac=0.002):
+            tend_frac=0.002, cpu_tend_frac=None):
     """Best-cost gap at fixed wall time (the metric's second half): the same SA
     (Philox streams, 64 sampled moves per step, geometric cooling from
-    0.5 to 0.002 x the mean edge spread over the wall-time budget by
-    _TimedCooling) on the GPU -- `chains` chains with elite migration every 5
-    epochs (across ranks when N > 1) -- and on the host cores
-    (oracle/oracle_c.c oracle_sa_run_resync, one chain per OpenMP thread,
+    t0_frac to tend_frac x the typical edge spread over the wall-time budget
+    by _TimedCooling, `epochs` epochs) on the GPU -- `chains` chains, every
+    `mig_every` epochs the mig_E best-so-far tours replace the mig_E worst
+    current ones (across ranks when N > 1) -- and on the host cores
+    (the same migration scaled to its chains; cpu_tend_frac: its own final
+    temperature) (oracle/oracle_c.c oracle_sa_run_resync, one chain per OpenMP thread,
     each candidate priced by walking only the span the move can change and
     jumping over unchanged routes -- the same trajectories as the full walk).  Both legs run until
     `seconds` of wall time are spent.  Both legs search giant tours with
@@ -221,11 +223,15 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
     from vrpms_amd import islands, runners
     n = inst.n
     n_sep = inst.K - 1 if n_sep is None else n_sep
-    mig_E = chains // 2 if mig_E is None else mig_E
+    # a quarter of the chains restart from the elites every epoch (at most the
+    # 1024 vrpms_pool_elites selects at once)
+    mig_E = min(max(1, chains // 4), 1024) if mig_E is None else mig_E
     dev = ctx.dev
     edge = runners.typical_edge(inst.durations)
     t0, t_end = t0_frac * edge, tend_frac * edge
     out = {"T_s": seconds, "algorithm": "sa", "instance": label, "cooling": "wall-time geometric",
+           "t0_per_edge": t0_frac, "t_end_per_edge": {"gpu": tend_frac,
+                                                      "cpu": cpu_tend_frac or tend_frac},
            "separators": n_sep, "window": window, "window_types": window_types, "start": start}
     if gpu:
         warm = runners.SARunner(ctx, n, chains=chains, total_steps=1000, durations=inst.durations,
@@ -281,7 +287,9 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
         cur = cur.copy()
         best = cur.copy()
         bk = np.full(threads, 2**64 - 1, dtype=np.uint64)
-        cool = _TimedCooling(seconds, t0, t_end, epochs=epochs)
+        # the host leg's final temperature (its own best schedule, if given)
+        t_end_h = t_end if cpu_tend_frac is None else cpu_tend_frac * edge
+        cool = _TimedCooling(seconds, t0, t_end_h, epochs=epochs)
         # the GPU leg's migration scaled to the host's chains: every mig_every
         # epochs the same fraction of chains restarts from the best-so-far
         # tours (the E best by key replace the E worst current tours)
@@ -419,13 +427,17 @@ def equal_time_cells(ctx, seconds, dist, with_cpu, instance="x1000", seeds=(0, 1
     from vrpms_amd.core import CVRP
     make = {"x1000": lambda sd: synth.x_style(1000, seed=sd),
             "tdvrp200": lambda sd: synth.td_cvrp(200, 16, seed=sd)}[instance]
-    # GPU shapes from tools/migration_scan.py (10 s, seeds 0-2): X-1000 at 512
-    # chains x 128 moves (W = 2: one wavefront per SIMD), a migration every
-    # epoch of 80 with the 128 best replacing the 128 worst; TD-200 at 256 x
-    # 128 (its shapes were within run-to-run noise of each other)
-    kw = dict(chains=512, moves=128, window=32, window_types=2, start="pack", epochs=80,
-              mig_E=128) if instance == "x1000" else \
-        dict(chains=256, moves=128, window=32, window_types=2, start="pack")
+    # GPU shapes from tools/migration_scan.py (10 s, seeds 0-2): X-1000 at 1024
+    # chains x 128 moves (W = 2: two wavefronts per SIMD, sa_seg_kernel's OCC = 2
+    # variant), a migration every epoch of 80 with the 256 best replacing the
+    # 256 worst; TD-200 at 256 x
+    # 128 (its shapes were within run-to-run noise of each other).  Final
+    # temperatures from tools/sched_scan.py (X-1000, 10 s, seeds 0-1, both legs
+    # at six schedules): each leg at the one that scored best for it on
+    # average, 0.004 x the typical edge for the GPU, 0.002 for the host
+    kw = dict(chains=1024, moves=128, window=32, window_types=2, start="pack", epochs=80,
+              mig_E=256, tend_frac=0.004, cpu_tend_frac=0.002) if instance == "x1000" else \
+        dict(chains=256, moves=128, window=32, window_types=2, start="pack", mig_E=128)
     cells = []
     spread = None
     for sd in seeds:

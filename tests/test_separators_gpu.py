@@ -500,3 +500,34 @@ def test_segment_sa_matches_c_restatement(ctx, coracle, name, maker, start, chai
         assert (cur.cpu().numpy().view(np.uint16) == ccur).all()
         assert u64(ck) == [int(x) for x in cck] and u64(bk) == [int(x) for x in cbk]
         assert (best.cpu().numpy().view(np.uint16) == cbest).all()
+
+
+@pytest.mark.parametrize("het,moves", [(False, 128), (True, 64)])
+def test_segment_sa_two_wavefronts_per_simd_same_trajectories(ctx, het, moves):
+    """A launch with more wavefronts than the chip has SIMDs runs
+    sa_seg_kernel's OCC = 2 variant (registers capped for two wavefronts per
+    SIMD).  Chain c draws the same Philox streams in any launch, so the first
+    chains of a 1,280-chain launch must follow exactly the trajectories of
+    an 8-chain launch (the OCC = 1 variant, checked against the C
+    restatement above)."""
+    torch = torch_()
+    inst = synth.x_style(1000, seed=3)
+    if het:
+        inst = _classes(inst, (1.4, 1.1, 0.9))
+    load(ctx, inst)
+    S = inst.K - 1
+    big = 1280
+    P0 = synth.random_perms(big, inst.n, seed=9, dtype=np.uint16)
+    P = np.array([spec.pack_separators(p, S, inst.demand, inst.capacities) for p in P0])
+    P = P.astype(np.int16)
+    out = []
+    for chains in (8, big):
+        cur = torch.from_numpy(P[:chains].copy()).to(ctx.dev)
+        best = cur.clone()
+        ck = torch.empty(chains, dtype=torch.int64, device=ctx.dev)
+        bk = torch.full((chains,), -1, dtype=torch.int64, device=ctx.dev)
+        ctx.sa_run(cur, ck, best, bk, steps=60, inv_t0=1 / 300.0, inv_alpha=1 / 0.99, seed=33,
+                   step0=5, window=32, window_types=2, moves=moves)
+        out.append((cur.cpu().numpy()[:8], u64(ck)[:8], best.cpu().numpy()[:8], u64(bk)[:8]))
+    a, b = out
+    assert (a[0] == b[0]).all() and a[1] == b[1] and (a[2] == b[2]).all() and a[3] == b[3]

@@ -2,7 +2,7 @@
 """GPU SA leg on X-1000 (cfg 4) at T seconds for several elite-migration
 settings (every k epochs, E elites into the worst chains) and chain /
 move / epoch counts; GPU only.
-usage: migration_scan.py T seed every:E[:chains[:moves[:epochs]]] ..."""
+usage: migration_scan.py T seed every:E[:chains[:moves[:epochs[:tend_per_mille]]]] ..."""
 import json
 import os
 import sys
@@ -19,11 +19,12 @@ td = os.environ.get("INSTANCE") == "td"
 x = synth.td_cvrp(200, 16, seed=seed) if td else synth.x_style(1000, seed=seed)
 ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
 for spec in sys.argv[3:]:
-    v = [int(t) for t in spec.split(":")] + [256, 128, 40][len(spec.split(":")) - 2:]
-    every, E, chains, moves, epochs = v[:5]
+    v = [int(t) for t in spec.split(":")] + [256, 128, 40, 2][len(spec.split(":")) - 2:]
+    every, E, chains, moves, epochs, tend = v[:6]   # tend: final temperature, 1/1000 edge
     q = bench.quality(ctx, x, T, 1, 0, None, with_cpu=False, chains=chains, moves=moves, window=32,
-                      window_types=2, start="pack", mig_every=every, mig_E=E, epochs=epochs)
-    print(json.dumps({"every": every, "E": E, "chains": chains, "moves": moves, "epochs_planned": epochs,
+                      window_types=2, start="pack", mig_every=every, mig_E=E, epochs=epochs,
+                      tend_frac=tend / 1000.0)
+    print(json.dumps({"every": every, "E": E, "chains": chains, "moves": moves, "epochs_planned": epochs, "tend": tend,
                       "gpu": q["gpu"]["duration_sum"],
                       "steps": q["gpu"]["steps_per_chain"], "epochs": q["gpu"]["epochs"]}),
           flush=True)

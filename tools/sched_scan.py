@@ -15,13 +15,15 @@ from vrpms_amd.core import CVRP, Context  # noqa: E402
 
 T, seed = float(sys.argv[1]), int(sys.argv[2])
 ctx = Context(0)
-x = synth.x_style(1000, seed=seed)
+# INSTANCE=td: cfg 3's TD-200 x 24 (sa_route_kernel, 256 chains, 40 epochs)
+td = os.environ.get("INSTANCE") == "td"
+x = synth.td_cvrp(200, 16, seed=seed) if td else synth.x_style(1000, seed=seed)
 ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
 for spec in sys.argv[3:]:
     a, b = (float(v) for v in spec.split(":"))
-    q = bench.quality(ctx, x, T, 1, 0, None, with_cpu=True, chains=512, moves=128, window=32,
-                      window_types=2, start="pack", mig_every=1, mig_E=128, epochs=80,
-                      cpu_moves=32, t0_frac=a, tend_frac=b)
+    shape = dict(chains=256, mig_E=128, epochs=40) if td else dict(chains=512, mig_E=128, epochs=80)
+    q = bench.quality(ctx, x, T, 1, 0, None, with_cpu=True, moves=128, window=32, window_types=2,
+                      start="pack", mig_every=1, cpu_moves=32, t0_frac=a, tend_frac=b, **shape)
     print(json.dumps({"t0": a, "t_end": b, "gpu": q["gpu"]["duration_sum"],
                       "gpu_ok": q["gpu"]["rescored_equal"], "cpu": q["cpu"]["duration_sum"],
                       "cpu_ok": q["cpu"]["rescored_equal"], "gap": q.get("gap")}), flush=True)

@@ -165,8 +165,13 @@ constexpr int kSegProf = 22;  // + cut iterations (wave max, lane sum), search s
 __device__ unsigned long long g_seg_prof[kSegProf * 8192];
 #endif
 
-template <typename MatT, bool HET>  // HET: per-vehicle capacities
-__global__ __launch_bounds__(64 * kSegMaxWaves) void sa_seg_kernel(SegArgs a) {
+// HET: per-vehicle capacities.  OCC: wavefronts per SIMD the register budget
+// allows -- 1 (the compiler's choice, ~270 registers) or 2 (capped at 256,
+// a little spill): a launch with more wavefronts than SIMDs takes OCC = 2,
+// whose second wavefront hides the first's dependent latency (X-1000, 1024
+// chains x W = 2: 33-38 k steps/s per chain against 17-22 k at OCC = 1)
+template <typename MatT, bool HET, int OCC>
+__global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 #ifdef VRPMS_SEG_PROF
   const unsigned long long pk0 = wall_clock64();
@@ -1178,7 +1183,7 @@ int launch_sa_seg(const vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* d_cu
   const size_t base = inst_lds_bytes_host(si) + (((size_t)in.N * 4u + 15u) & ~(size_t)15u);
   // wavefronts per chain: W > 1 prices the step's moves on W SIMDs at once
   // (same moves, same winner, so the same trajectories as W = 1), while the
-  // chains' wavefronts stay resident (two per SIMD at this kernel's VGPRs)
+  // chains' wavefronts stay resident (two per SIMD with the OCC = 2 variant)
   int W = std::min(moves / 64, kSegMaxWaves);
   while (W > 1 && (int64_t)p->chains * W > 8 * (int64_t)ctx->num_cus) W >>= 1;
   if (ctx->opt_seg_waves > 0) W = std::min(ctx->opt_seg_waves, kSegMaxWaves);  // A/B
@@ -1199,12 +1204,14 @@ int launch_sa_seg(const vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* d_cu
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     kern<<<dim3((p->chains + cpw - 1) / cpw), dim3(64 * cpw * W), lds, s>>>(a);
   };
+  // more wavefronts than SIMDs: the two-per-SIMD register budget
+  const bool occ2 = (int64_t)p->chains * W > 4 * (int64_t)ctx->num_cus;
   if (het) {
-    if (in.use16) go(sa_seg_kernel<uint16_t, true>);
-    else go(sa_seg_kernel<int32_t, true>);
+    if (in.use16) occ2 ? go(sa_seg_kernel<uint16_t, true, 2>) : go(sa_seg_kernel<uint16_t, true, 1>);
+    else occ2 ? go(sa_seg_kernel<int32_t, true, 2>) : go(sa_seg_kernel<int32_t, true, 1>);
   } else {
-    if (in.use16) go(sa_seg_kernel<uint16_t, false>);
-    else go(sa_seg_kernel<int32_t, false>);
+    if (in.use16) occ2 ? go(sa_seg_kernel<uint16_t, false, 2>) : go(sa_seg_kernel<uint16_t, false, 1>);
+    else occ2 ? go(sa_seg_kernel<int32_t, false, 2>) : go(sa_seg_kernel<int32_t, false, 1>);
   }
   VRPMS_HIP(hipGetLastError());
   return VRPMS_OK;
