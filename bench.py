@@ -199,7 +199,7 @@ class _TimedCooling:
 def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label="cvrp100_k8 seed 0",
             gpu_seed=None, n_sep=None, window=0, window_types=0, start="random", moves=64,
             cpu_moves=64, gpu=True, mig_every=1, mig_E=None, epochs=40, t0_frac=0.5,
-            tend_frac=0.002, cpu_tend_frac=None):
+            tend_frac=0.002, cpu_tend_frac=None, cpu_t0_frac=None):
     """Best-cost gap at fixed wall time (the metric's second half): the same SA
     (Philox streams, 64 sampled moves per step, geometric cooling from
     t0_frac to tend_frac x the typical edge spread over the wall-time budget
@@ -230,8 +230,8 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
     edge = runners.typical_edge(inst.durations)
     t0, t_end = t0_frac * edge, tend_frac * edge
     out = {"T_s": seconds, "algorithm": "sa", "instance": label, "cooling": "wall-time geometric",
-           "t0_per_edge": t0_frac, "t_end_per_edge": {"gpu": tend_frac,
-                                                      "cpu": cpu_tend_frac or tend_frac},
+           "t0_per_edge": {"gpu": t0_frac, "cpu": cpu_t0_frac or t0_frac},
+           "t_end_per_edge": {"gpu": tend_frac, "cpu": cpu_tend_frac or tend_frac},
            "separators": n_sep, "window": window, "window_types": window_types, "start": start}
     if gpu:
         warm = runners.SARunner(ctx, n, chains=chains, total_steps=1000, durations=inst.durations,
@@ -289,7 +289,8 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
         bk = np.full(threads, 2**64 - 1, dtype=np.uint64)
         # the host leg's final temperature (its own best schedule, if given)
         t_end_h = t_end if cpu_tend_frac is None else cpu_tend_frac * edge
-        cool = _TimedCooling(seconds, t0, t_end_h, epochs=epochs)
+        t0_h = t0 if cpu_t0_frac is None else cpu_t0_frac * edge
+        cool = _TimedCooling(seconds, t0_h, t_end_h, epochs=epochs)
         # the GPU leg's migration scaled to the host's chains: every mig_every
         # epochs the same fraction of chains restarts from the best-so-far
         # tours (the E best by key replace the E worst current tours)
@@ -432,12 +433,14 @@ def equal_time_cells(ctx, seconds, dist, with_cpu, instance="x1000", seeds=(0, 1
     # variant), a migration every epoch of 80 with the 256 best replacing the
     # 256 worst; TD-200 at 256 x
     # 128 (its shapes were within run-to-run noise of each other).  Final
-    # temperatures from tools/sched_scan.py (X-1000, 10 s, seeds 0-1, both legs
-    # at six schedules): each leg at the one that scored best for it on
-    # average, 0.004 x the typical edge for the GPU, 0.002 for the host
+    # temperatures from tools/sched_scan.py (10 s, seeds 0-1, both legs at six
+    # schedules): each leg at the one that scored best for it on average --
+    # X-1000: (t0, t_end) = (0.5, 0.004) x the typical edge for the GPU, (0.5,
+    # 0.002) for the host; TD-200: (0.5, 0.004) and (1.0, 0.002)
     kw = dict(chains=1024, moves=128, window=32, window_types=2, start="pack", epochs=80,
               mig_E=256, tend_frac=0.004, cpu_tend_frac=0.002) if instance == "x1000" else \
-        dict(chains=256, moves=128, window=32, window_types=2, start="pack", mig_E=128)
+        dict(chains=256, moves=128, window=32, window_types=2, start="pack", mig_E=128,
+             tend_frac=0.004, cpu_t0_frac=1.0, cpu_tend_frac=0.002)
     cells = []
     spread = None
     for sd in seeds:
