@@ -104,3 +104,23 @@ def test_pool_round_robin_two_devices_matches_app_contract():
 def test_pool_rejects_empty_configuration():
     with pytest.raises(ValueError):
         frontends.FrontEndPool(_store(1, 5), workers=0)
+
+
+def test_pool_raises_when_an_owner_dies():
+    """A GPU owner that exits leaves its batches unanswered: post_many raises
+    (it does not wait forever) and close() tears the pool down."""
+    import os
+
+    def factory(dev):
+        def launch(N, host):
+            os._exit(3)
+        return launch
+    N = 8
+    store = _store(4, N)
+    pool = frontends.FrontEndPool(store, workers=1, devices=(0,), slots_per_worker=8, nmax=16,
+                                  chunk=4, launch_factory=factory, app_factory=_fake_app(store))
+    try:
+        with pytest.raises(RuntimeError, match="exited"):
+            pool.post_many("tsp", "sa", [_body(i, N) for i in range(4)])
+    finally:
+        pool.close()

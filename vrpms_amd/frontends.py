@@ -439,7 +439,15 @@ class FrontEndPool:
                     (jid, problem, algorithm, bodies[start:start + self.chunk]))
             out = [None] * len(bodies)
             for _ in range(len(jobs)):
-                jid, res, rows = self._resp_q.get()
+                while True:   # a worker or owner that died leaves its jobs unanswered: raise
+                    try:
+                        jid, res, rows = self._resp_q.get(timeout=5.0)
+                        break
+                    except queue.Empty:
+                        dead = [p.name for p in self._procs if not p.is_alive()]
+                        if dead:
+                            raise RuntimeError(f"FrontEndPool: process(es) {dead} exited; "
+                                               f"{len(jobs)} job(s) of this call unanswered")
                 s = jobs[jid]
                 out[s:s + len(res)] = res if raw else [(st, json.loads(b)) for st, b in res]
                 if rows:
@@ -447,6 +455,13 @@ class FrontEndPool:
             return out
 
     def close(self):
+        if any(not p.is_alive() for p in self._procs):   # a process died: no orderly drain
+            for p in self._procs:
+                if p.is_alive():
+                    p.terminate()
+                p.join(timeout=10)
+            self.arena.close(unlink=True)
+            return
         for q in self._req_qs:
             q.put(_STOP)
         for _ in range(self.workers):           # workers drain before the owners stop
