@@ -331,7 +331,7 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
     return out
 
 
-def algo_quality(ctx, inst, seconds, seed=0, polish_steps=50, polish_top=4):
+def algo_quality(ctx, inst, seconds, seed=0, polish_steps=100, polish_top=4):
     """The GA and ACO endpoints' best cost at the same wall time as the SA
     quality leg (cfg 2, api/vrp/{ga,aco}/index.py): each runs on the GPU for
     `seconds` of wall time -- GA 256 islands x 256 (randomPermutationCount),

@@ -396,9 +396,10 @@ int oracle_sa_run(int problem, const int32_t* D, int H, int N, const int32_t* de
 /* Throughput-mode restatement (oracle/search.py tsp_batch_sa, the C-ABI's
  * vrpms_tsp_batch_sa): R static TSP requests, int32 [R][N][N]; per request 4
  * chains from Philox Fisher-Yates starts (counters (~0, ~0, 4r + w, i)), SA
- * steps drawing from one Philox block per two steps (counters (s >> 1, 0,
- * 4r + w, lane); words 0, 1 on even steps, 2, 3 on odd: the move by
- * decode_move1 (spec.py A13), the acceptance draw), every candidate priced by a full
+ * steps drawing from one Philox block per lane per four steps (A13:
+ * counters (s >> 2, 0, 4r + w, lane), word s & 3 decoded by decode_move1)
+ * and one per chain for the acceptance draws (counters (s >> 2, 1, 4r + w,
+ * 0), word s & 3), every candidate priced by a full
  * re-evaluation (the device prices by O(1) deltas, so equality checks them);
  * the answer is the best (key, chain).  Out: tours [R][N-1], keys [R]. */
 int oracle_tsp_batch_sa(const int32_t* mats, int R, int N, int steps, float inv_t0,
@@ -431,15 +432,17 @@ int oracle_tsp_batch_sa(const int32_t* mats, int R, int N, int steps, float inv_
       for (int s = 0; s < steps && n >= 2; ++s) {
         uint64_t kbest = ~0ull;
         move_t mbest = {0, 0, 0};
-        uint32_t wbest = 0;
+        const u32x4 ra = philox((uint32_t)(s >> 2), 1u, cid, 0u, k0, k1);  /* the chain's draws */
+        const uint32_t a4[4] = {ra.x, ra.y, ra.z, ra.w};
+        const uint32_t wbest = a4[s & 3];
         for (int lane = 0; lane < 64; ++lane) {
-          u32x4 rr = philox((uint32_t)(s >> 1), 0u, cid, (uint32_t)lane, k0, k1);
-          move_t m = decode_move1((s & 1) ? rr.z : rr.x, n);
+          u32x4 rr = philox((uint32_t)(s >> 2), 0u, cid, (uint32_t)lane, k0, k1);
+          const uint32_t w4[4] = {rr.x, rr.y, rr.z, rr.w};
+          move_t m = decode_move1(w4[s & 3], n);
           uint64_t kk = tour_key(&I, A, n, &m);
           if (kk < kbest) {
             kbest = kk;
             mbest = m;
-            wbest = (s & 1) ? rr.w : rr.y;
           }
         }
         int acc = kbest <= ck;

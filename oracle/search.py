@@ -122,11 +122,11 @@ def sa_run(score: Scorer, cur_tours, best_tours, best_keys, seed: int, step0: in
 
 def tsp_batch_sa(mats, steps: int, inv_t0: float, inv_alpha: float, seed: int):
     """vrpms_tsp_batch_sa: per request 4 chains (Philox Fisher-Yates starts,
-    counters (0xffffffff, 0xffffffff, 4r + w, i)); one Philox block with
-    counters (s >> 1, 0, 4r + w, lane) serves two SA steps (A13): step s uses
-    words (0, 1) when s is even, (2, 3) when odd -- the move from the first
-    (spec.decode_move1), the acceptance draw from the second; best (key,
-    wave).  Costs by full re-evaluation -- the device prices moves by O(1)
+    counters (0xffffffff, 0xffffffff, 4r + w, i)); A13: one Philox block per
+    lane with counters (s >> 2, 0, 4r + w, lane) serves four SA steps -- step
+    s decodes its move from word s & 3 (spec.decode_move1) -- and the chain's
+    acceptance draw of step s is word s & 3 of the block with counters
+    (s >> 2, 1, 4r + w, 0), one per chain; best (key, wave).  Costs by full re-evaluation -- the device prices moves by O(1)
     deltas, so equality checks the deltas."""
     key = spec.seed_key(seed)
     out_t, out_k = [], []
@@ -149,11 +149,11 @@ def tsp_batch_sa(mats, steps: int, inv_t0: float, inv_alpha: float, seed: int):
                 for s in range(steps):
                     cands = []
                     for lane in range(64):
-                        rr = spec.philox4x32_10((s >> 1, 0, cid, lane), key)
-                        h = 2 * (s & 1)
-                        m = spec.decode_move1(rr[h], n)
-                        cands.append((score(spec.apply_move(t, *m)), lane, m, rr[h + 1]))
-                    kk, lane, m, r3 = min(cands, key=lambda c: (c[0], c[1]))
+                        rr = spec.philox4x32_10((s >> 2, 0, cid, lane), key)
+                        m = spec.decode_move1(rr[s & 3], n)
+                        cands.append((score(spec.apply_move(t, *m)), lane, m))
+                    kk, lane, m = min(cands, key=lambda c: (c[0], c[1]))
+                    r3 = spec.philox4x32_10((s >> 2, 1, cid, 0), key)[s & 3]
                     acc = kk <= ck
                     if not acc:
                         dp = min((kk >> 28) - (ck >> 28), M32)

@@ -332,7 +332,8 @@ def decode_move(r0: int, r1: int, r2: int, n: int):
 
 def decode_move1(x: int, n: int):
     """A13: one Philox word -> (type, i, j), the throughput kernel's move
-    (vrpms_tsp_batch_sa, two SA steps per Philox block).  The word is split
+    (vrpms_tsp_batch_sa: four SA steps per lane's Philox block, the
+    acceptance draws from one block per chain, oracle/search.py).  The word is split
     by successive fixed-point multiplications: type = hi(3x), i = hi(n * f1)
     with f1 = lo(3x), j' = hi((n - 1) * f2) with f2 = lo(n * f1); j = j' + 1
     when j' >= i; swap / 2-opt canonicalised i < j."""

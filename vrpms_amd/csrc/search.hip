@@ -2123,12 +2123,18 @@ VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, unsigned cha
   uint64_t ck = pack_key(0, (uint32_t)dur, 0), bk = ck;
   for (int q = lane; q < n; q += 64) Best[q] = A[q];
   float invT = a.inv_t0;
-  // A13: one Philox block per lane serves two steps -- words (x, y) on an
-  // even step, (z, w) on the odd one: the move, then the acceptance draw
-  u32x4 rb = {0u, 0u, 0u, 0u};
+  // A13: one Philox block per lane serves four steps (word s & 3 is step s's
+  // move) and one per chain -- wave-uniform counters, so the scalar unit
+  // computes it -- the four steps' acceptance draws
+  u32x4 rb = {0u, 0u, 0u, 0u}, ra = {0u, 0u, 0u, 0u};
   for (int s = 0; s < a.steps && n >= 2; ++s) {
-    if ((s & 1) == 0) rb = philox((uint32_t)(s >> 1), 0u, cid, (uint32_t)lane, a.seed_lo, a.seed_hi);
-    const uint32_t xm = (s & 1) ? rb.z : rb.x, xa = (s & 1) ? rb.w : rb.y;
+    if ((s & 3) == 0) {
+      rb = philox((uint32_t)(s >> 2), 0u, cid, (uint32_t)lane, a.seed_lo, a.seed_hi);
+      ra = philox((uint32_t)(s >> 2), 1u, cid, 0u, a.seed_lo, a.seed_hi);
+    }
+    const int h = s & 3;
+    const uint32_t xm = h == 0 ? rb.x : h == 1 ? rb.y : h == 2 ? rb.z : rb.w;
+    const uint32_t xa = h == 0 ? ra.x : h == 1 ? ra.y : h == 2 ? ra.z : ra.w;
     const Move m = decode_move1(xm, n);
     auto tourA = [&](int q) { return (uint32_t)A[q]; };
     int delta;
@@ -2148,7 +2154,7 @@ VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, unsigned cha
     if (!accept) {
       const uint64_t d = (k >> 28) - (ck >> 28);
       const uint32_t dp = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
-      accept = ((uint32_t)wave_bcast((int)xa, bl) >> 8) < accept_threshold(dp, invT);
+      accept = (xa >> 8) < accept_threshold(dp, invT);
     }
     if (accept) {  // bl is wave-uniform: the winner's move by v_readlane
       Move mb;
