@@ -2097,17 +2097,20 @@ VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, unsigned cha
   uint16_t* B = buf + npad;
   uint16_t* Best = buf + 2 * npad;
   const uint32_t cid = (uint32_t)(r * 4 + wave);
-  // Philox Fisher-Yates start (lane 0): for i = n-1..1 swap t[i], t[x % (i+1)]
+  // Philox Fisher-Yates start: for i = n-1..1 swap t[i], t[x % (i+1)].  The
+  // draws have wave-uniform counters (the scalar unit computes them); lane 0
+  // swaps.
   for (int q = lane; q < n; q += 64) A[q] = (uint16_t)(q + 1);
   wave_sync();
-  if (lane == 0)
-    for (int i = n - 1; i >= 1; --i) {
-      const u32x4 x = philox(0xffffffffu, 0xffffffffu, cid, (uint32_t)i, a.seed_lo, a.seed_hi);
-      const int j = (int)(x.x % (uint32_t)(i + 1));
+  for (int i = n - 1; i >= 1; --i) {
+    const u32x4 x = philox(0xffffffffu, 0xffffffffu, cid, (uint32_t)i, a.seed_lo, a.seed_hi);
+    const int j = (int)__builtin_amdgcn_readfirstlane((int)(x.x % (uint32_t)(i + 1)));
+    if (lane == 0) {
       const uint16_t t = A[i];
       A[i] = A[j];
       A[j] = t;
     }
+  }
   wave_sync();
   auto dist = [&](uint32_t x, uint32_t y) { return (int)D[__umul24(x, (uint32_t)N) + y]; };
   auto full = [&](const uint16_t* T) {
