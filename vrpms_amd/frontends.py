@@ -4,7 +4,7 @@
 One Python process cannot serve cfg 5: the per-request JSON parse, the DB
 matrix ingest (a nested list of N^2 JSON integers -> int32) and the response
 build all hold the GIL, so one process saturates near 5 k requests/s while
-the kernel could answer ~800 k/s.  FrontEndPool splits the work:
+the kernel could answer ~1 M/s.  FrontEndPool splits the work:
 
   * W front-end WORKER processes (forked before any GPU call; they never
     touch the GPU) run the reference's request contract -- parse, parameter
@@ -17,7 +17,12 @@ the kernel could answer ~800 k/s.  FrontEndPool splits the work:
     into one int32 buffer, runs vrpms_tsp_batch_sa (one workgroup per
     request), and writes the tours and durations back into the slots;
   * the workers hand their batches to the owners round-robin (SURVEY.md §8e
-    cfg 5: replicas only, no collective), wait for the slots, and answer.
+    cfg 5: replicas only, no collective), wait for the slots, and answer
+    with the response bytes the HTTP handler would write (encoding is part
+    of serving, so it runs in parallel in the workers);
+  * an owner launches asynchronously (pinned staging, rotating streams) and
+    keeps up to two batches on the device while it collects the next; a
+    pool whose worker or owner process died raises instead of waiting.
 
 Requests that are not batchable (other endpoints, hour-indexed matrices,
 node counts outside the arena) go to an owner's full App.post (the unbatched
