@@ -2126,18 +2126,8 @@ VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, unsigned cha
   uint64_t ck = pack_key(0, (uint32_t)dur, 0), bk = ck;
   for (int q = lane; q < n; q += 64) Best[q] = A[q];
   float invT = a.inv_t0;
-  // A13: one Philox block per lane serves four steps (word s & 3 is step s's
-  // move) and one per chain -- wave-uniform counters, so the scalar unit
-  // computes it -- the four steps' acceptance draws
-  u32x4 rb = {0u, 0u, 0u, 0u}, ra = {0u, 0u, 0u, 0u};
-  for (int s = 0; s < a.steps && n >= 2; ++s) {
-    if ((s & 3) == 0) {
-      rb = philox((uint32_t)(s >> 2), 0u, cid, (uint32_t)lane, a.seed_lo, a.seed_hi);
-      ra = philox((uint32_t)(s >> 2), 1u, cid, 0u, a.seed_lo, a.seed_hi);
-    }
-    const int h = s & 3;
-    const uint32_t xm = h == 0 ? rb.x : h == 1 ? rb.y : h == 2 ? rb.z : rb.w;
-    const uint32_t xa = h == 0 ? ra.x : h == 1 ? ra.y : h == 2 ? ra.z : ra.w;
+  // one SA step: xm = the lane's move word, xa = the chain's acceptance draw
+  auto step = [&](uint32_t xm, uint32_t xa) __attribute__((always_inline)) {
     const Move m = decode_move1(xm, n);
     auto tourA = [&](int q) { return (uint32_t)A[q]; };
     int delta;
@@ -2178,6 +2168,27 @@ VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, unsigned cha
       wave_sync();
     }
     invT = invT * a.inv_alpha;
+  };
+  // A13: one Philox block per lane serves four steps (word s & 3 is step s's
+  // move) and one per chain -- wave-uniform counters, so the scalar unit
+  // computes it -- the four steps' acceptance draws.  Unrolled by four, so
+  // each step reads its words without a select.
+  int s = 0;
+  if (n >= 2) {
+    for (; s + 4 <= a.steps; s += 4) {
+      const u32x4 rb = philox((uint32_t)(s >> 2), 0u, cid, (uint32_t)lane, a.seed_lo, a.seed_hi);
+      const u32x4 ra = philox((uint32_t)(s >> 2), 1u, cid, 0u, a.seed_lo, a.seed_hi);
+      step(rb.x, ra.x);
+      step(rb.y, ra.y);
+      step(rb.z, ra.z);
+      step(rb.w, ra.w);
+    }
+    if (s < a.steps) {  // the last 1..3 steps
+      const u32x4 rb = philox((uint32_t)(s >> 2), 0u, cid, (uint32_t)lane, a.seed_lo, a.seed_hi);
+      const u32x4 ra = philox((uint32_t)(s >> 2), 1u, cid, 0u, a.seed_lo, a.seed_hi);
+      for (int h = 0; s + h < a.steps; ++h)
+        step(h == 0 ? rb.x : h == 1 ? rb.y : rb.z, h == 0 ? ra.x : h == 1 ? ra.y : ra.z);
+    }
   }
   if (lane == 0) wbest[wave] = bk;
   __syncthreads();
