@@ -479,23 +479,29 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
     }
     wave_sync();
     if (HET) {  // NB[d]: the next route that would split differently 1..kSegShift vehicles on / back
+      // one pass over the routes (top down): each lane reads its route's
+      // load and allowance once and scans the 2 kSegShift shifts from
+      // registers (a suffix maximum of 0xffff - r over the routes that fail)
+      uint32_t carry[2 * kSegShift];
+#pragma unroll
+      for (int d = 0; d < 2 * kSegShift; ++d) carry[d] = 0u;
 #pragma unroll 1
-      for (int d = 0; d < 2 * kSegShift; ++d) {
-        const int dl = d < kSegShift ? d - kSegShift : d - kSegShift + 1;
-        uint16_t* b = T.NB + d * (RM + 1);
-        uint32_t carry = 0;  // suffix maximum of 0xffff - r over the routes r that fail
-#pragma unroll 1
-        for (int top = (R / 64) * 64; top >= 0; top -= 64) {
-          const int r = top + lane;
+      for (int top = (R / 64) * 64; top >= 0; top -= 64) {
+        const int r = top + lane;
+        const bool in = r < R;
+        const uint32_t need = in ? T.need[r] : 0u, allow = in ? T.allow[r] : 0u;
+#pragma unroll
+        for (int d = 0; d < 2 * kSegShift; ++d) {
+          const int dl = d < kSegShift ? d - kSegShift : d - kSegShift + 1;
           uint32_t v = 0;
-          if (r < R) {
+          if (in) {
             const uint32_t c = capv(r + dl);
-            v = (r + dl < 0 || T.need[r] > c || c > T.allow[r]) ? 0xffffu - (uint32_t)r : 0u;
+            v = (r + dl < 0 || need > c || c > allow) ? 0xffffu - (uint32_t)r : 0u;
           }
           uint32_t tm;
-          const uint32_t m = max(dpp_rscan_max(v, tm), carry);
-          if (r <= R) b[r] = (uint16_t)(m ? 0xffffu - m : (uint32_t)R);
-          carry = max(carry, tm);
+          const uint32_t m = max(dpp_rscan_max(v, tm), carry[d]);
+          if (r <= R) T.NB[d * (RM + 1) + r] = (uint16_t)(m ? 0xffffu - m : (uint32_t)R);
+          carry[d] = max(carry[d], tm);
         }
       }
       wave_sync();
@@ -904,7 +910,10 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
           return true;
         };
         // the start of the first changed segment, up to lo: the current split
-        if (ra1 - ra > 1) aligned(p_start, ra, ra1);
+        // (the heterogeneous variant keeps round 3's run(): with the table
+        // path its composition measured ~2 us slower per step, and
+        // tools/het_rate.py 9.6 k -> 9.8 k steps/s without it)
+        if (!HET && ra1 - ra > 1) aligned(p_start, ra, ra1);
         else run(p_start, false, 0u);
 #pragma unroll
         for (int s = 0; s < 3; ++s) {
@@ -967,7 +976,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
           // (D) the part after the last separator opens the next route: read
           // forward, the current split of that segment's start (on the same
           // vehicles)
-          if (hs && !rev && RG1[s] - RG0[s] > 1 && (!HET || vo == RG0[s])) aligned(PDn[s], RG0[s], RG1[s]);
+          if (!HET && hs && !rev && RG1[s] - RG0[s] > 1) aligned(PDn[s], RG0[s], RG1[s]);
           else run(PDn[s], rev, 0u);
         }
         // the rest of the last changed segment, closed by its separator (or
