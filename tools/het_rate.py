@@ -33,6 +33,9 @@ fr = (1.3, 1.0, 0.8) if TD else (1.4, 1.1, 0.9)
 caps = np.array([max(int(base * fr[k * 3 // K]), int(x.demand.max())) for k in range(K)])
 starts = np.arange(K, dtype=np.int64) * 37 % 240 + (420 if TD else 0)
 window = 16 if TD else 32
+if os.environ.get("VRPMS_LIB"):  # an A/B build (e.g. build_ab/het8/libvrpms.so)
+    from vrpms_amd import _lib
+    _lib.load(os.environ["VRPMS_LIB"])
 ctx = Context(0)
 ctx.set_instance(CVRP, x.durations, x.demand, caps, starts)
 out = {}
