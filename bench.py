@@ -309,7 +309,7 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
             e += 1
             if e_host and e % mig_every == 0 and threads > 1:
                 top = np.argsort(bk, kind="stable")[:e_host]
-                worst = np.argsort(-np.asarray(ck, dtype=np.float64), kind="stable")[:e_host]
+                worst = np.argsort(np.asarray(ck, dtype=np.uint64), kind="stable")[::-1][:e_host]
                 cur[worst] = best[top]
         cpu_wall = cool.elapsed()
         ck = int(bk.min())
