@@ -42,9 +42,9 @@ namespace vrpms {
 constexpr int kSegRegs = 20;      // positions per lane in registers on an accept: n < 64 * 20
 constexpr int kSegMaxMoves = 8;   // moves per lane per step (64 M per step)
 #ifndef VRPMS_SEG_SHIFT
-#define VRPMS_SEG_SHIFT 6  // (A/B builds may set another)
+#define VRPMS_SEG_SHIFT 8  // (A/B builds may set another)
 #endif
-constexpr int kSegShift = VRPMS_SEG_SHIFT;  // heterogeneous fleets: shifts |delta| <= 6 from tables
+constexpr int kSegShift = VRPMS_SEG_SHIFT;  // heterogeneous fleets: shifts |delta| <= 8 from tables
 
 struct SegArgs {
   SearchInst si;
