@@ -140,10 +140,12 @@ int vrpms_eval_path(vrpms_ctx* ctx, int32_t perm_bytes, int64_t ld, const void* 
 /*   VRPMS_OPT_SA_ROUTE: 0 = auto (static symmetric matrix, every demand
  *   fitting the smallest vehicle: every move priced from per-position prefix
  *   sums, sa_seg_kernel -- one capacity, or per-vehicle capacities with each
- *   route tracked on its vehicle; otherwise windowed SA on an exchangeable
+ *   route tracked on its vehicle; hour-indexed matrix (H = 24): full walks
+ *   whose durations come from 24-hour edge rows cached per tour position in
+ *   LDS, sa_td_kernel, any fleet; otherwise windowed SA on an exchangeable
  *   fleet prices moves by route-local walks, sa_route_kernel), 2 = force full
- *   re-evaluation of every move (sa_kernel), 3 = force the route-local walks;
- *   A/B. */
+ *   re-evaluation of every move (sa_kernel), 3 = force the route-local walks,
+ *   4 = force the hour-row walks; A/B. */
 #define VRPMS_OPT_SA_ROUTE 8
 /*   VRPMS_OPT_ROUTE_WG_PER_CU: workgroups of sa_route_kernel per CU (0 =
  *   auto: 1 for multi-wavefront chains, whose LDS request is padded past

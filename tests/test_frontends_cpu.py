@@ -124,3 +124,123 @@ def test_pool_raises_when_an_owner_dies():
             pool.post_many("tsp", "sa", [_body(i, N) for i in range(4)])
     finally:
         pool.close()
+
+
+def test_http_pool_over_sockets_matches_the_handler_contract():
+    """listen mode: the workers serve HTTP on one port (SO_REUSEPORT); a
+    load-generator process pair holds 64 keep-alive connections and sends
+    every request; the answers, the GET banners, the VRP GA preflight, an
+    error body, a saved solution and an unbatched endpoint all follow the
+    reference handler's contract (service.endpoint_handler)."""
+    import http.client
+    N, R = 12, 300
+    store = _store(R, N)
+    counts = mp.get_context("fork").Array("l", 1)
+    path = list(range(1, N)) + [0]
+    with frontends.FrontEndPool(store, workers=3, devices=(0,), slots_per_worker=64, nmax=16,
+                                chunk=16, launch_factory=_stand_in(counts),
+                                app_factory=_fake_app(store), listen=("127.0.0.1", 0)) as pool:
+        out = frontends.loadgen("127.0.0.1", pool.port, R, N, connections=64, procs=2, sample=R)
+        c = http.client.HTTPConnection("127.0.0.1", pool.port, timeout=30)
+        c.request("GET", "/api/vrp/ga")
+        r = c.getresponse()
+        banner = (r.status, r.read())
+        c.request("GET", "/api")
+        r = c.getresponse()
+        hello = (r.status, r.read())
+        c.request("OPTIONS", "/api/vrp/ga")
+        r = c.getresponse()
+        pre = (r.status, r.getheader("Access-Control-Allow-Origin"), r.read())
+        c.request("POST", "/api/tsp/sa", body=json.dumps({"durationsKey": 1}))
+        r = c.getresponse()
+        err = (r.status, r.read())
+        c.request("POST", "/api/tsp/sa", body=_body(8, N, auth="tok"))
+        r = c.getresponse()
+        saved = (r.status, json.loads(r.read()))
+        c.request("POST", "/api/tsp/ga", body=_body(3, N))   # unbatched: an owner's App.post
+        r = c.getresponse()
+        ga = (r.status, json.loads(r.read()))
+        c.request("GET", "/nowhere")
+        r = c.getresponse()
+        missing = r.status
+        r.read()
+        c.close()
+    assert out["requests"] == R and out["ok"] == R and out["errors"] == 0
+    assert len(out["sample"]) == R
+    for i, (st, text) in out["sample"].items():
+        body = json.loads(text)
+        D = np.asarray(store.durations[i])
+        assert st == 200 and body["message"]["vehicle"] == [0] + path
+        assert body["message"]["duration"] == int(D[[0] + path[:-1], path].sum())
+        assert text == json.dumps(body)          # the handler's encoding of that result
+    assert banner == (200, b"Hi, this is the VRP Genetic Algorithm endpoint")
+    assert hello == (200, b"Hello!") and missing == 404
+    assert pre[0] == 200 and pre[1] == "*"
+    want = _fake_app(store)(0).post("tsp", "sa", json.dumps({"durationsKey": 1}).encode())
+    assert err == (400, json.dumps(want[1]).encode())
+    assert saved[0] == 200 and len(store.solutions) == 1
+    assert store.solutions[0]["duration"] == saved[1]["message"]["duration"]
+    assert ga[0] == 200 and ga[1]["message"]["vehicle"][0] == 0
+    assert counts[0] == R + 1
+
+
+def test_pool_unbatched_post_does_not_block_batches():
+    """A slow unbatched request (another endpoint) runs on the owner's post
+    thread: batched TSP SA answers keep arriving meanwhile."""
+    import http.client
+    import threading
+    import time
+    N = 10
+    store = _store(64, N)
+    counts = mp.get_context("fork").Array("l", 1)
+
+    def slow_app(st):
+        def factory(dev):
+            def solve(problem, algorithm, params, knobs, locations, durations):
+                time.sleep(6.0)
+                return {"duration": 0, "vehicle": [0, 0]}
+            return service.App(st, device=dev, solve=solve)
+        return factory
+
+    with frontends.FrontEndPool(store, workers=2, devices=(0,), slots_per_worker=64, nmax=16,
+                                chunk=8, launch_factory=_stand_in(counts),
+                                app_factory=slow_app(store), listen=("127.0.0.1", 0)) as pool:
+        slow = {}
+
+        def post_slow():
+            c = http.client.HTTPConnection("127.0.0.1", pool.port, timeout=30)
+            c.request("POST", "/api/tsp/ga", body=_body(1, N))
+            r = c.getresponse()
+            slow["r"] = (r.status, r.read(), time.perf_counter())
+            c.close()
+
+        th = threading.Thread(target=post_slow)
+        th.start()
+        time.sleep(0.3)
+        out = frontends.loadgen("127.0.0.1", pool.port, 64, N, connections=8, procs=1, sample=0)
+        t_done = time.perf_counter()
+        th.join()
+    assert out["ok"] == 64
+    assert t_done < slow["r"][2], "batched answers waited for the slow request"
+    assert slow["r"][0] == 200
+
+
+def test_pool_refuses_calls_after_a_death():
+    """post_many after a failure raises at once (the pool is marked broken)."""
+    import os
+
+    def factory(dev):
+        def launch(N, host):
+            os._exit(3)
+        return launch
+    N = 8
+    store = _store(4, N)
+    pool = frontends.FrontEndPool(store, workers=1, devices=(0,), slots_per_worker=8, nmax=16,
+                                  chunk=4, launch_factory=factory, app_factory=_fake_app(store))
+    try:
+        with pytest.raises(RuntimeError, match="exited"):
+            pool.post_many("tsp", "sa", [_body(i, N) for i in range(4)])
+        with pytest.raises(RuntimeError, match="broken"):
+            pool.post_many("tsp", "sa", [_body(0, N)])
+    finally:
+        pool.close()

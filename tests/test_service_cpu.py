@@ -271,18 +271,28 @@ def test_remote_front_end_over_http(monkeypatch):
                              random_permutation_count=10, iteration_count=5)
         assert v["durationSum"] == 21
         assert seen[-1][3] == {"random_permutationCount": 10, "iteration_count": 5, "seed": 0,
-                               "objective": "sum"}
+                               "objective": "sum", "inline": {}}
         assert seen[-1][2]["ignored_customers"] == [2]
         # objective, seed and time limit travel with the instance
         solver.solve_vrp("sa", MATRIX, locs, [5, 5], [0, 30], [], [], seed=3, objective="max",
                          time_limit=2.5)
         assert seen[-1][3] == {"random_permutationCount": None, "iteration_count": None,
-                               "seed": 3, "time_limit": 2.5, "objective": "max"}
+                               "seed": 3, "time_limit": 2.5, "objective": "max", "inline": {}}
         solver.solve_tsp("sa", MATRIX, [1, 2, 3], 0, 0, seed=5)
-        assert seen[-1][3] == {"seed": 5}
-        # a knob the box would not honour is refused, not dropped
-        with pytest.raises(ValueError, match="unsupported"):
-            solver.solve_vrp("sa", MATRIX, locs, [5, 5], [0, 30], [], [], chains=64)
+        assert seen[-1][3] == {"seed": 5, "inline": {}}
+        # the search knobs a local call takes travel too (the same
+        # call is accepted with or without a local GPU)
+        solver.solve_vrp("sa", MATRIX, locs, [5, 5], [0, 30], [], [], chains=64, window=8)
+        assert seen[-1][3]["inline"] == {"chains": 64, "window": 8}
+        solver.solve_tsp("ga", MATRIX, [1, 2, 3], 0, 0, pop=32, islands=2)
+        assert seen[-1][3]["inline"] == {"pop": 32, "islands": 2}
+        # an argument no solver takes is refused, not dropped
+        with pytest.raises(ValueError, match="unknown"):
+            solver.solve_vrp("sa", MATRIX, locs, [5, 5], [0, 30], [], [], chainz=64)
+        st, body = service.App(store(), solve=fake_solve).solve_inline(
+            "tsp", "sa", json.dumps({"durations": MATRIX, "customers": [1], "startNode": 0,
+                                     "startTime": 0, "knobs": {"bogus": 1}}).encode())
+        assert st == 400 and "unknown knob" in body["errors"][0]["reason"]
         p = solver.solve_vrp_problem(MATRIX, locs, [5, 5], [0, 30], [2], [])
         assert p["tour"] == [0, 1, 3, 0] and p["total_time"] == 21 and p["unvisited"] == []
         with pytest.raises(ValueError, match="Invalid request"):
@@ -335,3 +345,41 @@ def test_multi_device_scheduling_and_batcher_round_robin():
         assert st == 200
     assert [d for d, _ in launched] == [0, 1, 0, 1]
     assert app.batcher.per_device == {0: 2, 1: 2}
+
+
+def test_repeated_device_list_does_not_deadlock():
+    """devices=[0, 0] (one GPU standing in for two, as the GPU island test
+    does): a large request takes the island path and returns instead of
+    blocking on the second acquire of device 0's lock."""
+    seen = []
+
+    def fake_solve(problem, algorithm, params, knobs, locations, durations):
+        seen.append(knobs.get("devices"))
+        return {"duration": 1, "vehicle": [0, 1, 0]}
+
+    app = service.App(store(), devices=[0, 0], solve=fake_solve, island_min_n=2)
+    big = dict(FULL["tsp"], customers=[1, 2, 3])
+    out = {}
+    th = threading.Thread(target=lambda: out.setdefault("r", app.post("tsp", "ga",
+                                                                      json.dumps(big).encode())))
+    th.start()
+    th.join(10)
+    assert not th.is_alive(), "island request deadlocked on a repeated device"
+    assert out["r"][0] == 200 and seen == [[0, 0]]
+    assert all(not lk.locked() for lk in app.locks.values())
+
+
+@pytest.mark.parametrize("mt,want", [(True, [0, 1]), (False, None)])
+def test_multithreaded_selects_island_model(mt, want):
+    """VRP GA's multiThreaded (api/parameters.py:20): true runs the island
+    model over every device, false one device -- whatever the request size
+    (island_min_n is far above this 3-customer request)."""
+    seen = []
+
+    def fake_solve(problem, algorithm, params, knobs, locations, durations):
+        seen.append(knobs.get("devices"))
+        return {"durationMax": 0, "durationSum": 0, "vehicles": []}
+
+    app = service.App(store(), devices=[0, 1], solve=fake_solve, island_min_n=1000)
+    st, _ = app.post("vrp", "ga", json.dumps(dict(FULL["vrp"], multiThreaded=mt)).encode())
+    assert st == 200 and seen == [want]

@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libvrpms.so")
 SOURCES = ["capi.hip", "eval.hip", "eval_staged.hip", "eval_words.hip", "search.hip", "probe.hip",
-           "pool.hip", "ga_fused.hip", "sa_seg.hip"]
+           "pool.hip", "ga_fused.hip", "sa_seg.hip", "sa_td.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950",
          "-ffp-contract=off", "-Wall", "-Werror"]

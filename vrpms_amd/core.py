@@ -173,9 +173,10 @@ class Context:
         check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_WORDS_KERNEL, int(gen)))
 
     def set_sa_route(self, mode: int):
-        """0 = auto (O(1) segment pricing on static symmetric instances, else
-        route-local walks for windowed SA), 2 = full re-evaluation, 3 = force
-        the route-local walks."""
+        """0 = auto (O(1) segment pricing on static symmetric instances,
+        hour-row walks on hour-indexed ones, else route-local walks for
+        windowed SA), 2 = full re-evaluation (sa_kernel), 3 = force the
+        route-local walks, 4 = force the hour-row walks (sa_td_kernel)."""
         check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_SA_ROUTE, int(mode)))
 
     def set_route_wg_per_cu(self, wg: int):

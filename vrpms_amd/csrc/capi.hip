@@ -27,22 +27,37 @@ int hip_fail(hipError_t e, const char* what) {
 }
 
 // stats layout: 0 min_dur 1 max_dur 2 min_dem 3 max_dem 4 min_cap 5 max_cap
-//               6 min_start 7 max_start 8 asymmetric (slice 0)
+//               6 min_start 7 max_start 8 asymmetric (slice 0) 9 asymmetric (any slice)
 __global__ void stats_init_kernel(int32_t* s) {
   if (threadIdx.x < 8) s[threadIdx.x] = (threadIdx.x & 1) ? INT_MIN : INT_MAX;
-  if (threadIdx.x == 8) s[8] = 0;
+  if (threadIdx.x == 8 || threadIdx.x == 9) s[threadIdx.x] = 0;
 }
 
-// s[8] |= any D[a][b] != D[b][a] in hour slice 0 (selects the O(1) 2-opt delta).
-__global__ void asym_kernel(const int32_t* __restrict__ D, int N, int32_t* s) {
-  const int64_t total = (int64_t)N * N;
-  int asym = 0;
+// s[8] |= any D[a][b] != D[b][a] in hour slice 0 (selects the O(1) 2-opt
+// delta); s[9] |= the same in any slice (sa_td_kernel's reverse rows).
+__global__ void asym_kernel(const int32_t* __restrict__ D, int N, int H, int32_t* s) {
+  const int64_t NN = (int64_t)N * N, total = NN * H;
+  int asym0 = 0, asym = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t a = i / N, b = i - a * N;
-    asym |= D[i] != D[b * N + a];
+    const int64_t h = i / NN, e = i - h * NN, a = e / N, b = e - a * N;
+    const bool x = D[i] != D[h * NN + b * N + a];
+    asym |= x;
+    asym0 |= x && h == 0;
   }
-  if (__any(asym) && (threadIdx.x & 63) == 0) atomicOr(s + 8, 1);
+  if (__any(asym0) && (threadIdx.x & 63) == 0) atomicOr(s + 8, 1);
+  if (__any(asym) && (threadIdx.x & 63) == 0) atomicOr(s + 9, 1);
+}
+
+// [H][N][N] -> [N][N][H] (H = 24): the 24 hourly durations of an edge in one
+// 48-byte row, which sa_td_kernel caches per tour position.
+__global__ void hour_minor_kernel(const uint16_t* __restrict__ in, int64_t NN, int H,
+                                  uint16_t* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < NN * H;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i / H, h = i - e * H;
+    out[i] = in[h * NN + e];
+  }
 }
 
 __device__ __forceinline__ void block_minmax_commit(int vmin, int vmax, int32_t* smin,
@@ -152,6 +167,7 @@ static int bits_for(int v) {
 static void free_instance(Instance& in) {
   (void)hipFree(in.mat32);
   (void)hipFree(in.mat16);
+  (void)hipFree(in.mat16h);
   (void)hipFree(in.pack64);
   (void)hipFree(in.pack64p);
   (void)hipFree(in.pack64w);
@@ -230,9 +246,10 @@ int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value) {
     return VRPMS_OK;
   }
   if (option == VRPMS_OPT_SA_ROUTE) {
-    if (value != 0 && value != 2 && value != 3)
+    if (value != 0 && value != 2 && value != 3 && value != 4)
       return fail(VRPMS_EINVAL,
-                  "vrpms_set_option: SA route must be 0 (auto), 2 (full walks) or 3 (route walks)");
+                  "vrpms_set_option: SA route must be 0 (auto), 2 (full walks), 3 (route walks) "
+                  "or 4 (hour-row walks)");
     ctx->opt_sa_route = value;
     return VRPMS_OK;
   }
@@ -338,9 +355,9 @@ int vrpms_set_instance(vrpms_ctx* ctx, int32_t problem, const int32_t* d_dur, in
                                     problem == VRPMS_CVRP ? in.cap : nullptr, in.start, K,
                                     ctx->d_stats);
   VRPMS_HIP(hipGetLastError());
-  asym_kernel<<<grid, 256, 0, s>>>(in.mat32, N, ctx->d_stats);
+  asym_kernel<<<grid, 256, 0, s>>>(in.mat32, N, H, ctx->d_stats);
   VRPMS_HIP(hipGetLastError());
-  int32_t st[9];
+  int32_t st[10];
   std::vector<int32_t> caps(K);
   VRPMS_HIP(hipMemcpyAsync(st, ctx->d_stats, sizeof(st), hipMemcpyDeviceToHost, s));
   VRPMS_HIP(hipMemcpyAsync(caps.data(), in.cap, (size_t)K * 4, hipMemcpyDeviceToHost, s));
@@ -359,6 +376,7 @@ int vrpms_set_instance(vrpms_ctx* ctx, int32_t problem, const int32_t* d_dur, in
   in.max_start = st[7];
   in.min_start = st[6];
   in.symmetric = st[8] == 0;
+  in.sym_all = st[9] == 0;
   in.cap0 = caps[0];
   in.uniform_cap = std::all_of(caps.begin(), caps.end(), [&](int32_t c) { return c == caps[0]; });
   const long double bound = (long double)in.max_start + (long double)(N + K + 1) * in.max_dur;
@@ -373,6 +391,12 @@ int vrpms_set_instance(vrpms_ctx* ctx, int32_t problem, const int32_t* d_dur, in
     VRPMS_HIP(hipMalloc(&in.mat16, total * 2));
     to_u16_kernel<<<grid, 256, 0, s>>>(in.mat32, in.mat16, total);
     VRPMS_HIP(hipGetLastError());
+    // hour-minor rows for the hour-indexed SA walks (bounded: 48 bytes per edge)
+    if (H == 24 && total * 2 <= ((int64_t)1 << 30)) {
+      VRPMS_HIP(hipMalloc(&in.mat16h, total * 2));
+      hour_minor_kernel<<<grid, 256, 0, s>>>(in.mat16, (int64_t)N * N, H, in.mat16h);
+      VRPMS_HIP(hipGetLastError());
+    }
   }
   const size_t elem = in.use16 ? 2 : 4;
   in.tier = (size_t)total * elem <= 64 * 1024 ? kTierLds : kTierGlobal;

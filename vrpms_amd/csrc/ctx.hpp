@@ -21,10 +21,12 @@ struct Instance {
   int max_dur = 0, max_dem = 0, min_dem = 0, max_start = 0, min_start = 0, min_cap = 0, max_cap = 0;
   bool uniform_cap = true;
   bool symmetric = false;      // hour slice 0 is symmetric (O(1) 2-opt delta for static TSP)
+  bool sym_all = false;        // every hour slice is symmetric (sa_td_kernel: no reverse rows)
   int cap0 = 0;
   // device copies owned by the context
   int32_t* mat32 = nullptr;    // [H][N][N]
   uint16_t* mat16 = nullptr;   // [H][N][N] when max_dur <= 65535
+  uint16_t* mat16h = nullptr;  // [N][N][24] hour-minor copy (H = 24, u16; sa_td_kernel rows)
   uint64_t* pack64 = nullptr;  // [N][N] packed static CVRP layout (tier 0)
   int32_t* dem = nullptr;      // [N]
   int32_t* cap = nullptr;      // [K]
@@ -55,7 +57,7 @@ struct vrpms_ctx {
   int opt_words_lookahead = 0;  // VRPMS_OPT_WORDS_LOOKAHEAD (words2 gather lookahead, A/B)
   int opt_words_kernel = 0;     // VRPMS_OPT_WORDS_KERNEL (0 auto = words2/rows2, 1 = first generation)
   int opt_ga_fused = 0;          // VRPMS_OPT_GA_FUSED (0 auto, 2 = force the three-kernel GA)
-  int opt_sa_route = 0;         // VRPMS_OPT_SA_ROUTE (0 auto, 2 = force full re-evaluation)
+  int opt_sa_route = 0;         // VRPMS_OPT_SA_ROUTE (0 auto, 2 full re-evaluation, 3 route walks, 4 hour rows)
   int opt_rows_config = 0;      // VRPMS_OPT_ROWS_CONFIG (0 auto, 1..5 force eval_cvrp_rows2's (CW, ILP))
   int32_t* d_stats = nullptr;   // scratch for set_instance validation
   uint64_t* d_scratch = nullptr;  // small reduction scratch

@@ -2305,6 +2305,9 @@ int launch_ga_fused(const vrpms_ctx* ctx, const vrpms_ga_params* p, uint16_t* d_
 int launch_sa_seg(const vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* d_cur,
                   uint64_t* d_cur_key, uint16_t* d_best, uint64_t* d_best_key, int n,
                   uint32_t wtypes, int moves, hipStream_t s);  // sa_seg.hip
+int launch_sa_td(const vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* d_cur,
+                 uint64_t* d_cur_key, uint16_t* d_best, uint64_t* d_best_key, int n,
+                 uint32_t wtypes, int moves, hipStream_t s);  // sa_td.hip
 
 static void ensure_scratch(vrpms_ctx* ctx, size_t bytes, int* err) {
   if (ctx->search_scratch_bytes >= bytes) return;
@@ -2343,6 +2346,14 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
     return fail(VRPMS_EINVAL, "vrpms_sa_run: moves must be 64 * W, W = 1..8");
   const int wpc = moves / 64;
   VRPMS_HIP(hipSetDevice(ctx->device));
+  if (ctx->opt_sa_route == 4) {  // force the hour-row kernel (sa_td.hip)
+    const int rc = launch_sa_td(ctx, p, d_cur, d_cur_key, d_best, d_best_key, n, wtypes, moves,
+                                (hipStream_t)stream);
+    if (rc <= 0) return rc;
+    return fail(VRPMS_EINVAL,
+                "vrpms_sa_run: the hour-row kernel needs H = 24, a u16 matrix, moves <= 256 and "
+                "LDS room for one chain's rows");
+  }
   FastSplit f;
   if (wpc == 1 && ctx->inst.H == 1 && fast_split_params(ctx, n, &f)) {
     const uint32_t tb = ((uint32_t)n + 12u + 15u) & ~15u;
@@ -2366,6 +2377,13 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
   if (ctx->opt_sa_route == 0) {
     const int rc = launch_sa_seg(ctx, p, d_cur, d_cur_key, d_best, d_best_key, n, wtypes, moves,
                                  (hipStream_t)stream);
+    if (rc <= 0) return rc;
+  }
+  // hour-indexed matrices (H = 24): full walks over LDS hour rows, any fleet
+  // (sa_td.hip)
+  if (ctx->opt_sa_route == 0) {
+    const int rc = launch_sa_td(ctx, p, d_cur, d_cur_key, d_best, d_best_key, n, wtypes, moves,
+                                (hipStream_t)stream);
     if (rc <= 0) return rc;
   }
   SaArgs a{search_inst(ctx), p->chains, n, p->steps, p->window, wtypes, p->inv_t0, p->inv_alpha,

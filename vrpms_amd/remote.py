@@ -41,20 +41,27 @@ def _post(base: str, problem: str, algorithm: str, body: dict, timeout: float) -
     return out["message"]
 
 
-# knobs the GPU box's /solve route honours (App.solve_inline); anything else
-# would be silently ignored there, so it is refused here instead
+# knobs with a request name of their own (api/parameters.py:21-22); every
+# other search knob of solver.solve_tsp / solve_vrp (chains, pop, islands, ...)
+# travels in "knobs" and the GPU box's /solve route applies the same set
+# (service.INLINE_KNOBS), so a call behaves the same with or without a local GPU
 _FORWARDED = {"random_permutation_count": "randomPermutationCount",
               "iteration_count": "iterationCount"}
 
 
 def _options(body: dict, seed, time_limit, knobs: dict, objective=None):
-    extra = sorted(k for k in knobs if k not in _FORWARDED)
+    from .service import INLINE_KNOBS
+    extra = sorted(k for k in knobs if k not in _FORWARDED and k not in INLINE_KNOBS)
     if extra:
-        raise ValueError(f"remote solve: unsupported argument(s) {extra} "
-                         f"(forwarded: seed, time_limit, objective, {sorted(_FORWARDED)})")
+        raise ValueError(f"remote solve: unknown argument(s) {extra} "
+                         f"(known: seed, time_limit, objective, "
+                         f"{sorted(set(_FORWARDED) | set(INLINE_KNOBS))})")
     for k, name in _FORWARDED.items():
         if knobs.get(k):
             body[name] = int(knobs[k])
+    more = {k: knobs[k] for k in INLINE_KNOBS if knobs.get(k) is not None}
+    if more:
+        body["knobs"] = more
     body["seed"] = int(seed)
     if time_limit is not None:
         body["timeLimit"] = float(time_limit)

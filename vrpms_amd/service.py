@@ -45,6 +45,10 @@ _COMMON = {
             ("locationsKey", "locations_key"), ("durationsKey", "durations_key"),
             ("customers", "customers"), ("startNode", "start_node"), ("startTime", "start_time")],
 }
+# search knobs of solver.solve_tsp / solve_vrp that the /solve route accepts
+# in its "knobs" object (vrpms_amd.remote forwards them): name -> type
+INLINE_KNOBS = {"steps": int, "separators": int, "window": int, "chains": int,
+                "window_types": int, "pop": int, "islands": int, "colonies": int, "ants": int}
 # algorithm knobs (api/parameters.py:18-23; every other algorithm takes none)
 _KNOBS = {("vrp", "ga"): [("multiThreaded", "multi_threaded"),
                           ("randomPermutationCount", "random_permutationCount"),
@@ -295,7 +299,11 @@ class App:
     its own context and lock; a request takes the first free device (one
     request per device at a time), and a large SA / GA / ACO request (more
     than `island_min_n` customers) with two or more devices takes them all
-    and runs as an island model across them (solver.search_islands)."""
+    and runs as an island model across them (solver.search_islands).  The
+    VRP GA endpoint's `multiThreaded` (api/parameters.py:20, the reference's
+    only parallelism knob) decides that for its request instead: true runs
+    the island model over every device, false one device.  A device listed
+    twice (one GPU standing in for two) is locked once."""
 
     def __init__(self, store, device: int = 0, seed: int = 0, max_seconds: float | None = None,
                  solve=None, batch_tsp: bool = False, batch_window_s: float = 0.005,
@@ -323,14 +331,17 @@ class App:
         n = len(params.get("customers") or []) if problem == "tsp" else \
             max(0, len(locations or []) - 1)
         knobs = dict(knobs)
-        if len(self.devices) > 1 and algorithm != "bf" and n > self.island_min_n:
-            for d in self.devices:
+        mt = knobs.get("multi_threaded")
+        islands = n > self.island_min_n if mt is None else bool(mt)
+        if len(self.devices) > 1 and algorithm != "bf" and islands:
+            held = sorted(set(self.devices))   # each lock once, in one global order
+            for d in held:
                 self.locks[d].acquire()
             try:
                 knobs["devices"] = list(self.devices)
                 return self._solve(problem, algorithm, params, knobs, locations, durations)
             finally:
-                for d in reversed(self.devices):
+                for d in reversed(held):
                     self.locks[d].release()
         with self._rr_lock:
             start = self._rr
@@ -363,11 +374,11 @@ class App:
         tl = knobs.get("time_limit", self.max_seconds)
         devs = knobs.get("devices") or [knobs.get("device", self.device)]
         dv = dict(device=devs[0], devices=devs if len(devs) > 1 else None)
+        extra = dict(knobs.get("inline") or {})
         if problem == "tsp":
             return solver.solve_tsp(algorithm, durations, params["customers"],
                                     params["start_node"], params["start_time"] or 0,
-                                    seed=seed, time_limit=tl, **dv)
-        extra = {}
+                                    seed=seed, time_limit=tl, **dv, **extra)
         if knobs.get("random_permutationCount"):
             extra["random_permutation_count"] = int(knobs["random_permutationCount"])
         if knobs.get("iteration_count"):
@@ -471,6 +482,13 @@ class App:
                 if content["objective"] not in ("sum", "max"):
                     raise ValueError("objective must be 'sum' or 'max'")
                 knobs["objective"] = content["objective"]
+            inline = content.get("knobs") or {}
+            if not isinstance(inline, dict):
+                raise ValueError("knobs must be a JSON object")
+            bad = sorted(k for k in inline if k not in INLINE_KNOBS)
+            if bad:
+                raise ValueError(f"unknown knob(s) {bad}; known: {sorted(INLINE_KNOBS)}")
+            knobs["inline"] = {k: INLINE_KNOBS[k](v) for k, v in inline.items()}
         except (TypeError, ValueError) as e:
             return 400, {"success": False,
                          "errors": [{"what": "Invalid request", "reason": str(e)}]}
@@ -584,9 +602,30 @@ def main(argv=None):
                     help="coalesce concurrent /api/tsp/sa requests into one launch")
     ap.add_argument("--batch-window-ms", type=float, default=5.0)
     ap.add_argument("--batch-steps", type=int, default=2000)
+    ap.add_argument("--workers", type=int, default=0,
+                    help="throughput mode (BASELINE cfg 5): W front-end processes listen on "
+                         "--port together (SO_REUSEPORT) and feed one GPU-owner process per "
+                         "device (vrpms_amd.frontends.FrontEndPool); /api/tsp/sa requests are "
+                         "batched into tsp_batch_sa launches")
     args = ap.parse_args(argv)
     store = MemoryStore.from_json(args.data) if args.data else MemoryStore()
     devices = [int(x) for x in args.devices.split(",")] if args.devices else None
+    if devices:   # a GPU listed twice would only queue behind itself
+        devices = list(dict.fromkeys(devices))
+    if args.workers > 0:
+        from .frontends import FrontEndPool
+        pool = FrontEndPool(store, workers=args.workers, devices=devices or [args.device],
+                            steps=args.batch_steps, seed=args.seed,
+                            window_s=args.batch_window_ms * 1e-3, listen=(args.host, args.port))
+        print(f"vrpms_amd service ({args.workers} front-end processes) on "
+              f"http://{args.host}:{pool.port}/api", flush=True)
+        try:
+            pool.serve_forever()
+        except KeyboardInterrupt:
+            pass
+        finally:
+            pool.close()
+        return
     app = App(store, device=args.device, seed=args.seed, max_seconds=args.max_seconds,
               batch_tsp=args.batch_tsp, batch_window_s=args.batch_window_ms * 1e-3,
               batch_steps=args.batch_steps, devices=devices)
