@@ -40,6 +40,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "candidate route evals/sec (1/2/4/8 GPU) + best-cost gap at fixed wall time"
+# TD-200 equal-time cells (sa_td_kernel): chains, moves per step, migrated elites, final
+# temperature per typical edge (tools/td_quality_scan.py)
+TD_SHAPE = (1024, 64, 128, 0.004)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 
 
@@ -66,8 +69,13 @@ def parse():
                          "host leg repeated for the run-to-run spread; 0 disables)")
     ap.add_argument("--x1000-seeds", type=int, nargs="+", default=[0, 1, 2])
     ap.add_argument("--td-quality-seconds", type=float, default=10.0,
-                    help="wall time per side for the cfg-3 TD-200 x 24 best-cost gap (seed 0; "
-                         "0 disables)")
+                    help="wall time per side for the cfg-3 TD-200 x 24 best-cost gaps: the "
+                         "uniform fleet (seed 0) and the reference's normal request -- three "
+                         "capacity classes, staggered start times (seeds --het-seeds); 0 disables")
+    ap.add_argument("--het-seeds", type=int, nargs="+", default=[0, 1, 2])
+    ap.add_argument("--host-repeats", type=int, default=2,
+                    help="extra runs of X-1000 seed 0's better host leg: the host's run-to-run "
+                         "spread over 1 + this many runs")
     return ap.parse_args()
 
 
@@ -412,7 +420,7 @@ def _rescore(ctx, tour):
 
 
 def equal_time_cells(ctx, seconds, dist, with_cpu, instance="x1000", seeds=(0, 1, 2),
-                     cpu_moves=(32, 64), repeat_host=True):
+                     cpu_moves=(32, 64), repeat_host=True, host_repeats=2):
     """The metric's second half, several seeds: per seed the GPU
     leg (x1000: sa_seg_kernel; tdvrp200: sa_route_kernel -- 256 chains x 128
     moves per step, W = 2 wavefronts per chain) against the host port
@@ -427,7 +435,8 @@ def equal_time_cells(ctx, seconds, dist, with_cpu, instance="x1000", seeds=(0, 1
     from vrpms_amd import synth
     from vrpms_amd.core import CVRP
     make = {"x1000": lambda sd: synth.x_style(1000, seed=sd),
-            "tdvrp200": lambda sd: synth.td_cvrp(200, 16, seed=sd)}[instance]
+            "tdvrp200": lambda sd: synth.td_cvrp(200, 16, seed=sd),
+            "tdvrp200_het": lambda sd: synth.td_cvrp_het(200, 16, seed=sd)}[instance]
     # GPU shapes from tools/migration_scan.py (10 s, seeds 0-2): X-1000 at 1024
     # chains x 128 moves (W = 2: two wavefronts per SIMD, sa_seg_kernel's OCC = 2
     # variant), a migration every epoch of 80 with the 256 best replacing the
@@ -437,10 +446,12 @@ def equal_time_cells(ctx, seconds, dist, with_cpu, instance="x1000", seeds=(0, 1
     # schedules): each leg at the one that scored best for it on average --
     # X-1000: (t0, t_end) = (0.5, 0.004) x the typical edge for the GPU, (0.5,
     # 0.002) for the host; TD-200: (0.5, 0.004) and (1.0, 0.002)
+    # TD-200 (uniform and heterogeneous fleets) on sa_td_kernel, round 5: shape
+    # and final temperature from tools/td_quality_scan.py
     kw = dict(chains=1024, moves=128, window=32, window_types=2, start="pack", epochs=80,
               mig_E=256, tend_frac=0.004, cpu_tend_frac=0.002) if instance == "x1000" else \
-        dict(chains=256, moves=128, window=32, window_types=2, start="pack", mig_E=128,
-             tend_frac=0.004, cpu_t0_frac=1.0, cpu_tend_frac=0.002)
+        dict(chains=TD_SHAPE[0], moves=TD_SHAPE[1], window=32, window_types=2, start="pack",
+             mig_E=TD_SHAPE[2], tend_frac=TD_SHAPE[3], cpu_t0_frac=1.0, cpu_tend_frac=0.002)
     cells = []
     spread = None
     for sd in seeds:
@@ -457,14 +468,22 @@ def equal_time_cells(ctx, seconds, dist, with_cpu, instance="x1000", seeds=(0, 1
                                  "steps_per_chain": c["steps_per_chain"]} for c in legs]
             cell["gap"] = _gap(q["gpu"], best)
             if repeat_host and spread is None:
-                again = quality(ctx, x, seconds, 1, 0, dist, with_cpu=True, gpu=False,
-                                cpu_moves=best["moves_per_step"], **kw)["cpu"]
-                a, b = best["duration_sum"], again["duration_sum"]
-                spread = {"seed": sd, "moves_per_step": best["moves_per_step"],
-                          "runs": [a, b], "rel": abs(a - b) / min(a, b)}
+                runs = [best["duration_sum"]]
+                for _ in range(max(1, host_repeats)):
+                    runs.append(quality(ctx, x, seconds, 1, 0, dist, with_cpu=True, gpu=False,
+                                        cpu_moves=best["moves_per_step"], **kw)["cpu"]
+                                ["duration_sum"])
+                spread = {"seed": sd, "moves_per_step": best["moves_per_step"], "runs": runs,
+                          "min": min(runs), "max": max(runs),
+                          "rel": (max(runs) - min(runs)) / min(runs)}
         cells.append(cell)
     out = {"instance": instance, "T_s": seconds, "seeds": list(seeds),
-           "gpu_shape": f"{kw['chains']} chains x {kw['moves']} moves per step (W = 2)",
+           "fleet": {"capacities": [int(c) for c in make(seeds[0]).capacities],
+                     "start_times": [int(t) for t in make(seeds[0]).start_times]}
+           if instance == "tdvrp200_het" else "uniform",
+           "gpu_kernel": "sa_seg_kernel" if instance == "x1000" else "sa_td_kernel",
+           "gpu_shape": f"{kw['chains']} chains x {kw['moves']} moves per step "
+                        f"(W = {kw['moves'] // 64})",
            "host": f"oracle_sa_run_resync, better of {list(cpu_moves)} moves per step",
            "window": 32, "window_types": 2, "start": "pack", "cells": cells,
            "gap_sign": "negative = GPU better"}
@@ -477,6 +496,39 @@ def equal_time_cells(ctx, seconds, dist, with_cpu, instance="x1000", seeds=(0, 1
         if gaps:
             out["median_beyond_spread"] = out["gap_median"] < -spread["rel"]
     return out
+
+
+def quality_summary(out):
+    """Every equal-time cell as [gpu, host, gap %] (durationSum, gap negative
+    = GPU better), the medians and the host's run-to-run spread."""
+    def r(x, nd=2):
+        return None if x is None else round(100.0 * x, nd)
+    s = {}
+    q = out.get("quality") or {}
+    if "gpu" in q and "cpu" in q:
+        s["cfg2_sa"] = [q["gpu"]["duration_sum"], q["cpu"]["duration_sum"], r(q.get("gap"))]
+        for name, v in (q.get("by_algorithm") or {}).items():
+            s[f"cfg2_{name}"] = [v.get("duration_sum"), q["cpu"]["duration_sum"],
+                                 r(v.get("gap_vs_host_sa"))]
+    for key, tag in (("quality_x1000", "x1000"), ("quality_tdvrp200", "td200"),
+                     ("quality_tdvrp200_het", "td200het")):
+        c = out.get(key) or {}
+        for cell in c.get("cells", []):
+            if "cpu" in cell:
+                s[f"{tag}_s{cell['seed']}"] = [cell["gpu"]["duration_sum"],
+                                               cell["cpu"]["duration_sum"], r(cell.get("gap"))]
+        if "gap_median" in c:
+            s[f"{tag}_median"] = r(c["gap_median"])
+            s[f"{tag}_gpu_better"] = c.get("gpu_better")
+        sp = c.get("host_run_to_run")
+        if sp:
+            s[f"{tag}_host_spread"] = {"runs": sp["runs"], "min": sp["min"], "max": sp["max"],
+                                       "rel_pct": r(sp["rel"])}
+            s[f"{tag}_median_beyond_spread"] = c.get("median_beyond_spread")
+        if "error" in c:
+            s[f"{tag}_error"] = c["error"][-200:]
+    s["units"] = "[gpu, host, gap %] durationSum at equal wall time; gap < 0 = GPU better"
+    return s
 
 
 def other_configs(ctx, torch, dev, seed=0, r_lds=None):
@@ -543,6 +595,10 @@ def other_configs(ctx, torch, dev, seed=0, r_lds=None):
                                            "frac": mev * 8 / r_lds if r_lds else None}}
     del mats
     try:
+        out["cfg5_http"] = cfg5_http_leg(R=R, steps=steps)
+    except Exception:
+        out["cfg5_http"] = {"error": traceback.format_exc(limit=3)}
+    try:
         out["cfg5_api"] = cfg5_api_pool_leg(R=R, steps=steps)
     except Exception:
         out["cfg5_api"] = {"error": traceback.format_exc(limit=3)}
@@ -566,6 +622,27 @@ def cfg5_api_pool_leg(R=10000, steps=1000):
     workers = max(2, threads - 2)        # the parent and the GPU owner keep a core each
     cmd = [sys.executable, "-m", "vrpms_amd.frontends", "bench", "--requests", str(R),
            "--workers", str(workers), "--steps", str(steps)]
+    res = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    if res.returncode != 0:
+        return {"error": f"exit {res.returncode}", "stderr": res.stderr[-2000:]}
+    out = json.loads(res.stdout.strip().splitlines()[-1])
+    out["host_cores"] = cores
+    return out
+
+
+def cfg5_http_leg(R=10000, steps=1000, connections=1024):
+    """Config 5 over real sockets (BASELINE cfg 5: 10k concurrent TSP-50
+    requests): FrontEndPool workers listen on one port (SO_REUSEPORT) and a
+    load generator in separate client processes holds `connections`
+    keep-alive connections sending R POST /api/tsp/sa; requests/s at the
+    client.  Runs as a child program (this process has initialised the GPU)."""
+    import subprocess
+    threads, cores = host_cores()
+    clients = max(1, min(4, threads // 4))
+    workers = max(2, threads - clients - 2)   # the pool's parent and GPU owner keep a core each
+    cmd = [sys.executable, "-m", "vrpms_amd.frontends", "bench-http", "--requests", str(R),
+           "--workers", str(workers), "--steps", str(steps), "--clients", str(clients),
+           "--connections", str(connections)]
     res = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
     if res.returncode != 0:
         return {"error": f"exit {res.returncode}", "stderr": res.stderr[-2000:]}
@@ -923,9 +1000,10 @@ def main():
         try:
             xq = equal_time_cells(ctx, args.x1000_quality_seconds, dist,
                                   with_cpu=(rank == 0 and not args.no_cpu_baseline),
-                                  seeds=tuple(args.x1000_seeds))
+                                  seeds=tuple(args.x1000_seeds), host_repeats=args.host_repeats)
         except Exception:
             xq = {"error": traceback.format_exc(limit=3)}
+    hetq = None
     if args.td_quality_seconds > 0 and world == 1:
         try:
             tdq = equal_time_cells(ctx, args.td_quality_seconds, dist,
@@ -933,6 +1011,13 @@ def main():
                                    instance="tdvrp200", seeds=(0,), repeat_host=False)
         except Exception:
             tdq = {"error": traceback.format_exc(limit=3)}
+        try:
+            hetq = equal_time_cells(ctx, args.td_quality_seconds, dist,
+                                    with_cpu=(rank == 0 and not args.no_cpu_baseline),
+                                    instance="tdvrp200_het", seeds=tuple(args.het_seeds),
+                                    repeat_host=False)
+        except Exception:
+            hetq = {"error": traceback.format_exc(limit=3)}
 
     isl = None
     if args.island_epochs > 0:
@@ -998,6 +1083,8 @@ def main():
             out["quality_x1000"] = xq
         if tdq is not None:
             out["quality_tdvrp200"] = tdq
+        if hetq is not None:
+            out["quality_tdvrp200_het"] = hetq
         if isl is not None:
             out["islands"] = isl
         if world == 1 and not args.no_cpu_baseline:
@@ -1019,6 +1106,9 @@ def main():
                 out["cfg1_main_py"] = cfg1_leg()
             except Exception:
                 out["cfg1_main_py"] = {"error": traceback.format_exc(limit=3)}
+        # last key: every equal-time cell in a few hundred bytes, so a
+        # truncated record still holds them
+        out["quality_summary"] = quality_summary(out)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

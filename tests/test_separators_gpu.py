@@ -333,10 +333,15 @@ def test_sa_moves_validation(ctx):
         ctx.sa_run(cur, ck, cur.clone(), bk, 2, 0.01, 1.0, 1, 0, window=4, moves=100)
     with pytest.raises(RuntimeError):   # more than 8 wavefronts
         ctx.sa_run(cur, ck, cur.clone(), bk, 2, 0.01, 1.0, 1, 0, window=4, moves=576)
-    td = synth.td_cvrp(30, 4, seed=1)    # hour-indexed: no segment pricing
-    load(ctx, td)
+    asym = _asym(synth.cvrp(30, 4, seed=1), 3)   # static asymmetric: no segment pricing
+    load(ctx, asym)
     with pytest.raises(RuntimeError):   # window 0: not the route-local kernel
         ctx.sa_run(cur, ck, cur.clone(), bk, 2, 0.01, 1.0, 1, 0, window=0, moves=128)
+    td = synth.td_cvrp(30, 4, seed=1)    # hour-indexed: the hour-row kernel takes any window
+    load(ctx, td)
+    ctx.sa_run(cur, ck, cur.clone(), bk, 2, 0.01, 1.0, 1, 0, window=0, moves=128)
+    with pytest.raises(RuntimeError):   # and at most 4 wavefronts (then the route kernel,
+        ctx.sa_run(cur, ck, cur.clone(), bk, 2, 0.01, 1.0, 1, 0, window=0, moves=320)  # window 0)
 
 
 def test_route_local_sa_small_matches_python_oracle(ctx):

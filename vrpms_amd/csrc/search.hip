@@ -546,6 +546,9 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
       const int R = __builtin_amdgcn_readfirstlane(r);
       wave_sync();
       if (R > RMAX) return -1;
+      // route starts past the last route read a fixed value (the tour's end),
+      // never what the LDS held before (a stale start was a bug)
+      for (int x = R + 1 + lane; x < RM; x += 64) T.rs[x] = (uint16_t)n;
       derive(R);
       build_bits();
       return R;
@@ -615,6 +618,7 @@ __global__ __launch_bounds__(512) void sa_route_kernel(SaArgs a) {
       if (to < n) T.rid[to] = (uint8_t)r;
     }
     if (lane == 0) T.rs[R] = (uint16_t)n;
+    for (int x = R + 1 + lane; x < RM; x += 64) T.rs[x] = (uint16_t)n;
     wave_sync();
     derive(R);
     build_bits();
@@ -2113,6 +2117,19 @@ VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, unsigned cha
   }
   wave_sync();
   auto dist = [&](uint32_t x, uint32_t y) { return (int)D[__umul24(x, (uint32_t)N) + y]; };
+  // symmetric matrix: the current tour's edges E[q] = D(A[q-1], A[q]), q = 0..n
+  // (the depot at both ends), kept with the tour -- a move's removed edges
+  // are tour edges at positions i, i+1, j, j+1, so they are read from E
+  // (a few dwords, no bank conflicts) and only its added edges are random
+  // matrix gathers; E is rebuilt on an accept
+  const uint32_t epad = npad + 8u;
+  MatT* E = reinterpret_cast<MatT*>(work + 4 * 3 * npad * 2 + 4 * 8) + wave * epad;
+  auto build_E = [&]() {
+    for (int q = lane; q <= n; q += 64)
+      E[q] = (MatT)dist(q ? (uint32_t)A[q - 1] : 0u, q < n ? (uint32_t)A[q] : 0u);
+    wave_sync();
+  };
+  if constexpr (symmetric) build_E();
   auto full = [&](const uint16_t* T) {
     int s = 0;
     uint32_t prev = 0;
@@ -2131,7 +2148,7 @@ VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, unsigned cha
     const Move m = decode_move1(xm, n);
     auto tourA = [&](int q) { return (uint32_t)A[q]; };
     int delta;
-    if constexpr (symmetric) delta = tsp_move_delta_sym(dist, tourA, n, m);
+    if constexpr (symmetric) delta = tsp_move_delta_sym_cached(dist, tourA, [&](int q) { return (int)E[q]; }, n, m);
     else delta = tsp_move_delta(dist, tourA, n, m, false);
     const int nd = dur + delta;
     uint64_t k;
@@ -2160,6 +2177,7 @@ VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, unsigned cha
       uint16_t* t = A;
       A = B;
       B = t;
+      if constexpr (symmetric) build_E();
       ck = k;
       if (ck < bk) {
         bk = ck;
@@ -2660,7 +2678,9 @@ extern "C" int vrpms_tsp_batch_sa(vrpms_ctx* ctx, const int32_t* d_mats, int32_t
   if (!d_mats || !d_best_tours || !d_best_keys)
     return fail(VRPMS_EINVAL, "vrpms_tsp_batch_sa: NULL buffer");
   const size_t npad = ((size_t)N - 1 + 7) & ~(size_t)7;
-  const size_t lds = (((size_t)N * N * 4 + 15) & ~(size_t)15) + 4 * 3 * npad * 2 + 4 * 8;
+  // matrix, 4 chains x (current / next / best tour), their best keys, their edge caches E
+  const size_t lds = (((size_t)N * N * 4 + 15) & ~(size_t)15) + 4 * 3 * npad * 2 + 4 * 8 +
+                     4 * (npad + 8) * 4;
   if (lds > ctx->max_lds) return fail(VRPMS_EINVAL, "vrpms_tsp_batch_sa: request too large for LDS");
   VRPMS_HIP(hipSetDevice(ctx->device));
   TspBatchArgs a{d_mats, R, N, p->steps, p->inv_t0, p->inv_alpha, (uint32_t)p->seed,

@@ -293,6 +293,36 @@ VRPMS_DEV int tsp_move_delta_sym(const Dist& d, const Tour& T, int n, const Move
   return d(a0, b0) + d(a1, b1) + d(a2, b2) + d(a3, b3) - d(c0, e0) - d(c1, e1) - d(c2, e2) - d(c3, e3);
 }
 
+// tsp_move_delta_sym with the removed edges read from the current tour's edge
+// cache: Ec(q) = d(T[q-1], T[q]) for q = 0..n (the depot at both ends).  Every
+// removed edge is a tour edge at position i, i+1, j or j+1, so only the added
+// edges are matrix gathers; the pads of the gather form are masked out on
+// both sides.  Same integer result as tsp_move_delta.
+template <typename Dist, typename Tour, typename EdgeAt>
+VRPMS_DEV int tsp_move_delta_sym_cached(const Dist& d, const Tour& T, const EdgeAt& Ec, int n,
+                                        const Move& m) {
+  auto at = [&](int q) -> uint32_t { return (uint32_t)q < (uint32_t)n ? (uint32_t)T(q) : 0u; };
+  const int i = m.i, j = m.j;
+  const uint32_t im1 = at(i - 1), pi = at(i), ip1 = at(i + 1);
+  const uint32_t jm1 = at(j - 1), pj = at(j), jp1 = at(j + 1);
+  const bool swp = m.typ == kMoveSwap, opt = m.typ == kMove2Opt, rel = m.typ == kMoveRelocate;
+  const bool adj = swp && j == i + 1, lo = rel && i < j, hi = rel && i > j;
+  const bool full = swp && !adj;
+  // added edges as in tsp_move_delta_sym (slots 2 / 3 are pads for 2-opt / all but a full swap)
+  const uint32_t a0 = hi ? jm1 : im1, b0 = lo ? ip1 : (hi ? pi : pj);
+  const uint32_t a1 = opt ? pi : (lo ? pj : (hi ? pi : pj));
+  const uint32_t b1 = opt ? jp1 : (lo ? pi : (hi ? pj : (adj ? pi : ip1)));
+  const uint32_t a2 = hi ? im1 : (swp && !adj ? jm1 : pi);
+  const uint32_t b2 = hi ? ip1 : (swp && !adj ? pi : jp1);
+  const int g0 = d(a0, b0), g1 = d(a1, b1), g2 = d(a2, b2), g3 = d(pi, jp1);
+  const int plus = g0 + g1 + (opt ? 0 : g2) + (full ? g3 : 0);
+  // removed edges: swap i, i+1, j, j+1 (adjacent: i, i+1, j+1); 2-opt i, j+1;
+  // relocate i<j: i, i+1, j+1; relocate i>j: j, i, i+1
+  const int ei = Ec(i), ei1 = Ec(i + 1), ej = Ec(j), ej1 = Ec(j + 1);
+  const int minus = ei + (opt ? 0 : ei1) + (full || hi ? ej : 0) + (swp || opt || lo ? ej1 : 0);
+  return plus - minus;
+}
+
 // ---------------------------------------------------------------------------
 // Deterministic SA acceptance threshold: floor(2^24 * exp(-dp * invT)) using
 // only IEEE fp32 multiply/add/sub (built with -ffp-contract=off) and exact

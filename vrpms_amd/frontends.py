@@ -533,14 +533,16 @@ def _http_worker_main(w, arena, lo, hi, host, port, submit_qs, done_q, store, ba
             conn.respond(status, body, close=close)
         if rows:
             saved_q.put(rows)
-        flush()                 # slots came free
+        loop.call_soon(flush)   # slots came free (not re-entrantly: start() may finish a job)
 
     fe = _FrontEnd(w, arena, lo, hi, submit_qs, store, batchable_nmax, deliver)
 
     def flush(force=False):
         timer["h"] = None
         for key in list(pending):
-            items = pending[key]
+            items = pending.get(key)
+            if items is None:
+                continue
             while items:
                 take = items[:chunk]
                 if len(take) < chunk and not force:
@@ -553,7 +555,7 @@ def _http_worker_main(w, arena, lo, hi, host, port, submit_qs, done_q, store, ba
                 conns[jid] = [(c, cl) for _, c, cl in take]
                 fe.start((jid, key[0], key[1], [b for b, _, _ in take]))
             if not items:
-                del pending[key]
+                pending.pop(key, None)
         if pending and timer["h"] is None:
             timer["h"] = loop.call_later(window_s, flush, True)
 

@@ -102,6 +102,21 @@ def td_cvrp(n: int = 200, K: int = 16, seed: int = 0, start: int = 480) -> Insta
                     np.full(K, start, dtype=np.int64), "cvrp", {"xy": xy})
 
 
+def td_cvrp_het(n: int = 200, K: int = 16, seed: int = 0, fracs=(1.3, 1.0, 0.8),
+                start: int = 420) -> Instance:
+    """The reference's normal VRP request on cfg 3's matrix: td_cvrp's 24
+    hourly matrices with per-vehicle capacities (len(fracs) classes of
+    frac x the uniform capacity, in vehicle order, each at least the largest
+    demand; api/parameters.py:11) and staggered start times start + 37 k mod
+    240 (api/parameters.py:12)."""
+    x = td_cvrp(n, K, seed)
+    base = int(x.capacities[0])
+    caps = np.array([max(int(base * fracs[k * len(fracs) // K]), int(x.demand.max()))
+                     for k in range(K)], dtype=np.int64)
+    starts = np.arange(K, dtype=np.int64) * 37 % 240 + start
+    return Instance(f"tdvrp{n}_het", x.durations, x.demand, caps, starts, "cvrp", x.meta)
+
+
 def x_style(n: int = 1000, seed: int = 0, r: float = 12.0) -> Instance:
     """Cfg 4: Uchoa et al. (2017) X-style generator -- central depot,
     random-clustered customer positions, unitary-to-large demands, route
