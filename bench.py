@@ -39,6 +39,15 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+_T0 = time.perf_counter()
+
+
+def progress(msg):
+    """A progress line on stderr (stdout carries only the JSON line): a long
+    run keeps showing it is alive."""
+    print(f"[bench {time.perf_counter() - _T0:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 METRIC = "candidate route evals/sec (1/2/4/8 GPU) + best-cost gap at fixed wall time"
 # TD-200 equal-time cells (sa_td_kernel): chains, moves per step, migrated elites, final
 # temperature per typical edge (tools/td_quality_scan.py)
@@ -455,12 +464,14 @@ def equal_time_cells(ctx, seconds, dist, with_cpu, instance="x1000", seeds=(0, 1
     cells = []
     spread = None
     for sd in seeds:
+        progress(f"{instance} seed {sd}")
         x = make(sd)
         ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
         q = quality(ctx, x, seconds, 1, 0, dist, with_cpu=False, label=f"{instance} seed {sd}",
                     **kw)
         cell = {"seed": sd, "gpu": q["gpu"]}
         if with_cpu:
+            progress(f"{instance} seed {sd}: host legs")
             best, legs = _host_best(ctx, x, seconds, dist, kw, cpu_moves)
             cell["cpu"] = best
             cell["cpu_legs"] = [{"moves_per_step": c["moves_per_step"],
@@ -971,6 +982,7 @@ def main():
             wall = float(t.item())
         return wall, ev0.elapsed_time(ev1) / steps
 
+    progress("headline: eval_cvrp_words2")
     wall, kernel_ms = timed(lambda: ctx.eval_words(words, n, out=keys), args.steps, args.warmup,
                             world > 1)
     value = C * args.steps * world / wall
@@ -983,6 +995,7 @@ def main():
     # the gloo tests, tests/test_islands_cpu.py).
     if args.quality_seconds > 0 and world == 1:
         try:
+            progress("cfg-2 equal-time SA / GA / ACO")
             qual = quality(ctx, inst, args.quality_seconds, world, rank, dist,
                            with_cpu=(rank == 0 and not args.no_cpu_baseline))
             by = algo_quality(ctx, inst, args.quality_seconds)
@@ -998,6 +1011,7 @@ def main():
     xq = tdq = None
     if args.x1000_quality_seconds > 0 and world == 1:
         try:
+            progress("X-1000 equal-time cells")
             xq = equal_time_cells(ctx, args.x1000_quality_seconds, dist,
                                   with_cpu=(rank == 0 and not args.no_cpu_baseline),
                                   seeds=tuple(args.x1000_seeds), host_repeats=args.host_repeats)
@@ -1006,12 +1020,14 @@ def main():
     hetq = None
     if args.td_quality_seconds > 0 and world == 1:
         try:
+            progress("TD-200 equal-time cells")
             tdq = equal_time_cells(ctx, args.td_quality_seconds, dist,
                                    with_cpu=(rank == 0 and not args.no_cpu_baseline),
                                    instance="tdvrp200", seeds=(0,), repeat_host=False)
         except Exception:
             tdq = {"error": traceback.format_exc(limit=3)}
         try:
+            progress("heterogeneous TD-200 equal-time cells")
             hetq = equal_time_cells(ctx, args.td_quality_seconds, dist,
                                     with_cpu=(rank == 0 and not args.no_cpu_baseline),
                                     instance="tdvrp200_het", seeds=tuple(args.het_seeds),
@@ -1022,6 +1038,7 @@ def main():
     isl = None
     if args.island_epochs > 0:
         # after every other device use of the matrix instance: it loads its own
+        progress("island leg")
         isl = island_leg(ctx, torch, dev, world, rank, dist, epochs=args.island_epochs,
                          steps=args.island_steps)
 
@@ -1088,6 +1105,7 @@ def main():
         if isl is not None:
             out["islands"] = isl
         if world == 1 and not args.no_cpu_baseline:
+            progress("cpu baseline")
             cb, ref, S = cpu_baseline(inst, perms, args.cpu_seconds)
             got = keys[:S].cpu().numpy().view(np.uint64)
             cb["parity_on_sample"] = bool((got == ref[0]).all())
@@ -1095,10 +1113,12 @@ def main():
         if world == 1 and not args.no_other_configs:
             del perms, words
             try:   # secondary lines must never cost the headline line
+                progress("other configs (cfg 3-5, API legs)")
                 out["other_configs"] = other_configs(ctx, torch, dev, r_lds=r_gather)
             except Exception:
                 out["other_configs"] = {"error": traceback.format_exc(limit=3)}
             try:
+                progress("search lines")
                 out["search"] = search_lines(ctx, torch, dev, r_gather)
             except Exception:
                 out["search"] = {"error": traceback.format_exc(limit=3)}

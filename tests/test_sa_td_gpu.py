@@ -178,3 +178,37 @@ def test_td_rows_sa_forced_rejects_static(ctx):
     P = synth.random_perms(4, inst.n, seed=1, dtype=np.uint16)
     with pytest.raises(RuntimeError):
         run(ctx, P, 2, 0.01, 1.0, 1, 0, 0, 0, 64, 4)
+
+
+def test_td_rows_sa_large_instance_falls_back(ctx, coracle):
+    """TD-1000 x 24: the depot-leg rows alone (96 KB) and one chain's rows do
+    not fit the LDS -- option 4 is refused, the automatic dispatch takes the
+    full-walk L2 kernel, and the trajectory still equals the C restatement."""
+    inst = synth.td_cvrp(1000, 50, seed=35)
+    load(ctx, inst)
+    P = starts(ctx, inst, "pack", 2)
+    with pytest.raises(RuntimeError):
+        run(ctx, P, 3, 1 / 200.0, 1 / 0.99, 5, 0, 32, 2, 64, 4)
+    got = run(ctx, P, 3, 1 / 200.0, 1 / 0.99, 5, 0, 32, 2, 64, 0)
+    ccur, cbest = P.copy(), P.copy()
+    cbk = np.full(2, 2**64 - 1, dtype=np.uint64)
+    cck = coracle.sa_run(inst.durations, ccur, cbest, cbk, 3, 1 / 200.0, 1 / 0.99, 5, 0,
+                         inst.demand, inst.capacities, inst.start_times, window=32,
+                         window_types=2)
+    assert (got[0] == ccur).all() and got[1] == [int(x) for x in cck]
+
+
+def test_td_rows_sa_mid_size_fits(ctx, coracle):
+    """TD-600 x 24 (n + separators ~ 640 tokens): still one chain per
+    workgroup in the LDS, trajectory equal to the C restatement."""
+    inst = _starts(_classes(synth.td_cvrp(600, 40, seed=36), (1.2, 1.0)))
+    load(ctx, inst)
+    P = starts(ctx, inst, "pack", 4)
+    got = run(ctx, P, 20, 1 / 200.0, 1 / 0.99, 5, 0, 32, 2, 64, 4)
+    ccur, cbest = P.copy(), P.copy()
+    cbk = np.full(4, 2**64 - 1, dtype=np.uint64)
+    cck = coracle.sa_run(inst.durations, ccur, cbest, cbk, 20, 1 / 200.0, 1 / 0.99, 5, 0,
+                         inst.demand, inst.capacities, inst.start_times, window=32,
+                         window_types=2)
+    assert (got[0] == ccur).all() and got[1] == [int(x) for x in cck]
+    assert got[3] == [int(x) for x in cbk]

@@ -383,3 +383,29 @@ def test_multithreaded_selects_island_model(mt, want):
     app = service.App(store(), devices=[0, 1], solve=fake_solve, island_min_n=1000)
     st, _ = app.post("vrp", "ga", json.dumps(dict(FULL["vrp"], multiThreaded=mt)).encode())
     assert st == 200 and seen == [want]
+
+
+def test_bench_quality_summary_collects_every_cell():
+    """bench.quality_summary: [gpu, host, gap %] per cell, medians and the
+    host spread, from a bench record (CPU: a synthetic record)."""
+    import importlib.util
+    spec_ = importlib.util.spec_from_file_location(
+        "bench_mod", os.path.join(os.path.dirname(os.path.dirname(__file__)), "bench.py"))
+    bench = importlib.util.module_from_spec(spec_)
+    spec_.loader.exec_module(bench)
+    cell = lambda sd, g, c: {"seed": sd, "gpu": {"duration_sum": g}, "cpu": {"duration_sum": c},  # noqa: E731
+                             "gap": (g - c) / c}
+    out = {"quality": {"gpu": {"duration_sum": 100}, "cpu": {"duration_sum": 101}, "gap": -1 / 101,
+                       "by_algorithm": {"ga": {"duration_sum": 102, "gap_vs_host_sa": 1 / 101}}},
+           "quality_x1000": {"cells": [cell(0, 99, 100), cell(1, 98, 100)], "gap_median": -0.015,
+                             "gpu_better": "2 / 2",
+                             "host_run_to_run": {"runs": [100, 101, 100], "min": 100, "max": 101,
+                                                 "rel": 0.01},
+                             "median_beyond_spread": True},
+           "quality_tdvrp200_het": {"cells": [cell(0, 95, 100)], "gap_median": -0.05}}
+    s = bench.quality_summary(out)
+    assert s["cfg2_sa"] == [100, 101, -0.99] and s["cfg2_ga"][2] == 0.99
+    assert s["x1000_s0"] == [99, 100, -1.0] and s["x1000_median"] == -1.5
+    assert s["x1000_host_spread"]["min"] == 100 and s["x1000_median_beyond_spread"] is True
+    assert s["td200het_s0"] == [95, 100, -5.0]
+    assert list(out) != [] and "units" in s

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """sa_seg_kernel alone on cfg 4 (X-1000, K - 1 separators, first-fit
 starts, windowed 2-opt + swap / relocate anywhere) -- a short target for
-rocprofv3 --pmc / --stats passes.  usage: seg_run.py [chains] [moves] [steps]   (SEG_LIB=<path>: another libvrpms.so)"""
+rocprofv3 --pmc / --stats passes.  usage: seg_run.py [chains] [moves] [steps]   (SEG_LIB=<path>: another libvrpms.so;
+SEG_HET=1: three capacity classes)"""
 import os
 import sys
 
@@ -19,7 +20,13 @@ if os.environ.get("SEG_LIB"):  # an A/B build of the library
     _lib.load(os.environ["SEG_LIB"])
 ctx = Context(0)
 x = synth.x_style(1000, seed=0)
-ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
+caps = x.capacities
+if os.environ.get("SEG_HET"):  # three capacity classes (the heterogeneous variant)
+    import numpy as np
+    K, base = len(caps), int(caps[0])
+    fr = (1.4, 1.1, 0.9)
+    caps = np.array([max(int(base * fr[k * 3 // K]), int(x.demand.max())) for k in range(K)])
+ctx.set_instance(CVRP, x.durations, x.demand, caps, x.start_times)
 r = runners.SARunner(ctx, x.n, chains=chains, total_steps=2 * steps, durations=x.durations,
                      n_sep=x.K - 1, window=32, window_types=2, start="pack", moves=moves)
 r.epoch(steps)

@@ -2093,13 +2093,17 @@ struct TspBatchArgs {
 template <typename MatT, bool symmetric, bool small>
 VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, unsigned char* work) {
   const int N = a.N, n = N - 1, r = blockIdx.x;
-  const uint32_t npad = ((uint32_t)n + 7u) & ~7u;
+  // each tour buffer holds the depot (0) at positions -1 and n, so a move's
+  // six tour reads need no bounds test
+  const uint32_t npad = ((uint32_t)n + 2u + 7u) & ~7u;
   const int wave = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
   uint16_t* buf = reinterpret_cast<uint16_t*>(work) + wave * 3 * npad;
   uint64_t* wbest = reinterpret_cast<uint64_t*>(work + 4 * 3 * npad * 2);
-  uint16_t* A = buf;
-  uint16_t* B = buf + npad;
-  uint16_t* Best = buf + 2 * npad;
+  for (uint32_t q = lane; q < 3 * npad; q += 64) buf[q] = 0;
+  wave_sync();
+  uint16_t* A = buf + 1;
+  uint16_t* B = buf + npad + 1;
+  uint16_t* Best = buf + 2 * npad + 1;
   const uint32_t cid = (uint32_t)(r * 4 + wave);
   // Philox Fisher-Yates start: for i = n-1..1 swap t[i], t[x % (i+1)].  The
   // draws have wave-uniform counters (the scalar unit computes them); lane 0
@@ -2148,7 +2152,8 @@ VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, unsigned cha
     const Move m = decode_move1(xm, n);
     auto tourA = [&](int q) { return (uint32_t)A[q]; };
     int delta;
-    if constexpr (symmetric) delta = tsp_move_delta_sym_cached(dist, tourA, [&](int q) { return (int)E[q]; }, n, m);
+    if constexpr (symmetric)
+      delta = tsp_move_delta_sym_cached<true>(dist, tourA, [&](int q) { return (int)E[q]; }, n, m);
     else delta = tsp_move_delta(dist, tourA, n, m, false);
     const int nd = dur + delta;
     uint64_t k;
@@ -2164,7 +2169,7 @@ VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, unsigned cha
     if (!accept) {
       const uint64_t d = (k >> 28) - (ck >> 28);
       const uint32_t dp = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
-      accept = (xa >> 8) < accept_threshold(dp, invT);
+      accept = accept_test(dp, invT, xa >> 8);
     }
     if (accept) {  // bl is wave-uniform: the winner's move by v_readlane
       Move mb;
@@ -2677,7 +2682,7 @@ extern "C" int vrpms_tsp_batch_sa(vrpms_ctx* ctx, const int32_t* d_mats, int32_t
   if (R == 0) return VRPMS_OK;
   if (!d_mats || !d_best_tours || !d_best_keys)
     return fail(VRPMS_EINVAL, "vrpms_tsp_batch_sa: NULL buffer");
-  const size_t npad = ((size_t)N - 1 + 7) & ~(size_t)7;
+  const size_t npad = ((size_t)N - 1 + 2 + 7) & ~(size_t)7;   // tours padded with the depot
   // matrix, 4 chains x (current / next / best tour), their best keys, their edge caches E
   const size_t lds = (((size_t)N * N * 4 + 15) & ~(size_t)15) + 4 * 3 * npad * 2 + 4 * 8 +
                      4 * (npad + 8) * 4;

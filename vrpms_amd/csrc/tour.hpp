@@ -298,10 +298,14 @@ VRPMS_DEV int tsp_move_delta_sym(const Dist& d, const Tour& T, int n, const Move
 // removed edge is a tour edge at position i, i+1, j or j+1, so only the added
 // edges are matrix gathers; the pads of the gather form are masked out on
 // both sides.  Same integer result as tsp_move_delta.
-template <typename Dist, typename Tour, typename EdgeAt>
+// PADDED: T(-1) and T(n) read the depot (0) themselves.
+template <bool PADDED = false, typename Dist, typename Tour, typename EdgeAt>
 VRPMS_DEV int tsp_move_delta_sym_cached(const Dist& d, const Tour& T, const EdgeAt& Ec, int n,
                                         const Move& m) {
-  auto at = [&](int q) -> uint32_t { return (uint32_t)q < (uint32_t)n ? (uint32_t)T(q) : 0u; };
+  auto at = [&](int q) -> uint32_t {
+    if constexpr (PADDED) return (uint32_t)T(q);
+    else return (uint32_t)q < (uint32_t)n ? (uint32_t)T(q) : 0u;
+  };
   const int i = m.i, j = m.j;
   const uint32_t im1 = at(i - 1), pi = at(i), ip1 = at(i + 1);
   const uint32_t jm1 = at(j - 1), pj = at(j), jp1 = at(j + 1);
@@ -353,6 +357,21 @@ VRPMS_DEV uint32_t accept_threshold(uint32_t dp, float invT) {
   const int k = (int)kf;                      // 0..23
   const float scaled = p * (float)(1u << (24 - k));  // exact power-of-two scaling
   return (uint32_t)scaled;                    // truncation
+}
+
+// u < accept_threshold(dp, invT) for a wave-uniform draw u < 2^24, with an
+// exact early answer before the polynomial: the polynomial p never exceeds
+// 1.0f (1 - a non-negative product), so the threshold is at most 2^(24 - k),
+// k = floor(dp invT log2 e), and a draw at or above that bound is rejected
+// without evaluating it (at a cold temperature, almost every uphill move).
+VRPMS_DEV bool accept_test(uint32_t dp, float invT, uint32_t u) {
+  if (dp == 0) return u < (1u << 24);
+  const float x = (float)dp * invT;
+  const float y = x * 0x1.715476p+0f;
+  if (!(y < 24.0f)) return false;
+  const int k = __builtin_amdgcn_readfirstlane((int)floorf(y));
+  if (u >= (1u << (24 - k))) return false;
+  return u < accept_threshold(dp, invT);
 }
 
 }  // namespace vrpms
