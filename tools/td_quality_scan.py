@@ -19,6 +19,7 @@ from vrpms_amd.core import CVRP, Context  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--het", action="store_true")
+ap.add_argument("--x1000", action="store_true", help="X-1000 (sa_seg_kernel) instead of TD-200")
 ap.add_argument("--T", type=float, default=10.0)
 ap.add_argument("--seeds", type=int, nargs="+", default=[0])
 ap.add_argument("--cpu", action="store_true")
@@ -27,14 +28,16 @@ ap.add_argument("--tend", type=float, nargs="+", default=[0.004])
 args = ap.parse_args()
 ctx = Context(0)
 for sd in args.seeds:
-    x = synth.td_cvrp_het(200, 16, seed=sd) if args.het else synth.td_cvrp(200, 16, seed=sd)
+    x = synth.x_style(1000, seed=sd) if args.x1000 else (
+        synth.td_cvrp_het(200, 16, seed=sd) if args.het else synth.td_cvrp(200, 16, seed=sd))
     ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
     for shape in args.shapes.split(","):
         chains, moves = (int(v) for v in shape.split("x"))
         for te in args.tend:
             q = bench.quality(ctx, x, args.T, 1, 0, torch.distributed, with_cpu=False,
                               chains=chains, moves=moves, window=32, window_types=2,
-                              start="pack", mig_E=max(1, chains // 8), tend_frac=te)
+                              start="pack", mig_E=max(1, chains // 4 if args.x1000 else chains // 8),
+                              tend_frac=te, epochs=80 if args.x1000 else 40)
             g = q["gpu"]
             print(json.dumps({"seed": sd, "het": args.het, "chains": chains, "moves": moves,
                               "t_end": te, "duration_sum": g["duration_sum"],
