@@ -438,6 +438,9 @@ GA_FUSED_CASES = [
     (1, 1, 1.0, 2, 4, 3, 0.5),
     (2, 2, 1.0, 2, 6, 4, 0.5),
     (19, 2, 1.0, 2, 1000, 3, 0.2),
+    # three 64-position slots per lane (the span bitmask's widest case that
+    # fits the packed matrix in LDS)
+    (130, 10, 1.05, 2, 32, 4, 0.5),
 ]
 
 

@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 # GA_PROF_TAG=x: build_ab/gaprof_x (A/B); GA_PROF_SRC=<file>: that ga_fused.hip
 # instead of the tree's (e.g. an older revision written out by git show)
 TAG = os.environ.get("GA_PROF_TAG", "")
-LIB = os.path.join(ROOT, "build_ab", "gaprof" + (f"_{TAG}" if TAG else ""), "libvrpms.so")
+LIB = os.path.join(ROOT, os.environ.get("AB_DIR", "build_ab"), "gaprof" + (f"_{TAG}" if TAG else ""), "libvrpms.so")
 
 
 def build():
@@ -49,16 +49,20 @@ def run():
                               pmut=pmut)
         ga.epoch()
         torch.cuda.synchronize()
-        buf = (ctypes.c_ulonglong * (4 * 4096))()
-        lib.vrpms_debug_ga_prof(buf, 4 * 4096, 1)
+        buf = (ctypes.c_ulonglong * (5 * 4096))()
+        lib.vrpms_debug_ga_prof(buf, 5 * 4096, 1)
         ga.epoch()
         torch.cuda.synchronize()
-        lib.vrpms_debug_ga_prof(buf, 4 * 4096, 1)
+        lib.vrpms_debug_ga_prof(buf, 5 * 4096, 1)
         a = np.array(buf[:4 * islands], dtype=np.float64).reshape(islands, 4) / 20
+        redo = np.array(buf[4 * 4096:4 * 4096 + islands], dtype=np.float64) / 20
         names = ["breed", "score", "sort", "survivors"]
         print(json.dumps({"islands": islands, "pop": pop, "pmut": pmut,
                           "ticks_per_generation": dict(zip(names, a.mean(0).round(1).tolist())),
-                          "us_per_generation": round(a.mean(0).sum() / 100.0, 2)}), flush=True)
+                          "us_per_generation": round(a.mean(0).sum() / 100.0, 2),
+                          "exact_rewalks_per_generation": {"mean": round(redo.mean(), 2),
+                                                           "islands_with_any": int((redo > 0).sum())}}),
+              flush=True)
         del ga
 
 

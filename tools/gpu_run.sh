@@ -56,6 +56,8 @@ for step in "$@"; do
       S="python3 $ROOT/tools/search_run.py 3"
       run pmc_s_sq 300 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
           --output-format csv -d "$OUT/pmc_s_sq" -o run -- $S
+      run pmc_s_sq2 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_SCA \
+          --output-format csv -d "$OUT/pmc_s_sq2" -o run -- $S
       run pmc_s_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/pmc_s_stats" -o run -- $S
       cd "$ROOT" ;;
     pmc_l2)

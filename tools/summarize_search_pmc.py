@@ -32,9 +32,13 @@ def main():
     tag = sys.argv[1]
     note = sys.argv[2] if len(sys.argv) > 2 else ""
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
-    for f in glob.glob(os.path.join(OUT, "pmc_s_sq", "*counter_collection.csv")):
-        for r in csv.DictReader(open(f)):
-            agg[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    # pmc_s_sq2 (round 5): SALU, issue-wait and LDS-active counters
+    for d in ("pmc_s_sq", "pmc_s_sq2"):
+        for f in glob.glob(os.path.join(OUT, d, "*counter_collection.csv")):
+            for r in csv.DictReader(open(f)):
+                name = r["Counter_Name"] + ("" if d == "pmc_s_sq" or r["Counter_Name"] != "SQ_WAVES"
+                                            else "_2")
+                agg[short(r["Kernel_Name"])][name].append(float(r["Counter_Value"]))
     avg_s = {}
     for f in glob.glob(os.path.join(OUT, "pmc_s_stats", "*kernel_stats.csv")):
         for r in csv.DictReader(open(f)):
@@ -57,6 +61,13 @@ def main():
         if m.get("SQ_WAVES"):
             rec["valu_per_wave_step"] = m.get("SQ_INSTS_VALU", 0) / m["SQ_WAVES"] / steps
             rec["lds_per_wave_step"] = m.get("SQ_INSTS_LDS", 0) / m["SQ_WAVES"] / steps
+            if "SQ_INSTS_SALU" in m:
+                rec["salu_per_wave_step"] = m["SQ_INSTS_SALU"] / m["SQ_WAVES"] / steps
+        if m.get("SQ_WAVE_CYCLES") and "SQ_WAIT_INST_ANY" in m:
+            # SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* all count quad-cycles
+            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_ANY"):
+                if c in m:
+                    rec[c.lower()[3:] + "_frac_of_wave_cycles"] = m[c] / m["SQ_WAVE_CYCLES"]
         kernels[k] = rec
     out = {"command": "rocprofv3 --pmc SQ_* / --kernel-trace --stats -- python3 tools/search_run.py 3 "
                       "(tools/gpu_run.sh pmc_search)",
@@ -65,7 +76,12 @@ def main():
     json.dump(out, open(path, "w"), indent=1)
     for k, r in kernels.items():
         print(k, {x: round(r[x], 3) for x in ("valu_per_wave_step", "valu_frac_of_peak",
-                                               "lds_bank_conflict_frac") if r.get(x) is not None})
+                                               "lds_bank_conflict_frac", "salu_per_wave_step",
+                                               "lds_per_wave_step", "wait_any_frac_of_wave_cycles",
+                                               "wait_inst_any_frac_of_wave_cycles",
+                                               "wait_inst_lds_frac_of_wave_cycles",
+                                               "active_inst_any_frac_of_wave_cycles")
+                       if r.get(x) is not None})
 
 
 if __name__ == "__main__":

@@ -99,6 +99,17 @@ VRPMS_DEV uint32_t wave_min_u32_uniform(uint32_t v) {
   return min(min(r0, r1), min(r2, r3));
 }
 
+// Wave64 OR over uint32 with every lane active, returned wave-uniform: the
+// same DPP row reduction as wave_min_u32_uniform, rows combined in SGPRs.
+VRPMS_DEV uint32_t wave_or_u32_uniform(uint32_t v) {
+  v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad [1,0,3,2]
+  v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);   // quad [2,3,0,1]
+  v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) | (uint32_t)__builtin_amdgcn_readlane((int)v, 16) |
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 32) | (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+
 // Lexicographic (key, lane) argmin with every lane active, both wave-uniform:
 // the same DPP row reduction on the 64-bit key (two dword moves per step),
 // the row minima combined in SGPRs, then the lowest lane holding the minimum

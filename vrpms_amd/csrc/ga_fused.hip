@@ -36,9 +36,23 @@
 
 namespace vrpms {
 
+// (mu + lambda) selection: 1 = merge ranks over 64-runs of children,
+// 2 = children sorted first, one lower bound per pair (A/B only: the
+// block sort's LDS stages cost more than the run searches they save, sort
+// phase 4.0 -> 7.0 us at 256 x 256, tools/ga_prof.py)
+#ifndef VRPMS_GA_SEL
+#define VRPMS_GA_SEL 1
+#endif
+// children bred together per wavefront (each on its own stamp array)
+#ifndef VRPMS_GA_NC
+#define VRPMS_GA_NC 2
+#endif
+
 #ifdef VRPMS_GA_PROF
 // phase cycle counters per island (A/B builds only: tools/ga_prof.py)
-__device__ unsigned long long g_ga_prof[4 * 4096];
+// [island][0..3]: phase cycles; [4096 * 4 + island]: children re-walked
+// exactly (met the fleet limit)
+__device__ unsigned long long g_ga_prof[5 * 4096];
 #define GA_T(k)                                                                        \
   do {                                                                                 \
     __syncthreads();                                                                   \
@@ -91,9 +105,10 @@ static GaFusedLayout ga_fused_layout(int N, int n, int P) {
   a.off_crow = (uint32_t)off;   off = al16(off + (size_t)P * 2);
   a.off_sk = (uint32_t)off;     off = al16(off + (size_t)M * 8);
   a.off_si = (uint32_t)off;     off = al16(off + (size_t)M * 4);
-  a.off_used = (uint32_t)off;   off = al16(off + (size_t)32 * N);  // 2 u8 stamp arrays per wave
-  a.off_bits = (uint32_t)off;   off = al16(off + ((size_t)2 * P / 32 + 1) * 4);
-  const size_t runs = (size_t)64 * ((P + 63) / 64);
+  a.off_used = (uint32_t)off;   off = al16(off + (size_t)16 * VRPMS_GA_NC * N);  // u8 stamp arrays
+  a.off_bits = (uint32_t)off;   off = al16(off + (size_t)2 * P);  // u8 row-in-use flags
+  // child runs of merge_select / the sorted children of merge_select_sorted
+  const size_t runs = std::max((size_t)64 * ((P + 63) / 64), (size_t)std::max(64, M / 2));
   a.off_rk = (uint32_t)off;     off = al16(off + runs * 8);
   a.off_ri = (uint32_t)off;     off = al16(off + runs * 4);
   L.bytes = off;
@@ -107,6 +122,8 @@ VRPMS_DEV int tourney2(const uint64_t* keys, int pop, uint32_t r0, uint32_t r1) 
   return (ky < kx || (ky == kx && y < x)) ? y : x;
 }
 
+// H: 64-position slots per lane, ceil(n / 64)
+template <int H>
 __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int P = a.pop, n = a.n, island = blockIdx.x;
@@ -124,7 +141,7 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
   // genes fall in at most 64 distinct dwords -- distinct banks or one
   // address, no bank conflicts; the arrays are cleared before the stamps wrap
   uint8_t* mk = smem + a.off_used + wave * (uint32_t)a.f.N;
-  uint32_t* bits = reinterpret_cast<uint32_t*>(smem + a.off_bits);
+  uint8_t* used = smem + a.off_bits;
   uint16_t* gpop = a.pop_tours + (int64_t)island * P * n;
   uint64_t* gkeys = a.pop_keys + (int64_t)island * P;
 
@@ -142,7 +159,7 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
     pk[i] = gkeys[i];
   }
   auto clear_stamps = [&]() {
-    for (int i = threadIdx.x; i < 8 * a.f.N; i += blockDim.x)  // 32 N bytes
+    for (int i = threadIdx.x; i < 4 * VRPMS_GA_NC * a.f.N; i += blockDim.x)  // 16 NC N bytes
       reinterpret_cast<uint32_t*>(smem + a.off_used)[i] = 0u;
   };
   clear_stamps();
@@ -162,6 +179,14 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
   WordChains<1> ch;
   ch.setup(a.f, smem);
   const int nfull = n >> 2;
+#ifndef VRPMS_GA_SCORE_MINLPW
+#define VRPMS_GA_SCORE_MINLPW 64
+#endif
+  // scoring lanes per wavefront (A/B knob VRPMS_GA_SCORE_MINLPW): 64, so
+  // the first P / 64 wavefronts score -- spreading the children over more
+  // wavefronts (16 or 32 lanes each) measured slower, the walk being
+  // instruction-issue bound (tools/ga_prof.py)
+  const int lpw = min(64, max(VRPMS_GA_SCORE_MINLPW, (P + 15) / 16));
 #ifdef VRPMS_GA_PROF
   unsigned long long t_last = wall_clock64();
 #endif
@@ -182,13 +207,13 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
     {
       const int child = wave + 16 * lane;
       if (child < P) {
-        v_out = crow[child];
+        v_out = (int)((uint32_t)crow[child] * rs);
         const uint32_t cid = (uint32_t)(island * P + child);
         const u32x4 r = philox((uint32_t)gen, (uint32_t)(gen >> 32), cid, 0u, a.seed_lo, a.seed_hi);
         const u32x4 r2 =
             philox((uint32_t)gen, (uint32_t)(gen >> 32), cid, 1u, a.seed_lo, a.seed_hi);
-        v_pa = prow[tourney2(pk, P, r.x, r.y)];
-        v_pb = prow[tourney2(pk, P, r.z, r.w)];
+        v_pa = (int)((uint32_t)prow[tourney2(pk, P, r.x, r.y)] * rs);
+        v_pb = (int)((uint32_t)prow[tourney2(pk, P, r.z, r.w)] * rs);
         if (n >= 2) {
           int lo = (int)(r2.x % (uint32_t)n), hi = (int)(r2.y % (uint32_t)n);
           v_lo = lo < hi ? lo : hi;
@@ -203,121 +228,178 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
         }
       }
     }
-    // Two children of the wave at a time (each with its own stamp array),
-    // their A spans, B reads and stamp lookups issued together: the LDS
-    // round trips of one child hide behind the other's.
+    // Two children of the wave at a time (each with its own stamp array).
+    // Lane L owns positions L + 64h (h < H) of the child: it reads parent
+    // A's gene there and B's gene at OX1 fill index L + 64h (B from position
+    // hi + 1 on, wrapping), both children's reads issued together; then the
+    // span genes are written and stamped, B's genes looked up (a wave's LDS
+    // operations run in order: no wait between the stamps and the lookups)
+    // and compacted by ballot prefix counts.  Fixed H slots, no loops; a
+    // mutation is applied afterwards, in place, to the children that mutate.
+    // (Issuing the next pair's reads before the current pair's writes
+    // measured slower: the breed is issue-bound, not read-latency bound.)
     auto breed = [&](auto nc_tag, int k) __attribute__((always_inline)) {
       constexpr int NC = decltype(nc_tag)::value;
-      const uint8_t* A[NC];
-      const uint8_t* B[NC];
       uint8_t* out[NC];
       uint8_t* m[NC];
-      int lo[NC], hi[NC], mi[NC], mj[NC], rest[NC], filled[NC];
-      bool mut[NC];
-      uint32_t mtyp[NC], stamp[NC];
+      int lo[NC], hi[NC], rest[NC], filled[NC];
+      uint32_t stamp[NC], ga[NC][H], gb[NC][H];
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        A[c] = rows + (uint32_t)wave_bcast(v_pa, k + c) * rs;
-        B[c] = rows + (uint32_t)wave_bcast(v_pb, k + c) * rs;
-        out[c] = rows + (uint32_t)wave_bcast(v_out, k + c) * rs;
-        m[c] = mk + (uint32_t)((k + c) & 1) * 16u * (uint32_t)a.f.N;
+        const uint8_t* A = rows + (uint32_t)wave_bcast(v_pa, k + c);
+        const uint8_t* B = rows + (uint32_t)wave_bcast(v_pb, k + c);
+        out[c] = rows + (uint32_t)wave_bcast(v_out, k + c);
+        m[c] = mk + (uint32_t)((k + c) % VRPMS_GA_NC) * 16u * (uint32_t)a.f.N;
         lo[c] = wave_bcast(v_lo, k + c);
         hi[c] = wave_bcast(v_hi, k + c);
-        // the child's mutation (wave-uniform) folded into its writes: the
-        // gene OX1 puts at position p goes to the position the move maps p
-        // to (the inverse of moved_index), so no copy-and-gather pass follows
-        mut[c] = wave_bcast(v_mut, k + c) != 0;
-        mtyp[c] = (uint32_t)wave_bcast(v_mtyp, k + c);
-        mi[c] = wave_bcast(v_mi, k + c);
-        mj[c] = wave_bcast(v_mj, k + c);
         stamp[c] = 1u + (uint32_t)((g - gclr) * cpw + k + c);
         rest[c] = n - (hi[c] - lo[c] + 1);
         filled[c] = 0;
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          // lanes past the tour read its last position (unused)
+          const int q = min(lane + 64 * h, n - 1);
+          int src = hi[c] + 1 + q;
+          src = src >= n ? src - n : src;
+          ga[c][h] = (uint32_t)A[q];
+          gb[c][h] = (uint32_t)B[src];
+        }
       }
-      auto dst_of = [&](int c, int p) __attribute__((always_inline)) -> int {
-        if (!mut[c]) return p;
-        const int i = mi[c], j = mj[c];
-        if (mtyp[c] == kMoveSwap) return p == i ? j : (p == j ? i : p);
-        if (mtyp[c] == kMove2Opt) return (p >= i && p <= j) ? i + j - p : p;
-        if (i < j) return p == i ? j : ((p > i && p <= j) ? p - 1 : p);
-        return p == i ? j : ((p >= j && p < i) ? p + 1 : p);
-      };
-      // OX1: out[lo..hi] = A[lo..hi]; the rest, from position hi+1
-      // (wrapping), are B's genes from B[hi+1] onwards (wrapping) not yet
-      // used -- a gene is used when its stamp is this child's (no bitmap to
-      // clear)
+      // every read issued here, before the first write (no sinking into the
+      // exec-masked span writes, where each would wait on its own)
 #pragma unroll
       for (int c = 0; c < NC; ++c)
-        for (int q = lo[c] + lane; q <= hi[c]; q += 64) {
-          const uint32_t gq = A[c][q];
-          out[c][dst_of(c, q)] = (uint8_t)gq;
-          m[c][gq] = (uint8_t)stamp[c];
+#pragma unroll
+        for (int h = 0; h < H; ++h) asm volatile("" : "+v"(ga[c][h]), "+v"(gb[c][h]));
+      // OX1: out[lo..hi] = A[lo..hi], those genes stamped; the rest, from
+      // position hi+1 (wrapping), are B's genes from B[hi+1] onwards
+      // (wrapping) whose stamp is not this child's
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          const int q = lane + 64 * h;
+          if (q >= lo[c] && q <= hi[c]) {
+            out[c][q] = (uint8_t)ga[c][h];
+            m[c][ga[c][h]] = (uint8_t)stamp[c];
+          }
         }
       wave_sync();
-      for (int base = 0; base < n; base += 128) {
-        uint32_t gq[NC][2];
-        bool keep[NC][2];
+      uint32_t st[NC][H];
 #pragma unroll
-        for (int c = 0; c < NC; ++c)
+      for (int c = 0; c < NC; ++c)
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int q = base + 64 * h + lane;
-            int src = hi[c] + 1 + q;
-            src = src >= n ? src - n : src;
-            gq[c][h] = q < n ? (uint32_t)B[c][src] : 0u;
+        for (int h = 0; h < H; ++h) st[c][h] = m[c][gb[c][h]];  // every lane: no branch
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int h = 0; h < H; ++h) asm volatile("" : "+v"(st[c][h]));
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          const bool keep = (lane + 64 * h < n) & (st[c][h] != (stamp[c] & 0xFFu));
+          const uint64_t ball = __ballot(keep);
+          const int slot = filled[c] + (int)__builtin_amdgcn_mbcnt_hi(
+                                           (uint32_t)(ball >> 32),
+                                           __builtin_amdgcn_mbcnt_lo((uint32_t)ball, 0u));
+          if (keep && slot < rest[c]) {
+            int dst = hi[c] + 1 + slot;
+            dst = dst >= n ? dst - n : dst;
+            out[c][dst] = (uint8_t)gb[c][h];
           }
+          filled[c] += __popcll(ball);
+        }
+      // the mutation, in place: new[q] = old[moved_index(q)] over the window
+      // the move touches (the wave's reads finish before its writes)
 #pragma unroll
-        for (int c = 0; c < NC; ++c)
+      for (int c = 0; c < NC; ++c)
+        if (wave_bcast(v_mut, k + c) != 0) {
+          const Move mv{(uint32_t)wave_bcast(v_mtyp, k + c), wave_bcast(v_mi, k + c),
+                        wave_bcast(v_mj, k + c)};
+          const MoveMap fm = move_map(mv);
+          const int w0 = min(mv.i, mv.j), w1 = max(mv.i, mv.j);
+          wave_sync();
+          uint32_t x[H];
 #pragma unroll
-          for (int h = 0; h < 2; ++h)
-            keep[c][h] = base + 64 * h + lane < n && m[c][gq[c][h]] != stamp[c];
-#pragma unroll
-        for (int c = 0; c < NC; ++c)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const uint64_t ball = __ballot(keep[c][h]);
-            const int slot = filled[c] + __popcll(ball & ((1ull << lane) - 1ull));
-            if (keep[c][h] && slot < rest[c]) {
-              int dst = hi[c] + 1 + slot;
-              dst = dst >= n ? dst - n : dst;
-              out[c][dst_of(c, dst)] = (uint8_t)gq[c][h];
-            }
-            filled[c] += __popcll(ball);
+          for (int h = 0; h < H; ++h) {
+            const int q = min(w0 + lane + 64 * h, w1);
+            x[h] = out[c][map_src(fm, q)];
           }
-      }
+          wave_sync();
+#pragma unroll
+          for (int h = 0; h < H; ++h)
+            if (w0 + lane + 64 * h <= w1) out[c][w0 + lane + 64 * h] = (uint8_t)x[h];
+        }
     };
     if (n < 2) {
       for (int k = 0; wave + 16 * k < P; ++k) {
-        const uint8_t* A = rows + (uint32_t)wave_bcast(v_pa, k) * rs;
-        uint8_t* out = rows + (uint32_t)wave_bcast(v_out, k) * rs;
+        const uint8_t* A = rows + (uint32_t)wave_bcast(v_pa, k);
+        uint8_t* out = rows + (uint32_t)wave_bcast(v_out, k);
         for (int q = lane; q < n; q += 64) out[q] = A[q];
       }
     } else {
       int k = 0;
+#if VRPMS_GA_NC == 4
+      for (; wave + 16 * (k + 3) < P; k += 4) breed(std::integral_constant<int, 4>{}, k);
+#endif
       for (; wave + 16 * (k + 1) < P; k += 2) breed(std::integral_constant<int, 2>{}, k);
       if (wave + 16 * k < P) breed(std::integral_constant<int, 1>{}, k);
     }
     __syncthreads();
     GA_T(0);
     // ---- score the P children in place ---------------------------------------
-    for (int t = threadIdx.x; t < P; t += blockDim.x) {
+    // the tour words are read a chunk of eight ahead (one wait per chunk,
+    // not per word), each word's gathers one word ahead of its split steps
+    for (int t = wave * lpw + lane; lane < lpw && t < P; t += 16 * lpw) {
       const uint32_t* rw = reinterpret_cast<const uint32_t*>(rows + (uint32_t)crow[t] * rs);
       ch.reset(a.f);
+      constexpr int CW = 8;
+      const int last = max(nfull - 1, 0);
+      uint32_t cur[CW];
+#pragma unroll
+      for (int i = 0; i < CW; ++i) cur[i] = rw[min(i, last)];
       uint64_t e[1][4];
       if (nfull > 0) {
-        const uint32_t w0[1] = {rw[0]};
+        const uint32_t w0[1] = {cur[0]};
         ch.issue(e, w0, ch.wprev);
       }
-      for (int w = 0; w < nfull; ++w) {
-        const uint32_t cur[1] = {rw[w]};
-        uint64_t nx[1][4];
-        const bool more = w + 1 < nfull;
-        if (more) {
-          const uint32_t wn[1] = {rw[w + 1]};
-          ch.issue(nx, wn, cur);
+      // whole chunks whose eight words all have a next word: straight-line
+      // code, so each wait is for exactly the gathers it needs
+      const int full_chunks = nfull > 0 ? (nfull - 1) / CW : 0;
+      int w = 0;
+      for (; w < full_chunks * CW; w += CW) {
+        uint32_t nxt[CW];
+#pragma unroll
+        for (int i = 0; i < CW; ++i) nxt[i] = rw[min(w + CW + i, last)];
+#pragma unroll
+        for (int i = 0; i < CW; ++i) {
+          uint64_t nx[1][4];
+          const uint32_t wn[1] = {i + 1 < CW ? cur[i + 1] : nxt[0]};
+          const uint32_t wc[1] = {cur[i]};
+          ch.issue(nx, wn, wc);
+          // the next word's four gathers leave before this word's steps (the
+          // scheduler would otherwise trail each one a step behind its use)
+          __builtin_amdgcn_sched_barrier(0);
+          ch.steps(e);
+          ch.wprev[0] = cur[i];
+#pragma unroll
+          for (int x = 0; x < 4; ++x) e[0][x] = nx[0][x];
         }
+#pragma unroll
+        for (int i = 0; i < CW; ++i) cur[i] = nxt[i];
+      }
+      // the last 1..8 words
+#pragma unroll
+      for (int i = 0; i < CW; ++i) {
+        if (w + i >= nfull) break;
+        uint64_t nx[1][4];
+        const bool more = w + i + 1 < nfull;
+        const uint32_t wn[1] = {i + 1 < CW ? cur[i + 1] : 0u};
+        const uint32_t wc[1] = {cur[i]};
+        if (more) ch.issue(nx, wn, wc);
         ch.steps(e);
-        ch.wprev[0] = cur[0];
+        ch.wprev[0] = cur[i];
         if (more)
 #pragma unroll
           for (int x = 0; x < 4; ++x) e[0][x] = nx[0][x];
@@ -326,6 +408,9 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
         const uint32_t x[1] = {rw[nfull]};
         ch.partial(x, n & 3);
       }
+#ifdef VRPMS_GA_PROF
+      if ((int32_t)ch.sa[0].dsum < 0) atomicAdd(&g_ga_prof[4 * 4096 + blockIdx.x], 1ull);
+#endif
       ck[t] = (int32_t)ch.sa[0].dsum < 0  // met the fleet limit: exact re-walk
                   ? ch.redo_exact(a.f, n, [&](int w) { return rw[w]; }).key
                   : ch.sa[0].finish(a.f, n).key;
@@ -334,8 +419,13 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
     GA_T(1);
     // ---- (mu + lambda) survivors by (key, index) -----------------------------
     if (sorted_parents) {
+#if VRPMS_GA_SEL == 1
       merge_select(pk, ck, P, reinterpret_cast<uint64_t*>(smem + a.off_rk),
                    reinterpret_cast<uint32_t*>(smem + a.off_ri), sk, si);
+#else
+      merge_select_sorted(pk, ck, P, max(64, a.M / 2), reinterpret_cast<uint64_t*>(smem + a.off_rk),
+                          reinterpret_cast<uint32_t*>(smem + a.off_ri), sk, si);
+#endif
     } else {
       for (int i = threadIdx.x; i < a.M; i += blockDim.x) {
         sk[i] = i < P ? pk[i] : (i < 2 * P ? ck[i - P] : ~0ull);
@@ -353,7 +443,7 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
       const int i = threadIdx.x + 1024 * k;
       if (i < P) nrow[k] = si[i] < (uint32_t)P ? prow[si[i]] : crow[si[i] - P];
     }
-    for (uint32_t w = threadIdx.x; w <= (uint32_t)(2 * P) / 32; w += blockDim.x) bits[w] = 0u;
+    for (int w = threadIdx.x; w < (2 * P + 3) / 4; w += blockDim.x) reinterpret_cast<uint32_t*>(used)[w] = 0u;
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -361,31 +451,23 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
       if (i < P) {
         prow[i] = nrow[k];
         pk[i] = sk[i];
-        atomicOr(&bits[nrow[k] >> 5], 1u << (nrow[k] & 31u));
+        used[nrow[k]] = 1;  // survivors hold distinct rows: plain stores
       }
     }
     __syncthreads();
-    // the P rows no survivor holds, in row order, take the next children
+    // the P rows no survivor holds, in row order, take the next children:
+    // wave 0 compacts 64 rows at a time by ballot prefix counts
     if (wave == 0) {
-      const int nwords = (2 * P + 31) / 32;  // <= 64 (P <= 1024)
-      uint32_t fr = 0;
-      if (lane < nwords) {
-        fr = ~bits[lane];
-        const int tail = 2 * P - 32 * lane;
-        if (tail < 32) fr &= (1u << tail) - 1u;
-      }
-      const int cnt = __popc(fr);
-      int incl = cnt;
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const int o = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += o;
-      }
-      int slot = incl - cnt;
-      while (fr) {
-        const int b = __ffs((int)fr) - 1;
-        crow[slot++] = (uint16_t)(32 * lane + b);
-        fr &= fr - 1u;
+      int base = 0;
+      for (int j = 0; j < 2 * P; j += 64) {
+        const int r = j + lane;
+        const bool fr = r < 2 * P && used[r] == 0;
+        const uint64_t ball = __ballot(fr);
+        if (fr)
+          crow[base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(ball >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)ball, 0u))] =
+              (uint16_t)r;
+        base += __popcll(ball);
       }
     }
     __syncthreads();
@@ -420,9 +502,16 @@ int launch_ga_fused(const vrpms_ctx* ctx, const vrpms_ga_params* p, uint16_t* d_
   a.gen0 = p->gen0;
   a.pop_tours = d_pop;
   a.pop_keys = d_keys;
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ga_fused_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.bytes);
-  ga_fused_kernel<<<p->islands, 1024, L.bytes, s>>>(a);
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.bytes);
+    kern<<<p->islands, 1024, L.bytes, s>>>(a);
+  };
+  const int H = (n + 63) / 64;
+  if (H <= 1) go(ga_fused_kernel<1>);
+  else if (H == 2) go(ga_fused_kernel<2>);
+  else if (H == 3) go(ga_fused_kernel<3>);
+  else go(ga_fused_kernel<4>);
   VRPMS_HIP(hipGetLastError());
   return 1;
 }
@@ -435,7 +524,7 @@ extern "C" int vrpms_debug_ga_prof(unsigned long long* out, int count, int reset
       hipSuccess)
     return -2;
   if (reset) {
-    static unsigned long long zero[4 * 4096];
+    static unsigned long long zero[5 * 4096];
     (void)hipMemcpyToSymbol(HIP_SYMBOL(vrpms::g_ga_prof), zero, sizeof(zero));
   }
   return 0;

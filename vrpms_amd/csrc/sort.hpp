@@ -202,4 +202,47 @@ VRPMS_DEV void merge_select(const uint64_t* pk, const uint64_t* ck, int P, uint6
   __syncthreads();
 }
 
+// The same selection with the children fully sorted first (M2 = the power of
+// two >= max(P, 64), block_sort_pairs_waves: its stride >= 64 stages cross
+// the LDS), so every pair's final rank is its position in its own list plus
+// ONE lower bound in the other: a child's among the parents, a parent's
+// among the sorted children -- one binary search of log2 steps per pair
+// instead of one per child run.  Same sk[0..P) / si[0..P) as merge_select.
+// rk / ri hold M2 entries; needs M2 <= blockDim.x.  Every thread of the
+// block must call it.
+VRPMS_DEV void merge_select_sorted(const uint64_t* pk, const uint64_t* ck, int P, int M2,
+                                   uint64_t* rk, uint32_t* ri, uint64_t* sk, uint32_t* si) {
+  for (int c = threadIdx.x; c < M2; c += blockDim.x) {
+    rk[c] = c < P ? ck[c] : ~0ull;  // padding sorts last (index > 2P)
+    ri[c] = c < P ? (uint32_t)(P + c) : 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  block_sort_pairs_waves(rk, ri, M2);  // ends with a barrier
+  for (int e = threadIdx.x; e < 2 * P; e += blockDim.x) {
+    const bool child = e >= P;
+    const int j = child ? e - P : e;
+    const uint64_t k = child ? rk[j] : pk[j];
+    const uint32_t v = child ? ri[j] : (uint32_t)j;
+    int pos = 0;
+    if (child) {  // lower bound among the P parents
+      int hi = P;
+      while (pos < hi) {
+        const int mid = (pos + hi) >> 1;
+        if (pair_less(pk[mid], (uint32_t)mid, k, v)) pos = mid + 1;
+        else hi = mid;
+      }
+    } else {  // lower bound among the M2 sorted children (padding is never less)
+      for (int s = M2 >> 1; s > 0; s >>= 1)
+        if (pair_less(rk[pos + s - 1], ri[pos + s - 1], k, v)) pos += s;
+      if (pair_less(rk[pos], ri[pos], k, v)) ++pos;
+    }
+    const int rank = j + pos;
+    if (rank < P) {
+      sk[rank] = k;
+      si[rank] = v;
+    }
+  }
+  __syncthreads();
+}
+
 }  // namespace vrpms
