@@ -36,12 +36,10 @@
 
 namespace vrpms {
 
-// (mu + lambda) selection: 1 = merge ranks over 64-runs of children,
-// 2 = children sorted first, one lower bound per pair (A/B only: the
-// block sort's LDS stages cost more than the run searches they save, sort
-// phase 4.0 -> 7.0 us at 256 x 256, tools/ga_prof.py)
-#ifndef VRPMS_GA_SEL
-#define VRPMS_GA_SEL 1
+// breed stores: 1 = every lane stores, the lanes with nothing to store into
+// a per-wave sink byte; 0 = exec-masked stores
+#ifndef VRPMS_GA_PRED
+#define VRPMS_GA_PRED 1
 #endif
 // children bred together per wavefront (each on its own stamp array)
 #ifndef VRPMS_GA_NC
@@ -74,7 +72,8 @@ struct GaFusedArgs {
   uint32_t pmut, seed_lo, seed_hi;
   uint64_t gen0;
   uint32_t rs;  // LDS bytes per tour row (multiple of 4, rs / 4 odd)
-  uint32_t off_rows, off_pk, off_ck, off_prow, off_crow, off_sk, off_si, off_used, off_bits;
+  uint32_t off_rows, off_pk, off_ck, off_prow, off_crow, off_sk, off_si, off_used, off_bits,
+      off_sink;
   uint32_t off_rk, off_ri;  // child runs of merge_select
   uint16_t* pop_tours;  // [islands][pop][n] in/out
   uint64_t* pop_keys;   // [islands][pop] in/out
@@ -107,8 +106,8 @@ static GaFusedLayout ga_fused_layout(int N, int n, int P) {
   a.off_si = (uint32_t)off;     off = al16(off + (size_t)M * 4);
   a.off_used = (uint32_t)off;   off = al16(off + (size_t)16 * VRPMS_GA_NC * N);  // u8 stamp arrays
   a.off_bits = (uint32_t)off;   off = al16(off + (size_t)2 * P);  // u8 row-in-use flags
-  // child runs of merge_select / the sorted children of merge_select_sorted
-  const size_t runs = std::max((size_t)64 * ((P + 63) / 64), (size_t)std::max(64, M / 2));
+  a.off_sink = (uint32_t)off;   off = al16(off + 64);  // one sink dword per wave
+  const size_t runs = (size_t)64 * ((P + 63) / 64);  // child runs of merge_select
   a.off_rk = (uint32_t)off;     off = al16(off + runs * 8);
   a.off_ri = (uint32_t)off;     off = al16(off + runs * 4);
   L.bytes = off;
@@ -142,6 +141,11 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
   // address, no bank conflicts; the arrays are cleared before the stamps wrap
   uint8_t* mk = smem + a.off_used + wave * (uint32_t)a.f.N;
   uint8_t* used = smem + a.off_bits;
+  // the breed's sink: a dword per lane in sk (dead until the selection) when
+  // it is large enough, so the sink stores of a half-wave hit 32 distinct
+  // banks; else one shared dword per wave
+  uint8_t* sink = a.M * 8 >= 16 * 256 ? reinterpret_cast<uint8_t*>(sk) + wave * 256 + lane * 4
+                                      : smem + a.off_sink + 4 * wave;
   uint16_t* gpop = a.pop_tours + (int64_t)island * P * n;
   uint64_t* gkeys = a.pop_keys + (int64_t)island * P;
 
@@ -198,6 +202,9 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
       __syncthreads();
       gclr = g;
     }
+    // row-in-use flags for this generation's survivors (read after the
+    // selection, several barriers on)
+    for (int w = threadIdx.x; w < (2 * P + 3) / 4; w += blockDim.x) reinterpret_cast<uint32_t*>(used)[w] = 0u;
     // ---- breed: one child per wavefront at a time --------------------------
     // Lane k of wave w first draws everything random about child w + 16k in
     // parallel (two Philox blocks, both tournaments, the OX1 cut points, the
@@ -279,10 +286,18 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
 #pragma unroll
         for (int h = 0; h < H; ++h) {
           const int q = lane + 64 * h;
+#if VRPMS_GA_PRED
+          // lanes outside the span write the wave's sink byte instead of
+          // branching around the stores (no exec-mask bookkeeping)
+          const bool in = q >= lo[c] && q <= hi[c];
+          *(in ? out[c] + q : sink) = (uint8_t)ga[c][h];
+          *(in ? m[c] + ga[c][h] : sink) = (uint8_t)stamp[c];
+#else
           if (q >= lo[c] && q <= hi[c]) {
             out[c][q] = (uint8_t)ga[c][h];
             m[c][ga[c][h]] = (uint8_t)stamp[c];
           }
+#endif
         }
       wave_sync();
       uint32_t st[NC][H];
@@ -303,11 +318,13 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
           const int slot = filled[c] + (int)__builtin_amdgcn_mbcnt_hi(
                                            (uint32_t)(ball >> 32),
                                            __builtin_amdgcn_mbcnt_lo((uint32_t)ball, 0u));
-          if (keep && slot < rest[c]) {
-            int dst = hi[c] + 1 + slot;
-            dst = dst >= n ? dst - n : dst;
-            out[c][dst] = (uint8_t)gb[c][h];
-          }
+          int dst = hi[c] + 1 + slot;
+          dst = dst >= n ? dst - n : dst;
+#if VRPMS_GA_PRED
+          *(keep && slot < rest[c] ? out[c] + dst : sink) = (uint8_t)gb[c][h];
+#else
+          if (keep && slot < rest[c]) out[c][dst] = (uint8_t)gb[c][h];
+#endif
           filled[c] += __popcll(ball);
         }
       // the mutation, in place: new[q] = old[moved_index(q)] over the window
@@ -418,14 +435,10 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
     __syncthreads();
     GA_T(1);
     // ---- (mu + lambda) survivors by (key, index) -----------------------------
+    // si receives the survivors' LDS rows (merge_select maps them)
     if (sorted_parents) {
-#if VRPMS_GA_SEL == 1
       merge_select(pk, ck, P, reinterpret_cast<uint64_t*>(smem + a.off_rk),
-                   reinterpret_cast<uint32_t*>(smem + a.off_ri), sk, si);
-#else
-      merge_select_sorted(pk, ck, P, max(64, a.M / 2), reinterpret_cast<uint64_t*>(smem + a.off_rk),
-                          reinterpret_cast<uint32_t*>(smem + a.off_ri), sk, si);
-#endif
+                   reinterpret_cast<uint32_t*>(smem + a.off_ri), sk, si, prow, crow);
     } else {
       for (int i = threadIdx.x; i < a.M; i += blockDim.x) {
         sk[i] = i < P ? pk[i] : (i < 2 * P ? ck[i - P] : ~0ull);
@@ -435,39 +448,47 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
       if (a.M >= 64 && a.M <= 1024) block_sort_pairs_waves(sk, si, a.M);
       else block_sort_pairs(sk, si, a.M);
       sorted_parents = true;
+      uint16_t nrow[2] = {0, 0};
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int i = threadIdx.x + 1024 * k;
+        if (i < P) nrow[k] = si[i] < (uint32_t)P ? prow[si[i]] : crow[si[i] - P];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int i = threadIdx.x + 1024 * k;
+        if (i < P) si[i] = nrow[k];
+      }
+      __syncthreads();
     }
     GA_T(2);
-    uint16_t nrow[2] = {0, 0};
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int i = threadIdx.x + 1024 * k;
-      if (i < P) nrow[k] = si[i] < (uint32_t)P ? prow[si[i]] : crow[si[i] - P];
-    }
-    for (int w = threadIdx.x; w < (2 * P + 3) / 4; w += blockDim.x) reinterpret_cast<uint32_t*>(used)[w] = 0u;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int i = threadIdx.x + 1024 * k;
-      if (i < P) {
-        prow[i] = nrow[k];
-        pk[i] = sk[i];
-        used[nrow[k]] = 1;  // survivors hold distinct rows: plain stores
-      }
+    for (int i = threadIdx.x; i < P; i += blockDim.x) {
+      const uint32_t row = si[i];
+      prow[i] = (uint16_t)row;
+      pk[i] = sk[i];
+      used[row] = 1;  // survivors hold distinct rows: plain stores
     }
     __syncthreads();
     // the P rows no survivor holds, in row order, take the next children:
     // wave 0 compacts 64 rows at a time by ballot prefix counts
     if (wave == 0) {
       int base = 0;
-      for (int j = 0; j < 2 * P; j += 64) {
-        const int r = j + lane;
-        const bool fr = r < 2 * P && used[r] == 0;
-        const uint64_t ball = __ballot(fr);
-        if (fr)
-          crow[base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(ball >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)ball, 0u))] =
-              (uint16_t)r;
-        base += __popcll(ball);
+      for (int j0 = 0; j0 < 2 * P; j0 += 512) {
+        uint32_t f[8];  // eight chunks' flags read together
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = used[min(j0 + 64 * j + lane, 2 * P - 1)];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int r = j0 + 64 * j + lane;
+          const bool fr = r < 2 * P && f[j] == 0u;
+          const uint64_t ball = __ballot(fr);
+          if (fr)
+            crow[base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(ball >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)ball, 0u))] =
+                (uint16_t)r;
+          base += __popcll(ball);
+        }
       }
     }
     __syncthreads();

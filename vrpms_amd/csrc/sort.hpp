@@ -105,17 +105,30 @@ VRPMS_DEV void block_sort_pairs_waves(uint64_t* sk, uint32_t* si, int M) {
 }
 
 // x from lane (lane ^ stride), stride a compile-time power of two after
-// unrolling: DPP quad_perm (1, 2) and row_ror:8 (8) ride on a VALU move,
-// ds_swizzle's xor mode (4, 16) needs no address; only 32 crosses halves
-// through ds_bpermute.
+// unrolling, all in VALU (no LDS round trip): DPP quad_perm (1, 2) and
+// row_ror:8 (8) ride on a move; 4 picks row_shl:4 or row_shr:4 by lane bit
+// 2; 16 and 32 are gfx950's v_permlane16_swap / v_permlane32_swap of x with
+// itself (the odd 16-lane rows with the even ones, the upper 32 lanes with
+// the lower), the partner's copy picked by lane bit 4 / 5.
 VRPMS_DEV uint32_t xor_lanes(uint32_t x, int stride) {
+  const uint32_t l = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   switch (stride) {
     case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);
     case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, true);
-    case 4: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x101F);
+    case 4: {
+      const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x104, 0xF, 0xF, true);  // lane + 4
+      const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x114, 0xF, 0xF, true);  // lane - 4
+      return (l & 4u) ? dn : up;
+    }
     case 8: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xF, 0xF, true);
-    case 16: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);
-    default: return (uint32_t)__shfl_xor((int)x, stride, 64);
+    case 16: {
+      const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+      return (l & 16u) ? r[0] : r[1];
+    }
+    default: {
+      const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+      return (l & 32u) ? r[0] : r[1];
+    }
   }
 }
 
@@ -153,9 +166,12 @@ VRPMS_DEV bool pair_less(uint64_t ka, uint32_t ia, uint64_t kb, uint32_t ib) {
 // unique (the index breaks ties), so sk[0..P) / si[0..P) equal the first P of
 // block_sort_pairs over the 2P pairs.  rk / ri hold the child runs
 // (64 * ceil(P / 64) entries); needs blockDim.x >= 64 * ceil(P / 64).
-// Every thread of the block must call it.
+// With pmap / cmap, si receives pmap[index] for a parent and
+// cmap[index - P] for a child instead of the index (the fused GA's LDS rows
+// of the survivors).  Every thread of the block must call it.
 VRPMS_DEV void merge_select(const uint64_t* pk, const uint64_t* ck, int P, uint64_t* rk,
-                            uint32_t* ri, uint64_t* sk, uint32_t* si) {
+                            uint32_t* ri, uint64_t* sk, uint32_t* si,
+                            const uint16_t* pmap = nullptr, const uint16_t* cmap = nullptr) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int R = (P + 63) >> 6;
   if (w < R) {  // wave-uniform
@@ -167,23 +183,31 @@ VRPMS_DEV void merge_select(const uint64_t* pk, const uint64_t* ck, int P, uint6
     ri[c] = v;
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < 2 * P; e += blockDim.x) {
+  // the lower bounds a pair needs in the other runs (and a child's among the
+  // parents) are independent searches: with 4P <= blockDim.x two lanes share
+  // each pair, lane bit 0 choosing the runs of that parity (the even lane
+  // also takes the parents' search), their counts added by a DPP swap
+  const bool two = 4 * P <= (int)blockDim.x;  // block-uniform
+  const int step = two ? (int)blockDim.x >> 1 : (int)blockDim.x;
+  for (int t = two ? (int)threadIdx.x >> 1 : (int)threadIdx.x; t < 2 * P; t += step) {
+    const int half = two ? (int)(threadIdx.x & 1u) : -1;
+    const int e = t;
     const bool child = e >= P;
     const int c = e - P, own = child ? c >> 6 : -1;
-    if (child && (c & 63) >= P - (own << 6)) continue;  // run padding
+    const bool pad = child && (c & 63) >= P - (own << 6);  // run padding
     const uint64_t k = child ? rk[c] : pk[e];
     const uint32_t v = child ? ri[c] : (uint32_t)e;
-    int rank = child ? (c & 63) : e;
-    if (child) {
+    int part = 0;
+    if (child && half <= 0) {
       int lo = 0, hi = P;  // lower bound among the parents
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
         if (pair_less(pk[mid], (uint32_t)mid, k, v)) lo = mid + 1;
         else hi = mid;
       }
-      rank += lo;
+      part += lo;
     }
-    for (int r = 0; r < R; ++r) {  // lower bound in every other run
+    for (int r = half < 0 ? 0 : half; r < R; r += half < 0 ? 1 : 2) {  // every other run
       if (r == own) continue;
       const uint64_t* rkr = rk + (r << 6);
       const uint32_t* rir = ri + (r << 6);
@@ -192,54 +216,14 @@ VRPMS_DEV void merge_select(const uint64_t* pk, const uint64_t* ck, int P, uint6
       for (int s = 32; s > 0; s >>= 1)
         if (pair_less(rkr[pos + s - 1], rir[pos + s - 1], k, v)) pos += s;
       if (pair_less(rkr[pos], rir[pos], k, v)) ++pos;
-      rank += pos;
+      part += pos;
     }
-    if (rank < P) {
+    if (two)  // both lanes of the pair active here (the loop bound is per pair)
+      part += __builtin_amdgcn_mov_dpp(part, 0xB1, 0xF, 0xF, false);
+    const int rank = part + (child ? (c & 63) : e);
+    if (!pad && half <= 0 && rank < P) {
       sk[rank] = k;
-      si[rank] = v;
-    }
-  }
-  __syncthreads();
-}
-
-// The same selection with the children fully sorted first (M2 = the power of
-// two >= max(P, 64), block_sort_pairs_waves: its stride >= 64 stages cross
-// the LDS), so every pair's final rank is its position in its own list plus
-// ONE lower bound in the other: a child's among the parents, a parent's
-// among the sorted children -- one binary search of log2 steps per pair
-// instead of one per child run.  Same sk[0..P) / si[0..P) as merge_select.
-// rk / ri hold M2 entries; needs M2 <= blockDim.x.  Every thread of the
-// block must call it.
-VRPMS_DEV void merge_select_sorted(const uint64_t* pk, const uint64_t* ck, int P, int M2,
-                                   uint64_t* rk, uint32_t* ri, uint64_t* sk, uint32_t* si) {
-  for (int c = threadIdx.x; c < M2; c += blockDim.x) {
-    rk[c] = c < P ? ck[c] : ~0ull;  // padding sorts last (index > 2P)
-    ri[c] = c < P ? (uint32_t)(P + c) : 0xFFFFFFFFu;
-  }
-  __syncthreads();
-  block_sort_pairs_waves(rk, ri, M2);  // ends with a barrier
-  for (int e = threadIdx.x; e < 2 * P; e += blockDim.x) {
-    const bool child = e >= P;
-    const int j = child ? e - P : e;
-    const uint64_t k = child ? rk[j] : pk[j];
-    const uint32_t v = child ? ri[j] : (uint32_t)j;
-    int pos = 0;
-    if (child) {  // lower bound among the P parents
-      int hi = P;
-      while (pos < hi) {
-        const int mid = (pos + hi) >> 1;
-        if (pair_less(pk[mid], (uint32_t)mid, k, v)) pos = mid + 1;
-        else hi = mid;
-      }
-    } else {  // lower bound among the M2 sorted children (padding is never less)
-      for (int s = M2 >> 1; s > 0; s >>= 1)
-        if (pair_less(rk[pos + s - 1], ri[pos + s - 1], k, v)) pos += s;
-      if (pair_less(rk[pos], ri[pos], k, v)) ++pos;
-    }
-    const int rank = j + pos;
-    if (rank < P) {
-      sk[rank] = k;
-      si[rank] = v;
+      si[rank] = pmap ? (uint32_t)(child ? cmap[v - P] : pmap[v]) : v;
     }
   }
   __syncthreads();
