@@ -650,7 +650,7 @@ def cfg5_http_leg(R=10000, steps=1000, connections=1024):
     import subprocess
     threads, cores = host_cores()
     clients = max(1, min(4, threads // 4))
-    workers = max(2, threads - clients - 2)   # the pool's parent and GPU owner keep a core each
+    workers = max(2, threads - clients - 1)   # the GPU owner keeps a core (the pool's parent sleeps)
     cmd = [sys.executable, "-m", "vrpms_amd.frontends", "bench-http", "--requests", str(R),
            "--workers", str(workers), "--steps", str(steps), "--clients", str(clients),
            "--connections", str(connections)]

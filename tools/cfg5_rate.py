@@ -13,8 +13,11 @@ import torch  # noqa: E402
 from vrpms_amd import synth  # noqa: E402
 from vrpms_amd.core import Context  # noqa: E402
 
-R = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
+R = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 10000
 steps = 1000
+if "--lib" in sys.argv:  # an A/B build (tools/ab_build.py) instead of the tree's
+    from vrpms_amd import _lib
+    _lib.load(sys.argv[sys.argv.index("--lib") + 1])
 ctx = Context(0)
 rng = np.random.default_rng(0)
 mats = np.stack([synth.random_symmetric(50, rng) for _ in range(R)])

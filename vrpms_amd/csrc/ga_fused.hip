@@ -122,7 +122,9 @@ VRPMS_DEV int tourney2(const uint64_t* keys, int pop, uint32_t r0, uint32_t r1) 
 }
 
 // H: 64-position slots per lane, ceil(n / 64)
-template <int H>
+// CY: every customer demand >= 1, so the scoring walk's fit test is the
+// add's carry (split_step_carry, one VALU fewer per customer)
+template <int H, bool CY>
 __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int P = a.pop, n = a.n, island = blockIdx.x;
@@ -180,7 +182,7 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
   const int cpw = (P + 15) / 16;  // children per wavefront per generation
   int gclr = 0;                   // generation of the last stamp clear
 
-  WordChains<1> ch;
+  WordChains<1, CY> ch;
   ch.setup(a.f, smem);
   const int nfull = n >> 2;
 #ifndef VRPMS_GA_SCORE_MINLPW
@@ -529,10 +531,16 @@ int launch_ga_fused(const vrpms_ctx* ctx, const vrpms_ga_params* p, uint16_t* d_
     kern<<<p->islands, 1024, L.bytes, s>>>(a);
   };
   const int H = (n + 63) / 64;
-  if (H <= 1) go(ga_fused_kernel<1>);
-  else if (H == 2) go(ga_fused_kernel<2>);
-  else if (H == 3) go(ga_fused_kernel<3>);
-  else go(ga_fused_kernel<4>);
+  const bool cy = f.carry && ctx->opt_split_mode != 3;
+  auto pick = [&](auto cy_tag) {
+    constexpr bool C = decltype(cy_tag)::value;
+    if (H <= 1) go(ga_fused_kernel<1, C>);
+    else if (H == 2) go(ga_fused_kernel<2, C>);
+    else if (H == 3) go(ga_fused_kernel<3, C>);
+    else go(ga_fused_kernel<4, C>);
+  };
+  if (cy) pick(std::true_type{});
+  else pick(std::false_type{});
   VRPMS_HIP(hipGetLastError());
   return 1;
 }

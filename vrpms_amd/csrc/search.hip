@@ -2105,14 +2105,20 @@ VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, unsigned cha
   uint16_t* B = buf + npad + 1;
   uint16_t* Best = buf + 2 * npad + 1;
   const uint32_t cid = (uint32_t)(r * 4 + wave);
-  // Philox Fisher-Yates start: for i = n-1..1 swap t[i], t[x % (i+1)].  The
-  // draws have wave-uniform counters (the scalar unit computes them); lane 0
-  // swaps.
+  // Philox Fisher-Yates start: for i = n-1..1 swap t[i], t[x % (i+1)].  Lane
+  // l draws i = 64c + l's block for a chunk c of 64 steps at once (VALU, not
+  // 49 scalar Philox blocks in a row); lane 0 swaps, reading each j by
+  // v_readlane.
   for (int q = lane; q < n; q += 64) A[q] = (uint16_t)(q + 1);
   wave_sync();
+  uint32_t jv = 0;
   for (int i = n - 1; i >= 1; --i) {
-    const u32x4 x = philox(0xffffffffu, 0xffffffffu, cid, (uint32_t)i, a.seed_lo, a.seed_hi);
-    const int j = (int)__builtin_amdgcn_readfirstlane((int)(x.x % (uint32_t)(i + 1)));
+    if (i == n - 1 || (i & 63) == 63) {
+      const uint32_t il = (uint32_t)(i & ~63) + (uint32_t)lane;
+      const u32x4 x = philox(0xffffffffu, 0xffffffffu, cid, il, a.seed_lo, a.seed_hi);
+      jv = x.x % (il + 1u);
+    }
+    const int j = __builtin_amdgcn_readlane((int)jv, i & 63);
     if (lane == 0) {
       const uint16_t t = A[i];
       A[i] = A[j];
@@ -2177,16 +2183,33 @@ VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, unsigned cha
       mb.i = wave_bcast(m.i, bl);
       mb.j = wave_bcast(m.j, bl);
       dur = wave_bcast(nd, bl);
-      for (int q = lane; q < n; q += 64) B[q] = A[moved_index(q, mb)];
-      wave_sync();
-      uint16_t* t = A;
-      A = B;
-      B = t;
-      if constexpr (symmetric) build_E();
-      ck = k;
-      if (ck < bk) {
-        bk = ck;
-        for (int q = lane; q < n; q += 64) Best[q] = A[q];
+      if (n < 64) {  // one position per lane: the moved tour stays in registers
+        const uint32_t v = lane < n ? (uint32_t)A[moved_index(lane, mb)] : 0u;  // 0: the depot
+        if (lane < n) B[lane] = (uint16_t)v;
+        if constexpr (symmetric) {  // E from the moved tour: the predecessor by wave_shr:1
+          const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+          if (lane <= n) E[lane] = (MatT)dist(lane ? prev : 0u, v);
+        }
+        uint16_t* t = A;
+        A = B;
+        B = t;
+        ck = k;
+        if (ck < bk) {
+          bk = ck;
+          if (lane < n) Best[lane] = (uint16_t)v;
+        }
+      } else {
+        for (int q = lane; q < n; q += 64) B[q] = A[moved_index(q, mb)];
+        wave_sync();
+        uint16_t* t = A;
+        A = B;
+        B = t;
+        if constexpr (symmetric) build_E();
+        ck = k;
+        if (ck < bk) {
+          bk = ck;
+          for (int q = lane; q < n; q += 64) Best[q] = A[q];
+        }
       }
       wave_sync();
     }
