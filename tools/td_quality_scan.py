@@ -25,7 +25,11 @@ ap.add_argument("--seeds", type=int, nargs="+", default=[0])
 ap.add_argument("--cpu", action="store_true")
 ap.add_argument("--shapes", default="256x128,512x64,1024x64,512x128,1024x128")
 ap.add_argument("--tend", type=float, nargs="+", default=[0.004])
+ap.add_argument("--lib", default=None, help="an A/B build (tools/ab_build.py) instead of the tree's")
 args = ap.parse_args()
+if args.lib:
+    from vrpms_amd import _lib
+    _lib.load(args.lib)
 ctx = Context(0)
 for sd in args.seeds:
     x = synth.x_style(1000, seed=sd) if args.x1000 else (

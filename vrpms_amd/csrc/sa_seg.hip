@@ -39,7 +39,7 @@
 
 namespace vrpms {
 
-constexpr int kSegRegs = 20;      // tours up to 64 * 20 tokens (the sizes the tables were tested at)
+constexpr int kSegRegs = 20;      // positions per lane in registers on an accept: n < 64 * 20
 constexpr int kSegMaxMoves = 8;   // moves per lane per step (64 M per step)
 #ifndef VRPMS_SEG_SHIFT
 #define VRPMS_SEG_SHIFT 8  // (A/B builds may set another)
@@ -63,7 +63,6 @@ struct SegArgs {
   int rm, lv;   // route slots, sparse-table levels
   uint32_t chain_bytes;
   int W;        // wavefronts per chain (W > 1: one chain per workgroup, cpw = 1)
-  uint32_t stage_off;  // the accept's staging area within a chain's LDS
 };
 
 // The cross-wavefront exchange of a multi-wavefront chain: each wavefront's
@@ -83,19 +82,13 @@ constexpr uint32_t kSegXBytes = 2 * kSegMaxWaves * sizeof(SegXSlot) + 32;
 // each | sparse (lv-1) x rm | (het) need, allow rm+1 each], then u16 [tok n+2 |
 // SC n+2 | SP, RB, FNE, LNE1 segs+2 | RS rm+1 | (het) NB 2 kSegShift x (rm+1) |
 // SEGR rm+1 | cend K]
-// then the accept's staging area (u32 edges, u16 tokens of the changed span:
-// staged through LDS, not registers, which were the kernel's register peak)
-__host__ __device__ inline uint32_t seg_stage_off(int n, int segs, int rm, int lv, bool het, int K) {
+__host__ __device__ inline uint32_t seg_chain_bytes(int n, int segs, int rm, int lv, bool het, int K) {
   const uint32_t np2 = ((uint32_t)n + 2u + 1u) & ~1u;
   const uint32_t u32s = 3u * np2 + 4u * (uint32_t)(rm + 1) + (uint32_t)(lv - 1) * (uint32_t)rm +
                         (het ? 2u * (uint32_t)(rm + 1) : 0u);
   const uint32_t u16s = 2u * np2 + 4u * (uint32_t)(segs + 2) + (uint32_t)(rm + 1) +
                         (het ? (2u * kSegShift + 1u) * (uint32_t)(rm + 1) + (uint32_t)K : 0u);
-  return (4u * u32s + 2u * u16s + 15u) & ~15u;
-}
-__host__ __device__ inline uint32_t seg_chain_bytes(int n, int segs, int rm, int lv, bool het, int K) {
-  const uint32_t np2 = ((uint32_t)n + 2u + 1u) & ~1u;
-  return seg_stage_off(n, segs, rm, lv, het, K) + ((6u * np2 + 15u) & ~15u) + kSegXBytes;
+  return ((4u * u32s + 2u * u16s + 15u) & ~15u) + kSegXBytes;
 }
 
 __host__ __device__ inline int seg_levels(int rm) {
@@ -281,10 +274,6 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
   SegXSlot* xs = reinterpret_cast<SegXSlot*>(smem + inst_lds_bytes(a.si) + ((N * 4u + 15u) & ~15u) +
                                              (uint32_t)slot * a.chain_bytes + a.chain_bytes -
                                              kSegXBytes);
-  // the accept's staging area: u32 edges then u16 tokens of the changed span
-  uint32_t* stE = reinterpret_cast<uint32_t*>(smem + inst_lds_bytes(a.si) + ((N * 4u + 15u) & ~15u) +
-                                              (uint32_t)slot * a.chain_bytes + a.stage_off);
-  uint16_t* stT = reinterpret_cast<uint16_t*>(stE + ((((uint32_t)n + 2u + 1u) & ~1u)));
   int32_t* xr = reinterpret_cast<int32_t*>(xs + 2 * kSegMaxWaves);  // S, R, Tt, seg_ok, ck lo/hi
   auto d0 = [&](uint32_t x, uint32_t y) __attribute__((always_inline)) -> uint32_t {
     if ((x | y) == 0u) return 0u;  // two depots: an empty route lasts 0
@@ -1128,24 +1117,31 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
           reb_a = blo;
           reb_b = hq;
           pe_old = T.PE[hq + 1];
-          // staged through the chain's LDS staging area (the span's tokens and
-          // edges are read from the current tables first, then written)
-          for (int q = blo + lane; q <= hq; q += 64) {
+          uint32_t v_tok[kSegRegs], v_e[kSegRegs];
+#pragma unroll
+          for (int i = 0; i < kSegRegs; ++i) {
+            if (blo + 64 * i > hq) break;
+            const int q = blo + lane + 64 * i;
+            v_tok[i] = 0u;
+            v_e[i] = 0u;
+            if (q > hq) continue;
             const int sq = map_src(mmb, q), sp = map_src(mmb, q - 1);
-            uint32_t e;
-            if (q == blo) e = w0;
-            else if (q == blo + 1) e = w1;
-            else if (q == bhi) e = w2;
-            else if (q == bhi + 1) e = w3;
-            else if (sp + 1 == sq) e = T.PE[sq + 1] - T.PE[sq];
-            else e = T.PE[sp + 1] - T.PE[sp];  // reversed: the edge between A[sq] and A[sp]
-            stE[q - blo] = e;
-            if (q < n) stT[q - blo] = T.tok[sq];
+            if (q < n) v_tok[i] = T.tok[sq];
+            if (q == blo) v_e[i] = w0;
+            else if (q == blo + 1) v_e[i] = w1;
+            else if (q == bhi) v_e[i] = w2;
+            else if (q == bhi + 1) v_e[i] = w3;
+            else if (sp + 1 == sq) v_e[i] = T.PE[sq + 1] - T.PE[sq];
+            else v_e[i] = T.PE[sp + 1] - T.PE[sp];  // reversed: the edge between A[sq] and A[sp]
           }
           wave_sync();
-          for (int q = blo + lane; q <= hq; q += 64) {
-            if (q < n) T.tok[q] = stT[q - blo];
-            T.PE[q + 1] = stE[q - blo];
+#pragma unroll
+          for (int i = 0; i < kSegRegs; ++i) {
+            if (blo + 64 * i > hq) break;
+            const int q = blo + lane + 64 * i;
+            if (q > hq) continue;
+            if (q < n) T.tok[q] = (uint16_t)v_tok[i];
+            T.PE[q + 1] = v_e[i];
           }
         }
         need_build = true;
@@ -1205,7 +1201,9 @@ int launch_sa_seg(const vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* d_cu
   // tools/seg_waves.py -- but loses over an annealing run, where pricing
   // dominates: 192 k vs 337 k steps per chain in 10 s, 84,475 vs 83,018,
   // tools/td_quality_scan.py --x1000; so W = 2 stays up to two wavefronts
-  // per SIMD)
+  // per SIMD.  Staging the accept's span through LDS instead of the
+  // registers below halved that annealing run -- 187 k vs 333 k steps per
+  // chain, 84,421 vs 83,167 -- and was reverted.)
   int W = std::min(moves / 64, kSegMaxWaves);
   while (W > 1 && (int64_t)p->chains * W > 8 * (int64_t)ctx->num_cus) W >>= 1;
   if (ctx->opt_seg_waves > 0) W = std::min(ctx->opt_seg_waves, kSegMaxWaves);  // A/B
@@ -1219,8 +1217,7 @@ int launch_sa_seg(const vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* d_cu
   if (lds > ctx->max_lds) return 1;
   SegArgs a{si, p->chains, n, p->steps, p->window, wtypes, p->inv_t0, p->inv_alpha,
             (uint32_t)p->seed, (uint32_t)(p->seed >> 32), p->step0, d_cur, d_cur_key, d_best,
-            d_best_key, moves / 64 / W, cpw, segs, rm, lv, cb, W,
-            seg_stage_off(n, segs, rm, lv, het, in.K)};
+            d_best_key, moves / 64 / W, cpw, segs, rm, lv, cb, W};
   auto go = [&](auto kern) {
     if (lds > 65536)
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),

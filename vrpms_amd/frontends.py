@@ -874,14 +874,28 @@ def bench_api(R: int = 10000, N: int = 50, workers: int = 16, steps: int = 1000,
 # ---------------------------------------------------------------------------
 # cfg 5 over real sockets: a load generator in processes of its own
 # ---------------------------------------------------------------------------
+_REQ_PARTS = {}
+
+
 def _tsp_request(i: int, N: int, host: str = "127.0.0.1") -> bytes:
     """POST /api/tsp/sa with the reference's body (api/tsp/sa/index.py:16-63)
-    on matrix i, HTTP/1.1 keep-alive."""
-    body = json.dumps({"solutionName": "n", "solutionDescription": "d", "locationsKey": 0,
-                       "durationsKey": i, "customers": list(range(1, N)), "startNode": 0,
-                       "startTime": 0}).encode()
-    return (f"POST /api/tsp/sa HTTP/1.1\r\nHost: {host}\r\nContent-Type: application/json\r\n"
-            f"Content-Length: {len(body)}\r\n\r\n").encode("latin-1") + body
+    on matrix i, HTTP/1.1 keep-alive.  The body's bytes around durationsKey
+    are encoded once per (N, host): the load generator should not spend its
+    cores re-encoding the same JSON."""
+    parts = _REQ_PARTS.get((N, host))
+    if parts is None:
+        mark = -7310
+        body = json.dumps({"solutionName": "n", "solutionDescription": "d", "locationsKey": 0,
+                           "durationsKey": mark, "customers": list(range(1, N)), "startNode": 0,
+                           "startTime": 0}).encode()
+        pre, post = body.split(str(mark).encode())
+        head = (f"POST /api/tsp/sa HTTP/1.1\r\nHost: {host}\r\nContent-Type: application/json"
+                f"\r\nContent-Length: ").encode("latin-1")
+        parts = _REQ_PARTS[(N, host)] = (head, pre, post)
+    head, pre, post = parts
+    key = str(i).encode()
+    return b"".join((head, str(len(pre) + len(key) + len(post)).encode(), b"\r\n\r\n", pre, key,
+                     post))
 
 
 def _loadgen_proc(host, port, idx, N, conns, start_at, sample, out_q):
@@ -927,15 +941,13 @@ def _loadgen_proc(host, port, idx, N, conns, start_at, sample, out_q):
             i = self.buf.find(b"\r\n\r\n")
             if i < 0:
                 return
-            head = bytes(self.buf[:i]).decode("latin-1")
-            n = 0
-            for ln in head.split("\r\n")[1:]:
-                k, _, v = ln.partition(":")
-                if k.strip().lower() == "content-length":
-                    n = int(v)
+            head = bytes(self.buf[:i])
+            c = head.lower().find(b"\r\ncontent-length:")
+            n = int(head[c + 17:head.find(b"\r\n", c + 2) if head.find(b"\r\n", c + 2) > 0
+                         else len(head)]) if c >= 0 else 0
             if len(self.buf) < i + 4 + n:
                 return
-            status = int(head.split(" ", 2)[1])
+            status = int(head[9:12])
             body = bytes(self.buf[i + 4:i + 4 + n])
             del self.buf[:i + 4 + n]
             res["n"] += 1
