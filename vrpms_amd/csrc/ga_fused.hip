@@ -11,7 +11,8 @@
 //     (2P uint8 rows) and every key sit in LDS for the whole call;
 //   * survivors are never copied: slot i of the population points at one
 //     of the 2P rows (prow), and the next children are written into the P
-//     rows no survivor holds (crow, rebuilt by a ballot compaction);
+//     rows no survivor holds (crow: the selection hands over the rows of the
+//     pairs it drops);
 //   * children are scored in place by the headline kernel's split step
 //     (chains.hpp: v_perm + v_dot2 gather addressing, branch-free split,
 //     exact re-walk of the rare lanes that meet the fleet limit);
@@ -72,8 +73,7 @@ struct GaFusedArgs {
   uint32_t pmut, seed_lo, seed_hi;
   uint64_t gen0;
   uint32_t rs;  // LDS bytes per tour row (multiple of 4, rs / 4 odd)
-  uint32_t off_rows, off_pk, off_ck, off_prow, off_crow, off_sk, off_si, off_used, off_bits,
-      off_sink;
+  uint32_t off_rows, off_pk, off_ck, off_prow, off_crow, off_sk, off_si, off_used, off_sink;
   uint32_t off_rk, off_ri;  // child runs of merge_select
   uint16_t* pop_tours;  // [islands][pop][n] in/out
   uint64_t* pop_keys;   // [islands][pop] in/out
@@ -101,11 +101,10 @@ static GaFusedLayout ga_fused_layout(int N, int n, int P) {
   a.off_pk = (uint32_t)off;     off = al16(off + (size_t)P * 8);
   a.off_ck = (uint32_t)off;     off = al16(off + (size_t)P * 8);
   a.off_prow = (uint32_t)off;   off = al16(off + (size_t)P * 2);
-  a.off_crow = (uint32_t)off;   off = al16(off + (size_t)P * 2);
+  a.off_crow = (uint32_t)off;   off = al16(off + (size_t)P * 4);  // two u16 arrays (double buffer)
   a.off_sk = (uint32_t)off;     off = al16(off + (size_t)M * 8);
   a.off_si = (uint32_t)off;     off = al16(off + (size_t)M * 4);
   a.off_used = (uint32_t)off;   off = al16(off + (size_t)16 * VRPMS_GA_NC * N);  // u8 stamp arrays
-  a.off_bits = (uint32_t)off;   off = al16(off + (size_t)2 * P);  // u8 row-in-use flags
   a.off_sink = (uint32_t)off;   off = al16(off + 64);  // one sink dword per wave
   const size_t runs = (size_t)64 * ((P + 63) / 64);  // child runs of merge_select
   a.off_rk = (uint32_t)off;     off = al16(off + runs * 8);
@@ -134,7 +133,10 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
   uint64_t* pk = reinterpret_cast<uint64_t*>(smem + a.off_pk);
   uint64_t* ck = reinterpret_cast<uint64_t*>(smem + a.off_ck);
   uint16_t* prow = reinterpret_cast<uint16_t*>(smem + a.off_prow);
+  // crow[i]: the LDS row child i is bred into; the selection writes the
+  // next generation's (the rows of the pairs it drops) into crow_next
   uint16_t* crow = reinterpret_cast<uint16_t*>(smem + a.off_crow);
+  uint16_t* crow_next = crow + P;
   uint64_t* sk = reinterpret_cast<uint64_t*>(smem + a.off_sk);
   uint32_t* si = reinterpret_cast<uint32_t*>(smem + a.off_si);
   // mk[g] == the current child's stamp: gene g is in the child's A[lo..hi].
@@ -142,7 +144,6 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
   // genes fall in at most 64 distinct dwords -- distinct banks or one
   // address, no bank conflicts; the arrays are cleared before the stamps wrap
   uint8_t* mk = smem + a.off_used + wave * (uint32_t)a.f.N;
-  uint8_t* used = smem + a.off_bits;
   // the breed's sink: a dword per lane in sk (dead until the selection) when
   // it is large enough, so the sink stores of a half-wave hit 32 distinct
   // banks; else one shared dword per wave
@@ -204,9 +205,6 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
       __syncthreads();
       gclr = g;
     }
-    // row-in-use flags for this generation's survivors (read after the
-    // selection, several barriers on)
-    for (int w = threadIdx.x; w < (2 * P + 3) / 4; w += blockDim.x) reinterpret_cast<uint32_t*>(used)[w] = 0u;
     // ---- breed: one child per wavefront at a time --------------------------
     // Lane k of wave w first draws everything random about child w + 16k in
     // parallel (two Philox blocks, both tournaments, the OX1 cut points, the
@@ -440,7 +438,7 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
     // si receives the survivors' LDS rows (merge_select maps them)
     if (sorted_parents) {
       merge_select(pk, ck, P, reinterpret_cast<uint64_t*>(smem + a.off_rk),
-                   reinterpret_cast<uint32_t*>(smem + a.off_ri), sk, si, prow, crow);
+                   reinterpret_cast<uint32_t*>(smem + a.off_ri), sk, si, prow, crow, crow_next);
     } else {
       for (int i = threadIdx.x; i < a.M; i += blockDim.x) {
         sk[i] = i < P ? pk[i] : (i < 2 * P ? ck[i - P] : ~0ull);
@@ -456,6 +454,8 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
         const int i = threadIdx.x + 1024 * k;
         if (i < P) nrow[k] = si[i] < (uint32_t)P ? prow[si[i]] : crow[si[i] - P];
       }
+      for (int i = P + threadIdx.x; i < 2 * P; i += blockDim.x)  // the dropped pairs' rows
+        crow_next[i - P] = si[i] < (uint32_t)P ? prow[si[i]] : crow[si[i] - P];
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
@@ -466,34 +466,15 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
     }
     GA_T(2);
     for (int i = threadIdx.x; i < P; i += blockDim.x) {
-      const uint32_t row = si[i];
-      prow[i] = (uint16_t)row;
+      prow[i] = (uint16_t)si[i];
       pk[i] = sk[i];
-      used[row] = 1;  // survivors hold distinct rows: plain stores
     }
     __syncthreads();
-    // the P rows no survivor holds, in row order, take the next children:
-    // wave 0 compacts 64 rows at a time by ballot prefix counts
-    if (wave == 0) {
-      int base = 0;
-      for (int j0 = 0; j0 < 2 * P; j0 += 512) {
-        uint32_t f[8];  // eight chunks' flags read together
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = used[min(j0 + 64 * j + lane, 2 * P - 1)];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int r = j0 + 64 * j + lane;
-          const bool fr = r < 2 * P && f[j] == 0u;
-          const uint64_t ball = __ballot(fr);
-          if (fr)
-            crow[base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(ball >> 32),
-                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)ball, 0u))] =
-                (uint16_t)r;
-          base += __popcll(ball);
-        }
-      }
+    {  // the rows the selection dropped take the next children
+      uint16_t* t = crow;
+      crow = crow_next;
+      crow_next = t;
     }
-    __syncthreads();
     GA_T(3);
   }
   for (int64_t e = threadIdx.x; e < (int64_t)P * n; e += blockDim.x) {

@@ -168,10 +168,13 @@ VRPMS_DEV bool pair_less(uint64_t ka, uint32_t ia, uint64_t kb, uint32_t ib) {
 // (64 * ceil(P / 64) entries); needs blockDim.x >= 64 * ceil(P / 64).
 // With pmap / cmap, si receives pmap[index] for a parent and
 // cmap[index - P] for a child instead of the index (the fused GA's LDS rows
-// of the survivors).  Every thread of the block must call it.
+// of the survivors), and lost[rank - P] the row of each pair ranked P .. 2P - 1
+// (the rows no survivor holds; lost must not alias cmap).  Every thread of the
+// block must call it.
 VRPMS_DEV void merge_select(const uint64_t* pk, const uint64_t* ck, int P, uint64_t* rk,
                             uint32_t* ri, uint64_t* sk, uint32_t* si,
-                            const uint16_t* pmap = nullptr, const uint16_t* cmap = nullptr) {
+                            const uint16_t* pmap = nullptr, const uint16_t* cmap = nullptr,
+                            uint16_t* lost = nullptr) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int R = (P + 63) >> 6;
   if (w < R) {  // wave-uniform
@@ -221,9 +224,14 @@ VRPMS_DEV void merge_select(const uint64_t* pk, const uint64_t* ck, int P, uint6
     if (two)  // both lanes of the pair active here (the loop bound is per pair)
       part += __builtin_amdgcn_mov_dpp(part, 0xB1, 0xF, 0xF, false);
     const int rank = part + (child ? (c & 63) : e);
-    if (!pad && half <= 0 && rank < P) {
-      sk[rank] = k;
-      si[rank] = pmap ? (uint32_t)(child ? cmap[v - P] : pmap[v]) : v;
+    if (!pad && half <= 0) {
+      const uint32_t row = pmap ? (uint32_t)(child ? cmap[v - P] : pmap[v]) : v;
+      if (rank < P) {
+        sk[rank] = k;
+        si[rank] = row;
+      } else if (lost) {
+        lost[rank - P] = (uint16_t)row;
+      }
     }
   }
   __syncthreads();
