@@ -524,6 +524,50 @@ def test_ga_fused_pop256_cfg2_equals_three_kernel_and_oracle(ctx):
     assert out[2][1] == [k for ks in rkeys for k in ks]
 
 
+@pytest.mark.parametrize("how", ["zero_demands", "split_mode_3"])
+def test_ga_fused_without_carry_form_matches_three_kernel_and_oracle(ctx, how):
+    """The fused GA's scoring walk takes the carry form of the split step only
+    when every demand is >= 1 (ga_fused.hip, template CY): an instance with
+    zero-demand customers, and VRPMS_OPT_SPLIT_MODE = 3 on an ordinary one,
+    run the other instantiation -- same populations and keys as the
+    three-launch path and the Python replay (oracle/search.py)."""
+    torch = torch_()
+    inst = synth.cvrp(60, 5, seed=21, slack=1.05)
+    if how == "zero_demands":
+        dem = inst.demand.copy()
+        dem[1::7] = 0
+        inst = synth.Instance(inst.name, inst.durations, dem, inst.capacities, inst.start_times,
+                              inst.problem, inst.meta)
+    load(ctx, inst)
+    if how == "split_mode_3":
+        ctx.set_split_mode(3)
+    try:
+        islands, pop, n, gens, seed, pmut = 3, 48, inst.n, 3, 99, 0.4
+        P = synth.random_perms(islands * pop, n, seed=5).astype(np.int16)
+        out = []
+        for mode in (0, 2):
+            ctx.set_ga_fused(mode)
+            try:
+                dpop = torch.from_numpy(P.reshape(islands, pop, n).copy()).to(ctx.dev)
+                keys = ctx.eval(dpop.view(islands * pop, n)).view(islands, pop)
+                ctx.ga_generation(dpop, keys, generations=gens, pmut=pmut, seed=seed, gen0=0)
+                out.append((dpop.cpu().numpy(), u64(keys)))
+            finally:
+                ctx.set_ga_fused(0)
+        assert (out[0][0] == out[1][0]).all()
+        assert out[0][1] == out[1][1]
+        sc = scorer(inst)
+        rpop = [[list(r) for r in P.reshape(islands, pop, n)[i]] for i in range(islands)]
+        rkeys = [[sc(t) for t in rpop[i]] for i in range(islands)]
+        pm = min(int(round(pmut * 2**32)), 2**32 - 1)
+        for g in range(gens):
+            rpop, rkeys = search.ga_generation(sc, rpop, rkeys, seed, g, pm)
+        assert out[0][0].tolist() == rpop
+        assert out[0][1] == [k for ks in rkeys for k in ks]
+    finally:
+        ctx.set_split_mode(0)
+
+
 @pytest.mark.parametrize("problem", ["cvrp", "tsp"])
 def test_bf_n13_rank_windows_match_c_restatement(ctx, coracle, problem):
     """The front-end cap (13 customers, 13! = 6.2 G > 2^32 ranks): a window
