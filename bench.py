@@ -27,6 +27,7 @@ Reported beside the value:
 from __future__ import annotations
 
 import argparse
+import collections
 import json
 import math
 import os
@@ -77,6 +78,10 @@ def parse():
                          "the host leg at 32 and at 64 moves per step, the better kept, seed 0's "
                          "host leg repeated for the run-to-run spread; 0 disables)")
     ap.add_argument("--x1000-seeds", type=int, nargs="+", default=[0, 1, 2])
+    ap.add_argument("--x1000-long-seconds", type=float, default=60.0,
+                    help="one longer X-1000 cell (seed 0) at this wall time per side; the host "
+                         "at the move count that won most of the 10-s cells (ties: the "
+                         "smaller), one run; 0 disables")
     ap.add_argument("--td-quality-seconds", type=float, default=10.0,
                     help="wall time per side for the cfg-3 TD-200 x 24 best-cost gaps: the "
                          "uniform fleet (seed 0) and the reference's normal request -- three "
@@ -521,8 +526,8 @@ def quality_summary(out):
         for name, v in (q.get("by_algorithm") or {}).items():
             s[f"cfg2_{name}"] = [v.get("duration_sum"), q["cpu"]["duration_sum"],
                                  r(v.get("gap_vs_host_sa"))]
-    for key, tag in (("quality_x1000", "x1000"), ("quality_tdvrp200", "td200"),
-                     ("quality_tdvrp200_het", "td200het")):
+    for key, tag in (("quality_x1000", "x1000"), ("quality_x1000_long", "x1000_long"),
+                     ("quality_tdvrp200", "td200"), ("quality_tdvrp200_het", "td200het")):
         c = out.get(key) or {}
         for cell in c.get("cells", []):
             if "cpu" in cell:
@@ -1017,6 +1022,20 @@ def main():
                                   seeds=tuple(args.x1000_seeds), host_repeats=args.host_repeats)
         except Exception:
             xq = {"error": traceback.format_exc(limit=3)}
+    xlong = None
+    if args.x1000_long_seconds > 0 and world == 1 and xq is not None and xq.get("cells"):
+        try:
+            progress("X-1000 long cell")
+            won = collections.Counter(c["cpu"]["moves_per_step"] for c in xq["cells"]
+                                      if c.get("cpu"))
+            hm = min(won, key=lambda m: (-won[m], m)) if won else 32
+            xlong = equal_time_cells(ctx, args.x1000_long_seconds, dist,
+                                     with_cpu=(rank == 0 and not args.no_cpu_baseline),
+                                     seeds=(0,), cpu_moves=(hm,), repeat_host=False)
+            xlong["host_rule"] = ("the host move count that won most of the 10-s X-1000 cells "
+                                  "(ties: the smaller), one run")
+        except Exception:
+            xlong = {"error": traceback.format_exc(limit=3)}
     hetq = None
     if args.td_quality_seconds > 0 and world == 1:
         try:
@@ -1098,6 +1117,8 @@ def main():
             out["quality"] = qual
         if xq is not None:
             out["quality_x1000"] = xq
+        if xlong is not None:
+            out["quality_x1000_long"] = xlong
         if tdq is not None:
             out["quality_tdvrp200"] = tdq
         if hetq is not None:
