@@ -2164,6 +2164,12 @@ VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, unsigned cha
     const int nd = dur + delta;
     uint64_t k;
     int bl;
+#if VRPMS_TSPB_AB == 2  // timing attribution only (wrong search): no argmin, lane 0's move
+    if (true) {
+      bl = 0;
+      k = pack_key(0, (uint32_t)wave_bcast(nd, 0), 0);
+    } else
+#endif
     if constexpr (small) {  // (duration << 6 | lane): the same order as (key, lane)
       const uint32_t v = wave_min_u32_uniform(((uint32_t)nd << 6) | (uint32_t)lane);
       bl = (int)(v & 63u);
@@ -2177,6 +2183,9 @@ VRPMS_DEV void tsp_batch_body(const TspBatchArgs& a, const MatT* D, unsigned cha
       const uint32_t dp = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
       accept = accept_test(dp, invT, xa >> 8);
     }
+#if VRPMS_TSPB_AB >= 1  // timing attribution only (wrong search): the tour never moves
+    if (xa != 0xFFFFFFFFu) accept = false;
+#endif
     if (accept) {  // bl is wave-uniform: the winner's move by v_readlane
       Move mb;
       mb.typ = (uint32_t)wave_bcast((int)m.typ, bl);
