@@ -227,6 +227,22 @@ def test_tsp_batch_tsp50_matches_c_restatement(ctx, coracle):
     assert u64(keys) == [int(k) for k in rk]
 
 
+@pytest.mark.parametrize("N", [64, 65, 90])
+def test_tsp_batch_long_tours_match_c_restatement(ctx, coracle, N):
+    """Tours of n = N - 1 >= 63 customers: an accepted move at n < 64 keeps the
+    moved tour in registers (one position per lane), longer tours take the
+    loop over positions -- both sides of that boundary equal the C
+    restatement on 16 requests x 200 steps."""
+    torch = torch_()
+    rng = np.random.default_rng(N)
+    mats = np.stack([synth.random_symmetric(N, rng) for _ in range(16)])
+    M = torch.tensor(mats, dtype=torch.int32, device=ctx.dev)
+    tours, keys = ctx.tsp_batch_sa(M, steps=200, inv_t0=1 / 80.0, inv_alpha=1 / 0.99, seed=3)
+    rt, rk = coracle.tsp_batch_sa(mats, 200, 1 / 80.0, 1 / 0.99, 3)
+    assert (tours.cpu().numpy().view(np.uint16) == rt).all()
+    assert u64(keys) == [int(k) for k in rk]
+
+
 @pytest.mark.parametrize("kind", ["symmetric", "asymmetric", "large"])
 def test_tsp_batch_matches_oracle(ctx, kind):
     """Config-5 throughput kernel: O(1)-delta SA == full-evaluation replay.
