@@ -402,8 +402,11 @@ def test_bench_quality_summary_collects_every_cell():
                              "host_run_to_run": {"runs": [100, 101, 100], "min": 100, "max": 101,
                                                  "rel": 0.01},
                              "median_beyond_spread": True},
+           "quality_x1000_long": {"cells": [cell(0, 97, 100)], "gap_median": -0.03,
+                                  "gpu_better": "1 / 1"},
            "quality_tdvrp200_het": {"cells": [cell(0, 95, 100)], "gap_median": -0.05}}
     s = bench.quality_summary(out)
+    assert s["x1000_long_s0"] == [97, 100, -3.0] and s["x1000_long_gpu_better"] == "1 / 1"
     assert s["cfg2_sa"] == [100, 101, -0.99] and s["cfg2_ga"][2] == 0.99
     assert s["x1000_s0"] == [99, 100, -1.0] and s["x1000_median"] == -1.5
     assert s["x1000_host_spread"]["min"] == 100 and s["x1000_median_beyond_spread"] is True
