@@ -54,9 +54,17 @@ METRIC = "candidate route evals/sec (1/2/4/8 GPU) + best-cost gap at fixed wall 
 # temperature per typical edge (tools/td_quality_scan.py)
 TD_SHAPE = (1024, 64, 128, 0.004)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+# the guide's conflict-free ds_read_b64 rate (MI355X_MICROARCH.md §LDS: 256 B/clk/CU x
+# 256 CUs x 2.4 GHz), in 8-byte gathers per second
+GUIDE_LDS_GATHER_PEAK = 256 * 256 * 2.4e9 / 8
+# the driver keeps a bounded tail of stdout: the LAST line (the one it parses) stays
+# under this many bytes; every detailed leg is printed on an earlier stdout line
+FINAL_LINE_MAX = 8192
+HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                 "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -78,19 +86,207 @@ def parse():
                          "the host leg at 32 and at 64 moves per step, the better kept, seed 0's "
                          "host leg repeated for the run-to-run spread; 0 disables)")
     ap.add_argument("--x1000-seeds", type=int, nargs="+", default=[0, 1, 2])
-    ap.add_argument("--x1000-long-seconds", type=float, default=60.0,
-                    help="one longer X-1000 cell (seed 0) at this wall time per side; the host "
-                         "at the move count that won most of the 10-s cells (ties: the "
-                         "smaller), one run; 0 disables")
+    ap.add_argument("--x1000-long-seconds", type=float, default=0.0,
+                    help="opt-in: one longer X-1000 cell (seed 0) at this wall time per side "
+                         "(e.g. 60); the host at the move count that won most of the 10-s "
+                         "cells (ties: the smaller), one run; 0 (default) disables -- at 60 s "
+                         "it costs ~120 s of the default run's time budget")
     ap.add_argument("--td-quality-seconds", type=float, default=10.0,
                     help="wall time per side for the cfg-3 TD-200 x 24 best-cost gaps: the "
                          "uniform fleet (seed 0) and the reference's normal request -- three "
                          "capacity classes, staggered start times (seeds --het-seeds); 0 disables")
     ap.add_argument("--het-seeds", type=int, nargs="+", default=[0, 1, 2])
+    ap.add_argument("--cpu-standin", action="store_true",
+                    help="launcher / rendezvous rehearsal without a GPU: each rank times a "
+                         "numpy TSP tour-cost pass over gloo and rank 0 prints the final line "
+                         "(not a measurement; tests/test_bench_cpu.py)")
     ap.add_argument("--host-repeats", type=int, default=2,
-                    help="extra runs of X-1000 seed 0's better host leg: the host's run-to-run "
+                    help="extra runs of seed 0's better host leg in every equal-time cell "
+                         "family (X-1000, TD-200, heterogeneous TD-200): the host's run-to-run "
                          "spread over 1 + this many runs")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def launch_ranks(n, argv, child=None, port=None, poll_s=0.2, grace_s=30.0):
+    """`bench.py --gpus N` without a launcher: start N fresh child processes,
+    one per GPU, with the torch.distributed.run environment (RANK, LOCAL_RANK,
+    WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT), and wait
+    for all of them.  The caller has not touched the GPU (nothing here imports
+    torch), so no process that initialised HIP is replaced: the children are
+    new programs.  Rank 0's stdout is this process's stdout (it prints the
+    one JSON line); the other ranks' stdout goes to stderr.  When a rank exits
+    non-zero the others get `grace_s` to finish, then are terminated; the
+    return value is the first non-zero exit status (0 when every rank
+    succeeded).  `child` replaces the command (tests: a stub program)."""
+    import socket
+    import subprocess
+    if port is None:
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+    cmd = list(child) if child else [sys.executable, os.path.abspath(__file__)] + list(argv)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env, stdout=None if r == 0 else sys.stderr))
+    first_bad, deadline = 0, None
+    while True:
+        codes = [p.poll() for p in procs]
+        for c in codes:
+            if c not in (None, 0) and not first_bad:
+                first_bad = c
+                deadline = time.monotonic() + grace_s
+        if all(c is not None for c in codes):
+            break
+        if deadline is not None and time.monotonic() > deadline:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(10)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            break
+        time.sleep(poll_s)
+    if first_bad:
+        print(f"[bench] a rank failed (exit {first_bad}); ranks' exit codes: "
+              f"{[p.returncode for p in procs]}", file=sys.stderr, flush=True)
+    return first_bad
+
+
+def _sig(x, digits=6):
+    """Floats to `digits` significant digits (compact final line)."""
+    if isinstance(x, float):
+        return float(f"{x:.{digits}g}")
+    if isinstance(x, dict):
+        return {k: _sig(v, digits) for k, v in x.items()}
+    if isinstance(x, list):
+        return [_sig(v, digits) for v in x]
+    return x
+
+
+def _pick(d, keys):
+    if not isinstance(d, dict):
+        return None
+    if "error" in d:
+        return {"error": str(d["error"])[-200:]}
+    return {k: d[k] for k in keys if k in d}
+
+
+def final_line(out, limit=FINAL_LINE_MAX):
+    """The bench's LAST stdout line: the headline keys of the contract, the
+    roofline (measured-ceiling frac and the guide-peak frac side by side),
+    and compact cpu_baseline / islands / search / other-config /
+    quality_summary blocks -- the details are earlier stdout lines
+    ({"bench_detail": leg, ...}).  Optional blocks are dropped, least
+    important first, until the line fits in `limit` bytes; the headline and
+    the roofline are never dropped."""
+    line = {k: out[k] for k in HEADLINE_KEYS if k in out}
+    rf = out.get("roofline") or {}
+    line["roofline"] = _pick(rf, ("bound", "achieved", "peak", "unit", "frac",
+                                  "frac_vs_guide_peak", "guide_peak", "traffic", "traffic_unit",
+                                  "kernel", "kernel_ms", "G_per_eval", "peak_source"))
+    if out.get("hbm_roofline"):
+        line["hbm_roofline"] = _pick(out["hbm_roofline"], ("achieved", "peak", "unit", "frac"))
+    if "rows_vs_words_identical" in out:
+        line["rows_vs_words_identical"] = out["rows_vs_words_identical"]
+    cb = out.get("cpu_baseline")
+    if cb:
+        c = _pick(cb, ("value", "unit", "cores", "kind", "sample", "cpu_model",
+                       "parity_on_sample"))
+        if isinstance(cb.get("python_port"), dict):
+            c["python_port_evals_per_s"] = cb["python_port"].get("value")
+        line["cpu_baseline"] = c
+    isl = out.get("islands")
+    if isl:
+        line["islands"] = _pick(isl, ("ranks", "rccl_ranks", "chains_per_gpu", "epochs",
+                                      "chain_steps_per_s", "move_evals_per_s", "exchanges",
+                                      "exchange_ms_mean", "exchange_share_of_wall", "best",
+                                      "exchange_path"))
+    optional = []
+    se = out.get("search")
+    if isinstance(se, dict):
+        s = {}
+        if "error" in se:
+            s["error"] = str(se["error"])[-200:]
+        ga = se.get("ga") or {}
+        if ga.get("fused"):
+            f = ga["fused"]
+            s["ga"] = {"child_evals_per_s": f.get("child_evals_per_s"),
+                       "us_per_generation": 1e6 / f["generations_per_s"]
+                       if f.get("generations_per_s") else None,
+                       "frac_vs_measured": f.get("lds_gather_frac_whole_generation"),
+                       "speedup_fused": ga.get("speedup_fused")}
+        aco = se.get("aco") or {}
+        if aco:
+            s["aco"] = {"ant_tours_per_s": aco.get("ant_tours_per_s"),
+                        "iterations_per_s": aco.get("iterations_per_s"),
+                        "roofline": _pick(aco.get("roofline"), ("achieved", "peak", "unit",
+                                                                "frac", "frac_vs_guide_peak"))}
+        bf = se.get("bf") or {}
+        if bf:
+            s["bf_evals_per_s"] = {k: v.get("evals_per_s") for k, v in bf.items()
+                                   if isinstance(v, dict)}
+        optional.append(("search", s))
+    oc = out.get("other_configs")
+    if isinstance(oc, dict):
+        o = {}
+        if "error" in oc:
+            o["error"] = str(oc["error"])[-200:]
+        for k in ("cfg3_tdvrp200_h24", "cfg4_x1000"):
+            if isinstance(oc.get(k), dict) and "evals_per_s" in oc[k]:
+                o[k] = {"evals_per_s": oc[k]["evals_per_s"],
+                        "l2_frac": (oc[k].get("l2_roofline") or {}).get("frac")}
+        c5 = oc.get("cfg5_tsp50_x10k")
+        if isinstance(c5, dict) and "requests_per_s" in c5:
+            o["cfg5_kernel"] = {"requests_per_s": c5["requests_per_s"],
+                                "frac": (c5.get("roofline") or {}).get("frac")}
+        for k, keys in (("cfg5_http", ("requests_per_s", "ok", "answer_mismatches",
+                                       "banner_equal", "error_bytes_equal")),
+                        ("cfg5_api", ("requests_per_s", "ok", "duration_mismatches")),
+                        ("cfg5_api_one_process", ("requests_per_s", "ok"))):
+            if isinstance(oc.get(k), dict):
+                o[k] = _pick(oc[k], keys)
+        optional.append(("other_configs", o))
+    c1 = out.get("cfg1_main_py")
+    if isinstance(c1, dict):
+        optional.append(("cfg1_main_py", _pick(c1, ("calculate_duration_calls_per_s",))
+                         | {"solve_vrp_problem_calls_per_s":
+                            (c1.get("solve_vrp_problem") or {}).get("calls_per_s")}))
+    if out.get("quality_summary"):
+        optional.append(("quality_summary", out["quality_summary"]))
+    # most important last, so the drop order below is least important first
+    order = ("cfg1_main_py", "other_configs", "search", "quality_summary")
+    optional.sort(key=lambda kv: order.index(kv[0]))
+    for k, v in optional:
+        line[k] = v
+    line["detail"] = "earlier stdout lines {\"bench_detail\": <leg>, \"data\": {...}}"
+    line = _sig(line)
+    line["value"] = out.get("value")          # full precision for the headline number
+    s = json.dumps(line, separators=(",", ":"))
+    for k, _ in optional:
+        if len(s.encode()) <= limit:
+            break
+        line.pop(k, None)
+        s = json.dumps(line, separators=(",", ":"))
+    for k in ("hbm_roofline", "islands", "cpu_baseline"):
+        if len(s.encode()) <= limit:
+            break
+        line.pop(k, None)
+        s = json.dumps(line, separators=(",", ":"))
+    return s
+
+
+def detail_lines(out):
+    """One stdout line per detailed leg (everything final_line shortens)."""
+    for k, v in out.items():
+        if k in HEADLINE_KEYS:
+            continue
+        yield json.dumps({"bench_detail": k, "data": v}, separators=(",", ":"))
 
 
 def make_batch(ctx, C, n, seed, dtype=None):
@@ -785,7 +981,11 @@ def island_leg(ctx, torch, dev, world, rank, dist, epochs=40, steps=500, chains=
         wall, t_ex = float(t[0]), float(t[1])
         key, _ = islands.global_best(r)
     moves = world * chains * chain_steps * 64
-    out = {"workload": "cfg4 X-style CVRP-1000, island SA", "vehicles": x.K,
+    out = {"workload": "cfg4 X-style CVRP-1000, island SA", "ranks": world,
+           # the library communicator's own count (0: the torch fallback ran)
+           "rccl_ranks": ctx.island_world(),
+           "exchange_path": "fallback" if comm_err else "library rccl",
+           "vehicles": x.K,
            "separators": x.K - 1, "window": window,
            "kernel": "sa_seg_kernel (every move priced in O(1) from prefix sums over the "
                      "positions; static symmetric matrix, one capacity)",
@@ -933,8 +1133,69 @@ def pmc_traffic(kernel, grid):
     return None
 
 
+def standin_main(args):
+    """The bench's multi-rank control flow on the CPU (gloo): rendezvous from
+    the launcher's environment, W untimed steps, K steps bracketed by
+    barriers, the max over ranks, rank 0's final line.  A step is a numpy
+    TSP tour-cost pass (random 50-node matrix, 4096 random tours) -- a
+    rehearsal of the plumbing, not a measurement."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(args.seed + rank)
+    n, C = 50, 4096
+    D = rng.integers(1, 100, size=(n, n)).astype(np.int64)
+    tours = np.argsort(rng.random((C, n)), axis=1)
+
+    def step():
+        return int(D[tours, np.roll(tours, -1, axis=1)].sum())
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        import torch
+        t = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    if rank == 0:
+        out = {"metric": METRIC, "value": C * args.steps * world / wall, "unit": "evals/s",
+               "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": wall * 1e3 / args.steps, "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+               "data": "CPU stand-in (launcher rehearsal, not a measurement)",
+               "config": {"workload": "cpu_standin_tsp50", "per_rank_batch": C,
+                          "parallelism": f"islands{world}"},
+               "roofline": {"bound": "none", "achieved": None, "peak": None, "unit": None,
+                            "frac": None, "traffic": None}}
+        print(final_line(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no launcher: start one fresh process per GPU before anything here
+        # touches the GPU (this process never imports torch)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}; "
+                 "launch with --nproc-per-node equal to --gpus")
+    if args.cpu_standin:
+        return standin_main(args)
     import torch
     import torch.distributed as dist
 
@@ -1042,7 +1303,8 @@ def main():
             progress("TD-200 equal-time cells")
             tdq = equal_time_cells(ctx, args.td_quality_seconds, dist,
                                    with_cpu=(rank == 0 and not args.no_cpu_baseline),
-                                   instance="tdvrp200", seeds=(0,), repeat_host=False)
+                                   instance="tdvrp200", seeds=(0,),
+                                   host_repeats=args.host_repeats)
         except Exception:
             tdq = {"error": traceback.format_exc(limit=3)}
         try:
@@ -1050,7 +1312,7 @@ def main():
             hetq = equal_time_cells(ctx, args.td_quality_seconds, dist,
                                     with_cpu=(rank == 0 and not args.no_cpu_baseline),
                                     instance="tdvrp200_het", seeds=tuple(args.het_seeds),
-                                    repeat_host=False)
+                                    host_repeats=args.host_repeats)
         except Exception:
             hetq = {"error": traceback.format_exc(limit=3)}
 
@@ -1092,6 +1354,8 @@ def main():
                        "per_rank_batch": C, "parallelism": f"islands{world}"},
             "roofline": {"bound": "lds_gather", "achieved": evals_s * G, "peak": r_gather,
                          "unit": "gathers/s", "frac": evals_s * G / r_gather,
+                         "frac_vs_guide_peak": evals_s * G / GUIDE_LDS_GATHER_PEAK,
+                         "guide_peak": GUIDE_LDS_GATHER_PEAK,
                          "peak_source": "measured random ds_read_b64 ceiling "
                                         "(vrpms_probe_lds_gather, 1024-lane WGs, 2/CU); the "
                                         "guide's conflict-free ds_read_b64 rate is ~19.7 T/s",
@@ -1147,10 +1411,12 @@ def main():
                 out["cfg1_main_py"] = cfg1_leg()
             except Exception:
                 out["cfg1_main_py"] = {"error": traceback.format_exc(limit=3)}
-        # last key: every equal-time cell in a few hundred bytes, so a
-        # truncated record still holds them
         out["quality_summary"] = quality_summary(out)
-        print(json.dumps(out), flush=True)
+        # details first, one leg per line; the LAST line is the compact record
+        # the driver parses (<= FINAL_LINE_MAX bytes)
+        for ln in detail_lines(out):
+            print(ln, flush=True)
+        print(final_line(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
