@@ -244,3 +244,59 @@ def test_pool_refuses_calls_after_a_death():
             pool.post_many("tsp", "sa", [_body(0, N)])
     finally:
         pool.close()
+
+
+def _raw_http(port, data, timeout=10):
+    """Send raw bytes, return everything the server writes before closing."""
+    import socket
+    s = socket.create_connection(("127.0.0.1", port), timeout=timeout)
+    s.sendall(data)
+    out = b""
+    try:
+        while True:
+            b = s.recv(65536)
+            if not b:
+                break
+            out += b
+    except socket.timeout:
+        pass
+    s.close()
+    return out
+
+
+def test_http_pool_bounds_content_length_and_serves_solve():
+    """a negative or unparsable Content-Length is a 400 and an
+    oversized one a 413, each closing the connection; two pipelined requests
+    on one connection are both answered, in order; POST /solve/<p>/<a> (the
+    remote front-end's route) reaches an owner's App.solve_inline."""
+    N = 10
+    store = _store(8, N)
+    counts = mp.get_context("fork").Array("l", 1)
+    with frontends.FrontEndPool(store, workers=1, devices=(0,), slots_per_worker=64, nmax=16,
+                                chunk=8, launch_factory=_stand_in(counts),
+                                app_factory=_fake_app(store), listen=("127.0.0.1", 0)) as pool:
+        neg = _raw_http(pool.port, b"POST /api/tsp/sa HTTP/1.1\r\nContent-Length: -5\r\n\r\n")
+        bad = _raw_http(pool.port, b"POST /api/tsp/sa HTTP/1.1\r\nContent-Length: x\r\n\r\n")
+        big = _raw_http(pool.port, b"POST /api/tsp/sa HTTP/1.1\r\nContent-Length: %d\r\n\r\n"
+                        % (frontends.MAX_BODY + 1))
+        b1, b2 = _body(1, N), _body(2, N)
+        piped = _raw_http(pool.port, b"POST /api/tsp/sa HTTP/1.1\r\nContent-Length: %d\r\n\r\n"
+                          % len(b1) + b1 + b"POST /api/tsp/sa HTTP/1.1\r\nConnection: close\r\n"
+                          b"Content-Length: %d\r\n\r\n" % len(b2) + b2, timeout=30)
+        D = synth.random_symmetric(N, np.random.default_rng(3)).tolist()
+        inline = json.dumps({"durations": D, "customers": list(range(1, N)), "startNode": 0,
+                             "startTime": 0}).encode()
+        solve = _raw_http(pool.port, b"POST /solve/tsp/sa HTTP/1.1\r\nConnection: close\r\n"
+                          b"Content-Length: %d\r\n\r\n" % len(inline) + inline, timeout=30)
+    assert neg.startswith(b"HTTP/1.1 400") and b"Connection: close" in neg
+    assert bad.startswith(b"HTTP/1.1 400")
+    assert big.startswith(b"HTTP/1.1 413")
+    assert piped.count(b"HTTP/1.1 200") == 2
+    bodies = [json.loads(x.split(b"\r\n\r\n", 1)[1]) for x in piped.split(b"HTTP/1.1 ")[1:]]
+    for i, body in zip((1, 2), bodies):
+        Di = np.asarray(store.durations[i])
+        path = list(range(1, N)) + [0]
+        assert body["message"]["duration"] == int(Di[[0] + path[:-1], path].sum())
+    assert solve.startswith(b"HTTP/1.1 200"), solve[:300]
+    want = _fake_app(store)(0).solve_inline("tsp", "sa", inline)
+    assert json.loads(solve.split(b"\r\n\r\n", 1)[1]) == want[1]

@@ -36,6 +36,24 @@ def _classes(inst, fracs, shuffle=False):
     return dataclasses.replace(inst, capacities=caps)
 
 
+def _tight(inst, fracs, shuffle=False):
+    """Capacity classes whose smallest vehicle is below the largest demand
+    (half of it): some customers fit only some vehicles, so sa_td_kernel
+    takes its non-FAST walk (the per-token capacity branch, max_dem >
+    min_cap) -- ADVICE r5."""
+    K = len(inst.capacities)
+    base = int(inst.capacities[0])
+    small = max(1, int(inst.demand.max()) // 2)
+    caps = np.array([max(int(base * fracs[k * len(fracs) // K]), int(inst.demand.max()))
+                     for k in range(K)], dtype=np.int64)
+    caps[K // 2::3] = small
+    if shuffle:
+        np.random.default_rng(K + 1).shuffle(caps)
+    out = dataclasses.replace(inst, capacities=caps)
+    assert int(out.capacities.min()) < int(out.demand.max())
+    return out
+
+
 def _starts(inst, base=420):
     st = np.arange(inst.K, dtype=np.int64) * 37 % 240 + base
     return dataclasses.replace(inst, start_times=st)
@@ -131,6 +149,20 @@ TD_CASES = [
     # tiny tours (2 and 3 tokens, every move touches the ends)
     ("td2", lambda: synth.td_cvrp(2, 1, seed=32), "nosep", 4, 20, 1 / 50.0, 0, 0, 64),
     ("td3_seps", lambda: synth.td_cvrp(3, 2, seed=33), "random", 4, 20, 1 / 50.0, 0, 0, 64),
+    # round 6: a vehicle class smaller than the largest demand --
+    # the non-FAST variant (per-token capacity branch) -- packed and random
+    # separators, staggered starts, asymmetric hours, W = 2
+    ("td200_tight_pack_starts", lambda: _starts(_tight(synth.td_cvrp(200, 16, seed=41),
+                                                       (1.3, 1.0))), "pack", 8, 80, 1 / 200.0,
+     16, 2, 64),
+    ("td200_tight_random_seps", lambda: _tight(synth.td_cvrp(200, 16, seed=42), (1.2, 1.0),
+                                               shuffle=True), "random", 8, 60, 1 / 200.0, 0, 0,
+     64),
+    ("td150_tight_asym_hot", lambda: _starts(_tight(_asym_td(synth.td_cvrp(150, 12, seed=43), 6),
+                                                    (1.3, 0.9))), "pack", 8, 60, 1e-7, 0, 0, 64),
+    ("td200_tight_m128", lambda: _starts(_tight(synth.td_cvrp(200, 16, seed=44), (1.3, 1.0),
+                                                shuffle=True)), "random", 4, 60, 1 / 200.0, 16,
+     2, 128),
 ]
 
 

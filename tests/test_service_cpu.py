@@ -369,7 +369,10 @@ def test_repeated_device_list_does_not_deadlock():
     assert all(not lk.locked() for lk in app.locks.values())
 
 
-@pytest.mark.parametrize("mt,want", [(True, [0, 1]), (False, None)])
+@pytest.mark.parametrize("mt,want", [(True, [0, 1]), (False, None), ("false", None),
+                                     ("0", None), (0, None), ("TRUE", [0, 1]), (1, [0, 1]),
+                                     # not a boolean: the size rule (3 customers: one device)
+                                     ("maybe", None), ([1], None)])
 def test_multithreaded_selects_island_model(mt, want):
     """VRP GA's multiThreaded (api/parameters.py:20): true runs the island
     model over every device, false one device -- whatever the request size
@@ -412,3 +415,23 @@ def test_bench_quality_summary_collects_every_cell():
     assert s["x1000_host_spread"]["min"] == 100 and s["x1000_median_beyond_spread"] is True
     assert s["td200het_s0"] == [95, 100, -5.0]
     assert list(out) != [] and "units" in s
+
+
+@pytest.mark.parametrize("knob,value", [("islands", 10**6), ("ants", 10**7), ("chains", 2**30),
+                                        ("pop", 1), ("steps", 0), ("window", -1),
+                                        ("window_types", 8), ("chains", True), ("pop", [4])])
+def test_inline_knobs_out_of_range_are_400(knob, value):
+    """/solve knobs from the network are range-checked (a 400,
+    never an allocation); in-range values pass through as ints."""
+    seen = []
+
+    def fake_solve(problem, algorithm, params, knobs, locations, durations):
+        seen.append(knobs.get("inline"))
+        return {"duration": 1, "vehicle": [0, 1, 0]}
+
+    app = service.App(store(), solve=fake_solve)
+    body = {"durations": MATRIX, "customers": [1], "startNode": 0, "startTime": 0}
+    st, res = app.solve_inline("tsp", "sa", json.dumps(dict(body, knobs={knob: value})).encode())
+    assert st == 400 and knob in res["errors"][0]["reason"] and not seen
+    st, _ = app.solve_inline("tsp", "sa", json.dumps(dict(body, knobs={knob: 7})).encode())
+    assert st == 200 and seen == [{knob: 7}]

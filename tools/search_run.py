@@ -4,8 +4,10 @@
   cfg 5: tsp_batch_sa_kernel, 10,000 TSP-50 requests x 1000 SA steps
   cfg 2: sa_packed_kernel, 4096 SA chains on CVRP-100 K = 8, 400-step epochs
   cfg 2: ga_fused_kernel, 256 islands x 256, 20 generations per call
-  cfg 4: sa_route_kernel, 1024 SA chains on X-1000 with K - 1 separators
-         (first-fit start, windowed 2-opt), 100-step epochs
+  cfg 2: aco_construct_kernel, 64 colonies x 64 ants, 5 iterations per epoch
+         (one construct launch per iteration: n = 100 ant steps)
+  cfg 4: sa_seg_kernel, 1024 SA chains x 128 moves on X-1000 with K - 1
+         separators (first-fit start, windowed 2-opt), 100-step epochs
 usage: search_run.py [reps]"""
 import os
 import sys
@@ -35,12 +37,15 @@ for _ in range(reps):
 ga = runners.GARunner(ctx, inst.n, islands=256, pop=256, seed=1, gens_per_epoch=20)
 for _ in range(reps):
     ga.epoch()
+aco = runners.ACORunner(ctx, inst.n, colonies=64, ants=64, seed=1, iters_per_epoch=5)
+for _ in range(reps):
+    aco.epoch()
 torch.cuda.synchronize()
 x = synth.x_style(1000, seed=0)
 ctx.set_instance(CVRP, x.durations, x.demand, x.capacities, x.start_times)
 rx = runners.SARunner(ctx, x.n, chains=1024, total_steps=100 * reps, durations=x.durations,
-                      n_sep=x.K - 1, window=32, window_types=2, start="pack")
+                      n_sep=x.K - 1, window=32, window_types=2, start="pack", moves=128)
 for _ in range(reps):
     rx.epoch(100)
 torch.cuda.synchronize()
-print("done", r.best()[0], ga.best()[0], rx.best()[0])
+print("done", r.best()[0], ga.best()[0], aco.best()[0], rx.best()[0])

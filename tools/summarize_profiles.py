@@ -66,6 +66,9 @@ def main():
         shutil.copy(stats[0], os.path.join(PROF, f"{tag}_kernel_stats.csv"))
     per_grid(tag)
     means, meta = pmc_means(kernel)
+    if not means:
+        # round 5 wrote an empty record because no pmc_* pass had run: refuse
+        sys.exit(f"no PMC rows for '{kernel}' under gpurun_out/pmc_*/: run the pmc step first")
     rec = {"tag": tag, "kernel_filter": kernel, **meta, "counters_mean_per_dispatch": means}
     if "FETCH_SIZE" in means and "WRITE_SIZE" in means:
         fetch = means["FETCH_SIZE"] * 1024 * 2     # gfx950: FETCH_SIZE is half of the bytes

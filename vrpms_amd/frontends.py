@@ -163,7 +163,10 @@ def _owner_main(dev, arena, submit_q, done_qs, stats_q, make_launch, make_app, w
                 app["app"] = make_app(dev)
             a = app["app"]
             before = len(a.store.solutions)
-            status, resp = a.post(problem, algorithm, body)
+            if problem.startswith("solve:"):    # POST /solve/<problem>/<algo> (vrpms_amd.remote)
+                status, resp = a.solve_inline(problem[6:], algorithm, body)
+            else:
+                status, resp = a.post(problem, algorithm, body)
             rows = list(a.store.solutions[before:])
             del a.store.solutions[before:]
             done_qs[w].put(("post", token, status, resp, rows))
@@ -420,7 +423,10 @@ def _worker_main(w, arena, lo, hi, req_q, resp_q, submit_qs, done_q, store, batc
 # HTTP front: every worker listens on the same port (SO_REUSEPORT, the kernel
 # spreads the connections) and serves the reference's routes itself
 # ---------------------------------------------------------------------------
-_REASON = {200: "OK", 400: "Bad Request", 404: "Not Found", 501: "Not Implemented"}
+_REASON = {200: "OK", 400: "Bad Request", 404: "Not Found", 413: "Payload Too Large",
+           431: "Request Header Fields Too Large", 501: "Not Implemented"}
+MAX_BODY = 64 << 20        # bytes of one request body (an inline /solve matrix fits)
+MAX_HEAD = 64 << 10        # bytes of one request's header section
 
 
 def _listen_socket(host: str, port: int):
@@ -445,6 +451,7 @@ class _HttpConn(asyncio.Protocol):
 
     def connection_made(self, tr):
         self.tr = tr
+        self.loop = asyncio.get_running_loop()
 
     def connection_lost(self, exc):
         self.tr = None
@@ -467,6 +474,8 @@ class _HttpConn(asyncio.Protocol):
             return
         i = self.buf.find(b"\r\n\r\n")
         if i < 0:
+            if len(self.buf) > MAX_HEAD:
+                self._refuse(431)
             return
         lines = bytes(self.buf[:i]).decode("latin-1").split("\r\n")
         try:
@@ -478,7 +487,16 @@ class _HttpConn(asyncio.Protocol):
         for ln in lines[1:]:
             k, _, v = ln.partition(":")
             hdrs[k.strip().lower()] = v.strip()
-        n = int(hdrs.get("content-length", 0) or 0)
+        # Content-Length is the client's claim: not a number or negative is a
+        # 400, beyond MAX_BODY a 413, and the connection closes either way
+        # (its byte stream can no longer be framed)
+        try:
+            n = int(hdrs.get("content-length", 0) or 0)
+        except ValueError:
+            n = -1
+        if n < 0 or n > MAX_BODY:
+            self._refuse(400 if n < 0 else 413)
+            return
         if len(self.buf) < i + 4 + n:
             return
         body = bytes(self.buf[i + 4:i + 4 + n])
@@ -488,6 +506,15 @@ class _HttpConn(asyncio.Protocol):
         close = conn == "close" or (version == "HTTP/1.0" and conn != "keep-alive")
         self.busy = True
         self.server.handle(self, method, path, body, close)
+
+    def _refuse(self, status):
+        self.busy = True          # nothing more is parsed from this connection
+        self.buf.clear()
+        if self.tr is not None:
+            self.tr.write((f"{self.version} {status} {_REASON[status]}\r\nContent-Length: 0"
+                           "\r\nConnection: close\r\n\r\n").encode("latin-1"))
+            self.tr.close()
+            self.tr = None
 
     def respond(self, status, body: bytes, ctype="application/json", close=False, extra=()):
         if self.tr is None:
@@ -505,7 +532,10 @@ class _HttpConn(asyncio.Protocol):
             self.tr.close()
             self.tr = None
         else:
-            self._next()
+            # the next pipelined request is parsed from the event loop, not
+            # from inside this call: respond() can run inside a flush() that
+            # is still walking its pending lists
+            self.loop.call_soon(self._next)
 
 
 def _http_worker_main(w, arena, lo, hi, host, port, submit_qs, done_q, store, batchable_nmax,
@@ -576,11 +606,17 @@ def _http_worker_main(w, arena, lo, hi, host, port, submit_qs, done_q, store, ba
                              ("Access-Control-Allow-Origin: *", "Access-Control-Allow-Methods: *",
                               "Access-Control-Allow-Headers: *", "Access-Control-Allow-Headers: *"))
                 return
-            if method != "POST" or path not in banners:
+            parts = path.split("/")
+            if method == "POST" and len(parts) == 4 and parts[1] == "solve" and \
+                    parts[2] in ("tsp", "vrp") and parts[3] in service.TITLES:
+                # the remote front-end's inline route (vrpms_amd.remote), run by
+                # an owner's App.solve_inline
+                key = ("solve:" + parts[2], parts[3])
+            elif method != "POST" or path not in banners:
                 conn.respond(404 if path not in banners else 501, b"", None, close)
                 return
-            _, _, problem, algorithm = path.split("/")
-            key = (problem, algorithm)
+            else:
+                key = (parts[2], parts[3])
             pending.setdefault(key, []).append((body, conn, close))
             if len(pending[key]) >= chunk:
                 flush()
@@ -622,10 +658,10 @@ def _http_worker_main(w, arena, lo, hi, host, port, submit_qs, done_q, store, ba
     stats_q.put(("worker", fe.st))
 
 
-def _default_app(store, seed, steps):
+def _default_app(store, seed, steps, max_seconds=None):
     def make_app(dev):
         from . import service
-        return service.App(store, device=dev, seed=seed)
+        return service.App(store, device=dev, seed=seed, max_seconds=max_seconds)
     return make_app
 
 

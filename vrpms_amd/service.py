@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import sys
 import threading
 import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
@@ -49,6 +50,37 @@ _COMMON = {
 # in its "knobs" object (vrpms_amd.remote forwards them): name -> type
 INLINE_KNOBS = {"steps": int, "separators": int, "window": int, "chains": int,
                 "window_types": int, "pop": int, "islands": int, "colonies": int, "ants": int}
+# their accepted ranges (inclusive): a value from the network outside them is a
+# 400, never an allocation (islands = 10**6 or chains = 2**30 would
+# exhaust device memory while the request holds every device lock)
+KNOB_RANGES = {"steps": (1, 10**8), "separators": (0, 4096), "window": (0, 65535),
+               "chains": (1, 1 << 16), "window_types": (0, 7), "pop": (2, 4096),
+               "islands": (1, 4096), "colonies": (1, 4096), "ants": (1, 4096)}
+
+
+def check_knob(name, value):
+    """INLINE_KNOBS[name](value), range-checked by KNOB_RANGES (ValueError)."""
+    if isinstance(value, bool) or not isinstance(value, (int, float, str)):
+        raise ValueError(f"knob {name} must be an integer")
+    v = INLINE_KNOBS[name](value)
+    lo, hi = KNOB_RANGES[name]
+    if not lo <= v <= hi:
+        raise ValueError(f"knob {name}={v} outside [{lo}, {hi}]")
+    return v
+
+
+def multi_threaded(value):
+    """The VRP GA `multiThreaded` value (api/parameters.py:20 passes the raw
+    JSON through): a JSON boolean as is; the strings "true"/"1" and "false"/
+    "0" (any case) and the numbers 1 / 0 as those booleans; anything else is
+    None -- the size rule decides (bool("false") was True)."""
+    if isinstance(value, bool):
+        return value
+    if isinstance(value, (int, float)) and value in (0, 1):
+        return bool(value)
+    if isinstance(value, str) and value.strip().lower() in ("true", "1", "false", "0"):
+        return value.strip().lower() in ("true", "1")
+    return None
 # algorithm knobs (api/parameters.py:18-23; every other algorithm takes none)
 _KNOBS = {("vrp", "ga"): [("multiThreaded", "multi_threaded"),
                           ("randomPermutationCount", "random_permutationCount"),
@@ -331,8 +363,8 @@ class App:
         n = len(params.get("customers") or []) if problem == "tsp" else \
             max(0, len(locations or []) - 1)
         knobs = dict(knobs)
-        mt = knobs.get("multi_threaded")
-        islands = n > self.island_min_n if mt is None else bool(mt)
+        mt = multi_threaded(knobs.get("multi_threaded"))
+        islands = n > self.island_min_n if mt is None else mt
         if len(self.devices) > 1 and algorithm != "bf" and islands:
             held = sorted(set(self.devices))   # each lock once, in one global order
             for d in held:
@@ -488,7 +520,7 @@ class App:
             bad = sorted(k for k in inline if k not in INLINE_KNOBS)
             if bad:
                 raise ValueError(f"unknown knob(s) {bad}; known: {sorted(INLINE_KNOBS)}")
-            knobs["inline"] = {k: INLINE_KNOBS[k](v) for k, v in inline.items()}
+            knobs["inline"] = {k: check_knob(k, v) for k, v in inline.items()}
         except (TypeError, ValueError) as e:
             return 400, {"success": False,
                          "errors": [{"what": "Invalid request", "reason": str(e)}]}
@@ -613,10 +645,19 @@ def main(argv=None):
     if devices:   # a GPU listed twice would only queue behind itself
         devices = list(dict.fromkeys(devices))
     if args.workers > 0:
-        from .frontends import FrontEndPool
+        from .frontends import FrontEndPool, _default_app
+        if devices and len(devices) > 1:
+            # each GPU owner holds one device: large requests run on one
+            print("vrpms_amd service: --workers serves every device through its own owner "
+                  "process; requests are not run as an island model across --devices",
+                  file=sys.stderr, flush=True)
+        # --batch-tsp is implied (the owners batch /api/tsp/sa); --max-seconds
+        # caps every unbatched solve in the owners' App
         pool = FrontEndPool(store, workers=args.workers, devices=devices or [args.device],
                             steps=args.batch_steps, seed=args.seed,
-                            window_s=args.batch_window_ms * 1e-3, listen=(args.host, args.port))
+                            window_s=args.batch_window_ms * 1e-3, listen=(args.host, args.port),
+                            app_factory=_default_app(store, args.seed, args.batch_steps,
+                                                     args.max_seconds))
         print(f"vrpms_amd service ({args.workers} front-end processes) on "
               f"http://{args.host}:{pool.port}/api", flush=True)
         try:
