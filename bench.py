@@ -1060,10 +1060,24 @@ def search_lines(ctx, torch, dev, r_gather, seed=0):
     aco = runners.ACORunner(ctx, inst.n, colonies=colonies, ants=ants, seed=seed,
                             iters_per_epoch=iters)
     wall, dev_s = timed(aco.epoch, 3)
+    # roofline: the roulette reads the weight (tau >> 8) * eta of every free
+    # node at every ant step -- n - s of them at step s, n (n + 1) / 2 per
+    # ant -- one 8-byte LDS gather each (aco_construct_lds_kernel), against
+    # the LDS-gather peaks; timed over the whole iteration (construct +
+    # eval_cvrp_words2 scoring + the fused update), so a lower bound for the
+    # construct kernel alone (its own time: rocprofv3 stats in profiles/)
+    reads = inst.n * (inst.n + 1) // 2
+    rd_s = colonies * ants * iters * reads / dev_s
     out["aco"] = {"workload": "cfg2 CVRP-100, integer max-min ACO", "colonies": colonies,
                   "ants": ants, "scoring_kernel": "eval_cvrp_words2",
+                  "construct_kernel": "aco_construct_lds_kernel (colony weights staged in LDS)",
                   "iterations_per_s": iters / dev_s, "ant_tours_per_s": colonies * ants * iters / dev_s,
                   "wall_iterations_per_s": iters / wall,
+                  "roofline": {"bound": "lds_gather", "weight_reads_per_ant": reads,
+                               "achieved": rd_s, "peak": r_gather, "unit": "gathers/s",
+                               "frac": rd_s / r_gather if r_gather else None,
+                               "frac_vs_guide_peak": rd_s / GUIDE_LDS_GATHER_PEAK,
+                               "timed": "whole iteration (construct + scoring + update)"},
                   "best": {"duration_sum": (aco.best()[0] >> 28) & (2**28 - 1)}}
     del aco
     # BF: exhaustive lexicographic ranks on CVRP-n sub-instances (K = 3)

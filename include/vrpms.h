@@ -162,6 +162,11 @@ int vrpms_eval_path(vrpms_ctx* ctx, int32_t perm_bytes, int64_t ld, const void* 
  *   (0 = auto: moves / 64 up to 4 while every chain's wavefronts stay
  *   resident; 1..4 force, A/B -- the trajectories do not depend on it). */
 #define VRPMS_OPT_SEG_WAVES 11
+/*   VRPMS_OPT_ACO_CONSTRUCT: 0 = auto (ant construction reads the colony's
+ *   weights (tau >> 8) * eta from LDS, staged once per iteration by a
+ *   workgroup of up to 16 ants of one colony, whenever N * N * 8 bytes fit;
+ *   else from L2), 2 = force the L2 path; A/B -- the tours are the same. */
+#define VRPMS_OPT_ACO_CONSTRUCT 12
 int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value);
 
 /* Decode ONE giant tour into the result dict of api/vrp/ga/index.py:49-53

@@ -395,6 +395,51 @@ def test_aco_iterations_match_oracle_at_size(ctx, name, maker):
         assert all((got_tau[c] == rtau[c]).all() for c in range(colonies))
 
 
+ACO_STAGED = [
+    # (name, instance, colonies, ants): ants not a multiple of the 16-ant
+    # workgroup (16 + 16 + 8), one ant per colony, the largest N whose
+    # weights fit the LDS (141 * 141 * 8 B + tour buffers), the TSP layout
+    ("cvrp100_40ants", lambda: synth.cvrp(100, 8, seed=0), 3, 40),
+    ("cvrp60_1ant", lambda: synth.cvrp(60, 5, seed=4), 5, 1),
+    ("cvrp140_17ants", lambda: synth.cvrp(140, 10, seed=6), 2, 17),
+    ("tsp40_64ants", lambda: synth.Instance("tsp40", synth.random_symmetric(
+        40, np.random.default_rng(8))[None], None, None, np.array([0]), "tsp"), 2, 64),
+]
+
+
+@pytest.mark.parametrize("name,maker,colonies,ants", ACO_STAGED, ids=[s[0] for s in ACO_STAGED])
+def test_aco_lds_staged_construct_matches_l2_path_and_oracle(ctx, name, maker, colonies, ants):
+    """Round 6: the LDS-staged construction (VRPMS_OPT_ACO_CONSTRUCT auto)
+    gives the same tours, keys, iteration bests and tau as the L2 path
+    (option 2) and as oracle/search.py."""
+    inst = maker()
+    load(ctx, inst)
+    tau0 = 1 << 20
+    runs = []
+    for mode in (0, 2):
+        ctx.set_aco_construct(mode)
+        try:
+            tau, eta = ctx.aco_init(colonies, tau0)
+            out = []
+            for it in range(2):
+                tours, keys, ib = ctx.aco_iteration(tau, eta, ants, seed=13, it=it, evap_shift=3,
+                                                    tau_min=1 << 10, tau_max=1 << 30)
+                out.append((tours.cpu().numpy().tolist(), u64(keys), ib.cpu().tolist(),
+                            (tau.cpu().numpy().astype(np.int64) & 0xFFFFFFFF).tolist()))
+            runs.append(out)
+        finally:
+            ctx.set_aco_construct(0)
+    assert runs[0] == runs[1]
+    ref_eta = search.aco_eta(inst.durations[0])
+    rtau = [np.full((inst.N, inst.N), tau0, dtype=np.int64) for _ in range(colonies)]
+    sc = scorer(inst)
+    for it in range(2):
+        rt, rk, rib = search.aco_iteration(sc, rtau, ref_eta, ants, inst.n, 13, it, 3, 1 << 10,
+                                           1 << 30)
+        assert runs[0][it][0] == rt
+        assert runs[0][it][1] == [k for ks in rk for k in ks]
+
+
 @pytest.mark.parametrize("name,maker", SMALL, ids=[s[0] for s in SMALL])
 def test_bf_matches_oracle(ctx, name, maker):
     inst = maker()

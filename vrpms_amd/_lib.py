@@ -36,6 +36,7 @@ OPT_SA_ROUTE = 8
 OPT_ROUTE_WG_PER_CU = 9
 OPT_ISLAND_TIMEOUT_S = 10
 OPT_SEG_WAVES = 11
+OPT_ACO_CONSTRUCT = 12
 OBJ_SUM = 0
 OBJ_MAX = 1
 INJECT_WORST = 0

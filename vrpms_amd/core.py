@@ -188,6 +188,10 @@ class Context:
         """sa_seg_kernel wavefronts per chain: 0 = auto, 1..4 force (A/B)."""
         check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_SEG_WAVES, int(w)))
 
+    def set_aco_construct(self, mode: int):
+        """0 = auto (LDS-staged colony weights when they fit), 2 = the L2 path (A/B)."""
+        check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_ACO_CONSTRUCT, int(mode)))
+
     def set_ga_fused(self, mode: int):
         """0 = auto (fused one-workgroup-per-island GA when it fits), 2 = three kernels."""
         check(self.lib.vrpms_set_option(self._ctx, _lib.OPT_GA_FUSED, int(mode)))

@@ -296,6 +296,12 @@ int vrpms_set_option(vrpms_ctx* ctx, int32_t option, int32_t value) {
     ctx->opt_seg_waves = value;
     return VRPMS_OK;
   }
+  if (option == VRPMS_OPT_ACO_CONSTRUCT) {
+    if (value != 0 && value != 2)
+      return fail(VRPMS_EINVAL, "vrpms_set_option: ACO construct must be 0 (auto) or 2 (L2 path)");
+    ctx->opt_aco_construct = value;
+    return VRPMS_OK;
+  }
   if (option == VRPMS_OPT_ISLAND_TIMEOUT_S) {
     if (value <= 0)
       return fail(VRPMS_EINVAL, "vrpms_set_option: island timeout must be > 0 seconds");

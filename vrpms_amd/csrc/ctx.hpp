@@ -69,6 +69,7 @@ struct vrpms_ctx {
   int comm_rank = 0, comm_world = 1;
   int opt_island_timeout_s = 120;  // VRPMS_OPT_ISLAND_TIMEOUT_S
   int opt_seg_waves = 0;           // VRPMS_OPT_SEG_WAVES (0 auto, 1..4 force)
+  int opt_aco_construct = 0;       // VRPMS_OPT_ACO_CONSTRUCT (0 auto, 2 = the L2 path)
 };
 
 namespace vrpms {

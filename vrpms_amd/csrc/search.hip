@@ -1798,6 +1798,92 @@ __global__ __launch_bounds__(256) void aco_construct_kernel(AcoArgs a) {
   }
 }
 
+// The register path with the colony's weights staged in LDS (N * N * 8 bytes
+// fit beside the tour buffers): a workgroup is up to 16 ants of ONE colony
+// (wpg wavefronts), which first forms w[i][j] = (tau[i][j] >> 8) * eta[i][j]
+// -- the same uint64 products the L2 path forms at every step -- for the
+// whole colony, coalesced, once per iteration; then each step of each ant
+// reads its row with one ds_read_b64 per chunk (conflict-free: consecutive
+// lanes, consecutive entries) instead of a dependent tau + eta round trip to
+// L2 and a 64-bit multiply.  Philox streams (colony * ants + ant, step), the
+// roulette and the pick are the register path's, so the tours are the same.
+template <bool WORDS, int CH>
+__global__ __launch_bounds__(1024) void aco_construct_lds_kernel(AcoArgs a, int wpg) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int N = a.N, n = a.n;
+  uint64_t* Wt = reinterpret_cast<uint64_t*>(smem);  // [N][N]
+  uint8_t* tbuf = smem + (((size_t)N * N * 8 + 15) & ~(size_t)15);
+  const int groups = (a.ants + wpg - 1) / wpg;
+  const int colony = (int)blockIdx.x / groups;
+  const int ant0 = ((int)blockIdx.x % groups) * wpg;
+  {
+    const uint32_t* T = a.tau + (int64_t)colony * N * N;
+    const int NN = N * N;
+    for (int e = threadIdx.x; e < NN; e += blockDim.x)
+      Wt[e] = (uint64_t)(T[e] >> 8) * a.eta[e];
+  }
+  __syncthreads();
+  const int wave = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
+  const int ant = ant0 + wave;
+  if (ant >= a.ants) return;  // (no barrier after this point)
+  uint8_t* tb = tbuf + wave * 256;
+  const int64_t gid = (int64_t)colony * a.ants + ant;
+  const int64_t total_ants = (int64_t)a.colonies * a.ants;
+  if constexpr (WORDS) {
+    for (int q = n + lane; q < 256; q += 64) tb[q] = 0;
+  }
+  uint16_t* out = a.tours + gid * n;
+  uint32_t vm = lane == 0 ? 1u : 0u;  // bit c: node lane + 64c visited (or past N); depot
+#pragma unroll
+  for (int c = 0; c < CH; ++c)
+    if (lane + 64 * c >= N) vm |= 1u << c;
+  uint32_t cur = 0;
+  for (int s = 0; s < n; ++s) {
+    const u32x4 r = philox((uint32_t)a.iter, (uint32_t)(a.iter >> 32), (uint32_t)gid, (uint32_t)s,
+                           a.seed_lo, a.seed_hi);
+    const uint64_t* Wr = Wt + cur * (uint32_t)N;
+    uint64_t w[CH], inc[CH], ct[CH], tot = 0;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) w[c] = !((vm >> c) & 1u) ? Wr[lane + 64 * c] : 0ull;
+    uint32_t pick = 0xffffffffu;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      inc[c] = w[c];
+      ct[c] = wave_scan_add_u64(inc[c]);
+      tot += ct[c];
+      const uint64_t fb = __ballot(!((vm >> c) & 1u));
+      if (pick == 0xffffffffu && fb) pick = (uint32_t)(64 * c + __ffsll((long long)fb) - 1);
+    }
+    if (tot != 0) {  // else: the first free node
+      const uint64_t rr = umod64(((uint64_t)r.y << 32) | r.x, tot);
+      uint64_t run = 0;
+      uint32_t hp = 0xffffffffu;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const uint64_t ball = __ballot(w[c] > 0 && run + inc[c] > rr);
+        if (hp == 0xffffffffu && ball) hp = (uint32_t)(64 * c + __ffsll((long long)ball) - 1);
+        run += ct[c];
+      }
+      if (hp != 0xffffffffu) pick = hp;  // always: tot > rr
+    }
+    if (lane == 0) {
+      out[s] = (uint16_t)pick;
+      if constexpr (WORDS) tb[s] = (uint8_t)pick;
+    }
+    if (lane == (int)(pick & 63u)) vm |= 1u << (pick >> 6);
+    cur = pick;
+  }
+  if constexpr (WORDS) {
+    wave_sync();
+    const int nw = (n + 3) >> 2;
+    for (int w = lane; w < nw; w += 64)
+      a.words[(int64_t)w * total_ants + gid] = reinterpret_cast<const uint32_t*>(tb)[w];
+  }
+}
+
+// LDS bytes of aco_construct_lds_kernel (weights + a 256-byte tour buffer per wavefront)
+static size_t aco_lds_bytes(int N, int wpg) { return (((size_t)N * N * 8 + 15) & ~(size_t)15) + 256 * (size_t)wpg; }
+
 struct AcoUpdateArgs {
   int colonies, ants, n, N;
   uint32_t evap_shift, tau_min, tau_max;
@@ -2605,8 +2691,26 @@ extern "C" int vrpms_aco_iteration(vrpms_ctx* ctx, const vrpms_aco_params* p, ui
             d_tau, d_eta, d_tours, wbuf};
   const size_t lds = ((4 * (((size_t)in.N + 31) / 32) * 4 + 15) & ~(size_t)15) + (words ? 4 * 256 : 0);
   const dim3 grid((unsigned)((ants + 3) / 4));
+  // LDS-staged weights (one workgroup = up to 16 ants of one colony) when the
+  // colony's N x N uint64 weights fit; VRPMS_OPT_ACO_CONSTRUCT 2 forces the L2 path
+  const int wpg = std::min(16, p->ants);
+  const bool staged = ctx->opt_aco_construct != 2 && in.N <= 256 &&
+                      aco_lds_bytes(in.N, wpg) <= ctx->max_lds;
   auto construct = [&](auto wtag) {
     constexpr bool WD = decltype(wtag)::value;
+    if (staged) {
+      const size_t l2 = aco_lds_bytes(in.N, wpg);
+      const dim3 g2((unsigned)(p->colonies * ((p->ants + wpg - 1) / wpg)));
+      auto go = [&](auto kern) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)l2);
+        kern<<<g2, 64 * wpg, l2, s>>>(c, wpg);
+      };
+      if (in.N <= 64) go(aco_construct_lds_kernel<WD, 1>);
+      else if (in.N <= 128) go(aco_construct_lds_kernel<WD, 2>);
+      else go(aco_construct_lds_kernel<WD, 4>);
+      return;
+    }
     if (in.N <= 64) aco_construct_kernel<WD, 1><<<grid, 256, lds, s>>>(c);
     else if (in.N <= 128) aco_construct_kernel<WD, 2><<<grid, 256, lds, s>>>(c);
     else if (in.N <= 256) aco_construct_kernel<WD, 4><<<grid, 256, lds, s>>>(c);
