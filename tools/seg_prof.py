@@ -17,7 +17,8 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 VARIANT = os.environ.get("SEG_PROF_VARIANT", "")  # e.g. NOCUT (A/B: no capacity cuts)
-LIB = os.path.join(ROOT, "build_ab", "segprof" + VARIANT.lower(), "libvrpms.so")
+# abl/ travels to the GPU box (build_ab/ is in .gpurunignore)
+LIB = os.path.join(ROOT, "abl", "segprof" + VARIANT.lower(), "libvrpms.so")
 
 
 def build():

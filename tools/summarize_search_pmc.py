@@ -21,7 +21,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 VALU_PEAK = 1228.8e9
 STEPS = {"tsp_batch_sa_kernel": 1000, "sa_packed_kernel": 400, "sa_route_kernel": 100,
-         "sa_seg_kernel": 100, "ga_fused_kernel": 20, "aco_construct_kernel": 100}
+         "sa_seg_kernel": 100, "ga_fused_kernel": 20, "aco_construct_kernel": 100,
+         "aco_construct_lds_kernel": 100}
 
 
 def short(name):

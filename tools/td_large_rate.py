@@ -25,6 +25,9 @@ argv = sys.argv[1:]
 chains = int(argv[0]) if len(argv) > 0 else 256
 steps = int(argv[1]) if len(argv) > 1 else 60
 sizes = [int(x) for x in argv[2:]] or [400, 600, 800, 1000]
+# FLEET=uniform: one capacity, one start time (sa_route_kernel's exchangeable
+# fleet, RouteK) instead of the heterogeneous one
+uniform = os.environ.get("FLEET") == "uniform"
 ctx = Context(0)
 rows = []
 for n in sizes:
@@ -34,6 +37,8 @@ for n in sizes:
     fr = (1.3, 1.0, 0.8)
     caps = np.array([max(int(base * fr[k * 3 // K]), int(x.demand.max())) for k in range(K)])
     starts = np.arange(K, dtype=np.int64) * 37 % 240 + 420
+    if uniform:
+        caps, starts = x.capacities, x.start_times
     ctx.set_instance(CVRP, x.durations, x.demand, caps, starts)
     out, rates = {}, {}
     for mode in (0, 3, 2):
@@ -52,12 +57,12 @@ for n in sizes:
             ctx.set_sa_route(0)
         out[mode] = (r.cur.cpu(), r.cur_key.cpu())
         rates[mode] = steps / dt
-        print(f"TD-{n} x 24 het K={K}: option {mode}: {steps / dt:,.1f} steps/s per chain",
+        print(f"TD-{n} x 24 {'uniform' if uniform else 'het'} K={K}: option {mode}: {steps / dt:,.1f} steps/s per chain",
               flush=True)
     same = all(torch.equal(out[0][0], out[m][0]) and torch.equal(out[0][1], out[m][1])
                for m in out)
-    row = {"n": n, "K": K, "chains": chains, "steps": steps, "auto": rates[0],
-           "route_hk": rates[3], "sa_kernel": rates[2], "route_over_sa": rates[3] / rates[2],
+    row = {"n": n, "K": K, "fleet": "uniform" if uniform else "het", "chains": chains, "steps": steps, "auto": rates[0],
+           "route": rates[3], "sa_kernel": rates[2], "route_over_sa": rates[3] / rates[2],
            "same_trajectories": same}
     rows.append(row)
     print(json.dumps(row), flush=True)

@@ -1686,9 +1686,17 @@ __global__ __launch_bounds__(256) void aco_construct_kernel(AcoArgs a) {
     for (int c = 0; c < CH; ++c)
       if (lane + 64 * c >= N) vm |= 1u << c;
     uint32_t cur = 0;
+    uint32_t rx = 0, ry = 0;  // lane l: Philox block (iter, ant, s0 + l), words x / y
     for (int s = 0; s < n; ++s) {
-      const u32x4 r = philox((uint32_t)a.iter, (uint32_t)(a.iter >> 32),
-                             (uint32_t)(colony * a.ants + ant), (uint32_t)s, a.seed_lo, a.seed_hi);
+      if ((s & 63) == 0) {  // the next 64 steps' draws, one per lane, in VALU
+        const u32x4 r = philox((uint32_t)a.iter, (uint32_t)(a.iter >> 32),
+                               (uint32_t)(colony * a.ants + ant), (uint32_t)(s + lane), a.seed_lo,
+                               a.seed_hi);
+        rx = r.x;
+        ry = r.y;
+      }
+      const uint32_t r_x = (uint32_t)__builtin_amdgcn_readlane((int)rx, s & 63);
+      const uint32_t r_y = (uint32_t)__builtin_amdgcn_readlane((int)ry, s & 63);
       const uint32_t* Tr = T + (int64_t)cur * N;
       const uint32_t* Er = a.eta + (int64_t)cur * N;
       uint32_t tv[CH], ev[CH];
@@ -1710,7 +1718,7 @@ __global__ __launch_bounds__(256) void aco_construct_kernel(AcoArgs a) {
         if (pick == 0xffffffffu && fb) pick = (uint32_t)(64 * c + __ffsll((long long)fb) - 1);
       }
       if (tot != 0) {  // else: the first free node
-        const uint64_t rr = umod64(((uint64_t)r.y << 32) | r.x, tot);
+        const uint64_t rr = umod64(((uint64_t)r_y << 32) | r_x, tot);
         uint64_t run = 0;
         uint32_t hp = 0xffffffffu;
 #pragma unroll
@@ -1807,6 +1815,10 @@ __global__ __launch_bounds__(256) void aco_construct_kernel(AcoArgs a) {
 // lanes, consecutive entries) instead of a dependent tau + eta round trip to
 // L2 and a 64-bit multiply.  Philox streams (colony * ants + ant, step), the
 // roulette and the pick are the register path's, so the tours are the same.
+// (Both paths draw the Philox blocks of 64 steps at once, lane l computing
+// step s0 + l's in VALU and each step reading its own with v_readlane: the
+// per-step block on the scalar unit made the construction SALU-issue bound,
+// ~142 SALU per wave-step beside ~136 VALU, profiles/round6_aco_lds_*.)
 template <bool WORDS, int CH>
 __global__ __launch_bounds__(1024) void aco_construct_lds_kernel(AcoArgs a, int wpg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1838,9 +1850,16 @@ __global__ __launch_bounds__(1024) void aco_construct_lds_kernel(AcoArgs a, int 
   for (int c = 0; c < CH; ++c)
     if (lane + 64 * c >= N) vm |= 1u << c;
   uint32_t cur = 0;
+  uint32_t rx = 0, ry = 0;  // lane l: Philox block (iter, gid, s0 + l), words x / y
   for (int s = 0; s < n; ++s) {
-    const u32x4 r = philox((uint32_t)a.iter, (uint32_t)(a.iter >> 32), (uint32_t)gid, (uint32_t)s,
-                           a.seed_lo, a.seed_hi);
+    if ((s & 63) == 0) {  // the next 64 steps' draws, one per lane, in VALU
+      const u32x4 r = philox((uint32_t)a.iter, (uint32_t)(a.iter >> 32), (uint32_t)gid,
+                             (uint32_t)(s + lane), a.seed_lo, a.seed_hi);
+      rx = r.x;
+      ry = r.y;
+    }
+    const uint32_t r_x = (uint32_t)__builtin_amdgcn_readlane((int)rx, s & 63);
+    const uint32_t r_y = (uint32_t)__builtin_amdgcn_readlane((int)ry, s & 63);
     const uint64_t* Wr = Wt + cur * (uint32_t)N;
     uint64_t w[CH], inc[CH], ct[CH], tot = 0;
 #pragma unroll
@@ -1855,7 +1874,7 @@ __global__ __launch_bounds__(1024) void aco_construct_lds_kernel(AcoArgs a, int 
       if (pick == 0xffffffffu && fb) pick = (uint32_t)(64 * c + __ffsll((long long)fb) - 1);
     }
     if (tot != 0) {  // else: the first free node
-      const uint64_t rr = umod64(((uint64_t)r.y << 32) | r.x, tot);
+      const uint64_t rr = umod64(((uint64_t)r_y << 32) | r_x, tot);
       uint64_t run = 0;
       uint32_t hp = 0xffffffffu;
 #pragma unroll
@@ -2535,8 +2554,15 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
   // start time) or not (HV: walks re-synchronise on the same vehicle only)
   const Instance& in = ctx->inst;
   const bool hv = !(in.uniform_cap && in.min_start == in.max_start);
+  // Hour-indexed (H = 24) requests with per-vehicle capacities or start times
+  // that sa_td_kernel cannot hold (its LDS rows: large n) go to sa_kernel's
+  // full L2 walks when one wavefront prices a chain's moves: measured faster
+  // than the route-local walks there, 1.15-1.21x at TD-400 .. TD-1000 x 24
+  // (tools/td_large_rate.py, profiles/round6_td_large_rate.log; same
+  // trajectories).  Option 3 still forces the route kernel.
+  const bool td_full_walk = ctx->opt_sa_route == 0 && in.H == 24 && hv && wpc == 1;
   if (p->window > 0 && in.problem == VRPMS_CVRP && in.max_dem <= in.min_cap &&
-      in.max_dem <= 65535 && route_max(in.K) <= 255 &&
+      in.max_dem <= 65535 && route_max(in.K) <= 255 && !td_full_walk &&
       n <= 65535 && ctx->opt_sa_route != 2) {  // (0 auto, 3 force this kernel)
     const size_t npad = ((size_t)n + 7) & ~(size_t)7;
     const size_t wbytes = ((size_t)route_wave_bytes((int)npad, in.K) + 15) & ~(size_t)15;
