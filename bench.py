@@ -655,11 +655,15 @@ def equal_time_cells(ctx, seconds, dist, with_cpu, instance="x1000", seeds=(0, 1
     # temperatures from tools/sched_scan.py (10 s, seeds 0-1, both legs at six
     # schedules): each leg at the one that scored best for it on average --
     # X-1000: (t0, t_end) = (0.5, 0.004) x the typical edge for the GPU, (0.5,
-    # 0.002) for the host; TD-200: (0.5, 0.004) and (1.0, 0.002)
+    # 0.002) for the host; TD-200: (0.5, 0.004) and (1.0, 0.002).  Round 6
+    # (tools/migration_scan.py, seeds 0-2, profiles/round6_x1000_shape_scan_*):
+    # the GPU's X-1000 t_end 0.004 -> 0.003 (82,844 / 78,514 / 78,392 against
+    # 83,156 / 78,730 / 78,291; 512 x 128, 512 x 256, 256 x 256 and 1,024 x 256
+    # were worse on the mean)
     # TD-200 (uniform and heterogeneous fleets) on sa_td_kernel, round 5: shape
     # and final temperature from tools/td_quality_scan.py
     kw = dict(chains=1024, moves=128, window=32, window_types=2, start="pack", epochs=80,
-              mig_E=256, tend_frac=0.004, cpu_tend_frac=0.002) if instance == "x1000" else \
+              mig_E=256, tend_frac=0.003, cpu_tend_frac=0.002) if instance == "x1000" else \
         dict(chains=TD_SHAPE[0], moves=TD_SHAPE[1], window=32, window_types=2, start="pack",
              mig_E=TD_SHAPE[2], tend_frac=TD_SHAPE[3], cpu_t0_frac=1.0, cpu_tend_frac=0.002)
     cells = []

@@ -2540,8 +2540,17 @@ extern "C" int vrpms_sa_run(vrpms_ctx* ctx, const vrpms_sa_params* p, uint16_t* 
     if (rc <= 0) return rc;
   }
   // hour-indexed matrices (H = 24): full walks over LDS hour rows, any fleet
-  // (sa_td.hip)
-  if (ctx->opt_sa_route == 0) {
+  // (sa_td.hip) -- except a uniform fleet's long tours, where the route-local
+  // walks are faster: sa_td / sa_route 1.08x at 419 tokens, 0.85x at 629
+  // (TD-400 / TD-600 x 24, tools/td_large_rate.py FLEET=uniform,
+  // profiles/round6_td_large_rate_uniform.log), so past 480 tokens the
+  // route kernel takes them when it applies
+  const Instance& in0 = ctx->inst;
+  const bool uniform_fleet = in0.uniform_cap && in0.min_start == in0.max_start;
+  const bool route_applies = p->window > 0 && in0.problem == VRPMS_CVRP &&
+                             in0.max_dem <= in0.min_cap && in0.max_dem <= 65535 &&
+                             route_max(in0.K) <= 255 && n <= 65535;
+  if (ctx->opt_sa_route == 0 && !(uniform_fleet && route_applies && n > 480)) {
     const int rc = launch_sa_td(ctx, p, d_cur, d_cur_key, d_best, d_best_key, n, wtypes, moves,
                                 (hipStream_t)stream);
     if (rc <= 0) return rc;
