@@ -431,6 +431,14 @@ SEG_CASES = [
      128),
     ("cvrp300_few_seps_cold", lambda: synth.cvrp(300, 24, seed=18), "pack_few", 8, 300, 0.5, 24,
      2, 128),
+    # round 6: the incremental split (only the segments a move touches are
+    # split again, the routes after them shifted) over a long warm run, where
+    # most steps accept and route counts change -- and a windowless one, whose
+    # swaps / relocates span 64 segments or more (the full pass)
+    ("x1000_warm_incremental", lambda: synth.x_style(1000, seed=20), "pack", 8, 600, 1 / 30.0,
+     32, 2, 128),
+    ("cvrp600_warm_windowless", lambda: synth.cvrp(600, 40, seed=21), "pack", 8, 300, 1 / 60.0,
+     0, 0, 64),
     # total demand past 2^31 with the capacity: the u32 prefix demands cannot hold
     # it, so the launcher hands the chains to the full re-evaluation kernels
     ("cvrp150_huge_demand", lambda: _huge_demand(synth.cvrp(150, 12, seed=19)), "pack", 4, 40,

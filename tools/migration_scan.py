@@ -13,6 +13,9 @@ from vrpms_amd import synth  # noqa: E402
 from vrpms_amd.core import CVRP, Context  # noqa: E402
 
 T, seed = float(sys.argv[1]), int(sys.argv[2])
+if os.environ.get("SEG_LIB"):  # an A/B build of the library
+    from vrpms_amd import _lib
+    _lib.load(os.environ["SEG_LIB"])
 ctx = Context(0)
 # INSTANCE=td: cfg 3's TD-200 x 24 (sa_route_kernel) instead of X-1000
 td = os.environ.get("INSTANCE") == "td"

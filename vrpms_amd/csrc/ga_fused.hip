@@ -244,7 +244,7 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
       constexpr int NC = decltype(nc_tag)::value;
       uint8_t* out[NC];
       uint8_t* m[NC];
-      int lo[NC], hi[NC], rest[NC], filled[NC];
+      int lo[NC], hi[NC], filled[NC];
       uint32_t stamp[NC], ga[NC][H], gb[NC][H];
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
@@ -255,7 +255,6 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
         lo[c] = wave_bcast(v_lo, k + c);
         hi[c] = wave_bcast(v_hi, k + c);
         stamp[c] = 1u + (uint32_t)((g - gclr) * cpw + k + c);
-        rest[c] = n - (hi[c] - lo[c] + 1);
         filled[c] = 0;
 #pragma unroll
         for (int h = 0; h < H; ++h) {
@@ -309,7 +308,9 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
                                            __builtin_amdgcn_mbcnt_lo((uint32_t)ball, 0u));
           int dst = hi[c] + 1 + slot;
           dst = dst >= n ? dst - n : dst;
-          *(keep && slot < rest[c] ? out[c] + dst : sink) = (uint8_t)gb[c][h];
+          // (a kept gene's slot is always < n - (hi - lo + 1): exactly that
+          // many of B's genes lie outside A's span, and dst stays in [0, n))
+          *(keep ? out[c] + dst : sink) = (uint8_t)gb[c][h];
           filled[c] += __popcll(ball);
         }
       // the mutation, in place: new[q] = old[moved_index(q)] over the window

@@ -313,6 +313,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
 #endif
   int reb_a = 0, reb_b = n;
   bool rb_valid = false;  // T.RB holds a previous split (the heterogeneous pass starts from it)
+  bool tab_ok = false;    // the segment / route tables describe the tour before this rebuild
   uint32_t pe_old = 0;
   auto rebuild = [&]() __attribute__((always_inline)) {
     wave_sync();
@@ -362,7 +363,10 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
     wave_sync();
     SEG_PT(8);
     seg_ok = S <= SEGS;
-    if (!seg_ok) return;
+    if (!seg_ok) {
+      tab_ok = false;
+      return;
+    }
     // segments, one lane each: how many routes the greedy split makes of it
     // (binary-searched capacity cuts), the first route RB, the nearest
     // non-empty segments at or before (LNE1, +1) / at or after (FNE).  A
@@ -387,10 +391,72 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
       }
       return cnt;
     };
+    // Incremental split (one capacity; round 6).  A move permutes the tokens
+    // of positions qa..qb and nothing else, so every segment outside
+    // SC[qa] .. SC[qb + 1] keeps its tokens, its demand-prefix differences
+    // and its edges: its cuts, its route count and its routes' durations.
+    // Only those segments are split again (one lane each); the routes after
+    // them move by the change of route count (dur / RS shifted, RB bumped).
+    // The prefix scans below (FNE, LNE1, dsp, pmx, smx, sparse table) still
+    // run over everything: they search nothing.  Falls back to the full pass
+    // when the span touches 64 segments or more, or the tables were not valid.
+    int g_lo = 0, g_hi = S;  // the segments whose routes are (re)written below
+    bool inc = false;
+    if (!HET && tab_ok && !(qa == 0 && qb >= n)) {
+      const int ga = (int)T.SC[qa];
+      const int gb = qb < n ? min((int)T.SC[qb + 1], S) : S;
+      const int r0 = T.RB[ga], r1o = T.RB[gb + 1], Rold = R;
+      if (gb - ga < 64 && Rold - r1o <= 4 * 64) {
+        const int g = ga + lane;
+        const uint32_t cnt = g <= gb ? seg_routes(g, 0) : 0u;
+        uint32_t tc;
+        const uint32_t incl = dpp_scan<false>(cnt, tc);
+        const int dR = (int)tc - (r1o - r0);
+        if (Rold + dR <= RM) {
+          inc = true;
+          if (dR != 0) {  // routes r1o .. Rold - 1 move to r1o + dR ..
+            uint32_t vd[4], vr[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int r = r1o + lane + 64 * i;
+              vd[i] = r < Rold ? T.dur[r] : 0u;
+              vr[i] = r < Rold ? (uint32_t)T.RS[r] : 0u;
+            }
+            wave_sync();
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int r = r1o + lane + 64 * i;
+              if (r < Rold) {
+                T.dur[r + dR] = vd[i];
+                T.RS[r + dR] = (uint16_t)vr[i];
+              }
+            }
+            for (int x = gb + 1 + lane; x <= S + 1; x += 64) T.RB[x] = (uint16_t)((int)T.RB[x] + dR);
+          }
+          if (g <= gb) T.RB[g] = (uint16_t)(r0 + (int)(incl - cnt));
+          R = Rold + dR;
+          g_lo = ga;
+          g_hi = gb;
+          // LNE1 (the last non-empty segment at or before g, + 1): a prefix
+          // maximum over the segments, as the full pass forms it
+          uint32_t lcarry = 0;
+#pragma unroll 1
+          for (int base = 0; base <= S; base += 64) {
+            const int gg = base + lane;
+            const bool ne = gg <= S && SPX(gg) - 1 >= SPX(gg - 1) + 1;
+            uint32_t tl;
+            const uint32_t lne = dpp_scan<true>(ne ? (uint32_t)gg + 1u : 0u, tl);
+            if (gg <= S) T.LNE1[gg] = (uint16_t)max(lcarry, lne);
+            lcarry = max(lcarry, tl);
+          }
+          wave_sync();
+        }
+      }
+    }
     uint32_t rcarry = 0;
     bool moved = true;
 #pragma unroll 1
-    for (int it = 0; moved && it < (HET ? 6 : 1); ++it) {
+    for (int it = 0; !inc && moved && it < (HET ? 6 : 1); ++it) {
       rcarry = 0;
       uint32_t lcarry = 0;
       moved = false;
@@ -429,9 +495,12 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
       wave_sync();
       rcarry = (uint32_t)T.RB[S] + seg_routes(S, (int)T.RB[S]);
     }
-    R = (int)rcarry;
+    if (!inc) R = (int)rcarry;
     seg_ok = R <= RM;
-    if (!seg_ok) return;
+    if (!seg_ok) {
+      tab_ok = false;
+      return;
+    }
     uint32_t fcarry = 0;  // FNE[g] = S + 1 - (suffix max of S + 1 - g over non-empty g)
 #pragma unroll 1
     for (int top = (S / 64) * 64; top >= 0; top -= 64) {
@@ -449,9 +518,10 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
     if (lane == 0) T.RB[S + 1] = (uint16_t)R;
     wave_sync();
     SEG_PT(9);
-    // route durations (heterogeneous: loads and allowances), one lane per segment
+    // route durations (heterogeneous: loads and allowances), one lane per
+    // segment (incremental: the re-split segments only)
 #pragma unroll 1
-    for (int g = lane; g <= S; g += 64) {
+    for (int g = g_lo + lane; g <= g_hi; g += 64) {
       const int s0 = SPX(g - 1) + 1, s1 = SPX(g) - 1;
       int r = T.RB[g], x = s0;
       T.RS[r] = (uint16_t)s0;
@@ -550,6 +620,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
     }
     SEG_PT(11);
     rb_valid = true;
+    tab_ok = true;
     const int l1 = T.LNE1[S];
     Tt = l1 ? S - (l1 - 1) : S;
   };
