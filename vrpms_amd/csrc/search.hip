@@ -1845,10 +1845,17 @@ __global__ __launch_bounds__(1024) void aco_construct_lds_kernel(AcoArgs a, int 
     for (int q = n + lane; q < 256; q += 64) tb[q] = 0;
   }
   uint16_t* out = a.tours + gid * n;
-  uint32_t vm = lane == 0 ? 1u : 0u;  // bit c: node lane + 64c visited (or past N); depot
+  // Lane l owns the CH consecutive nodes CH l .. CH l + CH - 1, so the
+  // roulette's prefix sums in node order are the lanes' prefix (ONE 64-bit
+  // wave scan of each lane's sum, not one per 64-node chunk) followed by the
+  // lane's own running sum: the first lane whose inclusive prefix passes r
+  // holds the pick, the first of its nodes whose running sum passes r.  (The
+  // first node j with prefix P_j > r has w_j > 0, the register path's rule.)
+  uint32_t vm = lane == 0 ? 1u : 0u;  // bit c: node CH lane + c visited (or past N); depot
 #pragma unroll
   for (int c = 0; c < CH; ++c)
-    if (lane + 64 * c >= N) vm |= 1u << c;
+    if (CH * lane + c >= N) vm |= 1u << c;
+  constexpr uint32_t kAll = (1u << CH) - 1u;
   uint32_t cur = 0;
   uint32_t rx = 0, ry = 0;  // lane l: Philox block (iter, gid, s0 + l), words x / y
   for (int s = 0; s < n; ++s) {
@@ -1860,36 +1867,41 @@ __global__ __launch_bounds__(1024) void aco_construct_lds_kernel(AcoArgs a, int 
     }
     const uint32_t r_x = (uint32_t)__builtin_amdgcn_readlane((int)rx, s & 63);
     const uint32_t r_y = (uint32_t)__builtin_amdgcn_readlane((int)ry, s & 63);
-    const uint64_t* Wr = Wt + cur * (uint32_t)N;
-    uint64_t w[CH], inc[CH], ct[CH], tot = 0;
-#pragma unroll
-    for (int c = 0; c < CH; ++c) w[c] = !((vm >> c) & 1u) ? Wr[lane + 64 * c] : 0ull;
-    uint32_t pick = 0xffffffffu;
+    const uint64_t* Wr = Wt + cur * (uint32_t)N + CH * lane;
+    uint64_t w[CH], sum = 0;
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
-      inc[c] = w[c];
-      ct[c] = wave_scan_add_u64(inc[c]);
-      tot += ct[c];
-      const uint64_t fb = __ballot(!((vm >> c) & 1u));
-      if (pick == 0xffffffffu && fb) pick = (uint32_t)(64 * c + __ffsll((long long)fb) - 1);
+      w[c] = !((vm >> c) & 1u) ? Wr[c] : 0ull;
+      sum += w[c];
     }
-    if (tot != 0) {  // else: the first free node
+    uint64_t incl = sum;
+    const uint64_t tot = wave_scan_add_u64(incl);
+    uint32_t mine, L;  // this lane's candidate node, the lane that holds the pick
+    if (tot != 0) {
       const uint64_t rr = umod64(((uint64_t)r_y << 32) | r_x, tot);
-      uint64_t run = 0;
-      uint32_t hp = 0xffffffffu;
+      L = (uint32_t)__ffsll((long long)__ballot(incl > rr)) - 1u;  // exists: the last lane's is tot
+      uint64_t run = incl - sum;
+      uint32_t cc = CH - 1;
+      bool found = false;
 #pragma unroll
       for (int c = 0; c < CH; ++c) {
-        const uint64_t ball = __ballot(w[c] > 0 && run + inc[c] > rr);
-        if (hp == 0xffffffffu && ball) hp = (uint32_t)(64 * c + __ffsll((long long)ball) - 1);
-        run += ct[c];
+        run += w[c];
+        if (!found && run > rr) {
+          cc = (uint32_t)c;
+          found = true;
+        }
       }
-      if (hp != 0xffffffffu) pick = hp;  // always: tot > rr
+      mine = CH * (uint32_t)lane + cc;
+    } else {  // every free weight is 0: the first free node
+      L = (uint32_t)__ffsll((long long)__ballot(vm != kAll)) - 1u;
+      mine = CH * (uint32_t)lane + (uint32_t)__builtin_ctz((~vm & kAll) | (1u << CH));
     }
+    const uint32_t pick = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)L);
     if (lane == 0) {
       out[s] = (uint16_t)pick;
       if constexpr (WORDS) tb[s] = (uint8_t)pick;
     }
-    if (lane == (int)(pick & 63u)) vm |= 1u << (pick >> 6);
+    if ((uint32_t)lane == pick / CH) vm |= 1u << (pick % CH);
     cur = pick;
   }
   if constexpr (WORDS) {
