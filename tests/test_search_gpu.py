@@ -398,10 +398,12 @@ def test_aco_iterations_match_oracle_at_size(ctx, name, maker):
 ACO_STAGED = [
     # (name, instance, colonies, ants): ants not a multiple of the 16-ant
     # workgroup (16 + 16 + 8), one ant per colony, the largest N whose
-    # weights fit the LDS (141 * 141 * 8 B + tour buffers), the TSP layout
+    # weights fit the LDS (140 x 140 x 8 B + 16 tour buffers; rows padded to
+    # an even stride), the TSP layout
     ("cvrp100_40ants", lambda: synth.cvrp(100, 8, seed=0), 3, 40),
     ("cvrp60_1ant", lambda: synth.cvrp(60, 5, seed=4), 5, 1),
-    ("cvrp140_17ants", lambda: synth.cvrp(140, 10, seed=6), 2, 17),
+    ("cvrp139_17ants", lambda: synth.cvrp(139, 10, seed=6), 2, 17),
+    ("cvrp140_past_lds", lambda: synth.cvrp(140, 10, seed=6), 2, 17),   # N = 141: the L2 path
     ("tsp40_64ants", lambda: synth.Instance("tsp40", synth.random_symmetric(
         40, np.random.default_rng(8))[None], None, None, np.array([0]), "tsp"), 2, 64),
 ]

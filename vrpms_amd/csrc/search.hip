@@ -1823,16 +1823,20 @@ template <bool WORDS, int CH>
 __global__ __launch_bounds__(1024) void aco_construct_lds_kernel(AcoArgs a, int wpg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = a.N, n = a.n;
-  uint64_t* Wt = reinterpret_cast<uint64_t*>(smem);  // [N][N]
-  uint8_t* tbuf = smem + (((size_t)N * N * 8 + 15) & ~(size_t)15);
+  // [N][NS] weights, NS = N rounded up to even: a row starts 16-byte aligned,
+  // so lane l's CH consecutive entries are whole ds_read_b128s (conflict-free)
+  const int NS = (N + 1) & ~1;
+  uint64_t* Wt = reinterpret_cast<uint64_t*>(smem);
+  uint8_t* tbuf = smem + (((size_t)N * NS * 8 + 15) & ~(size_t)15);
   const int groups = (a.ants + wpg - 1) / wpg;
   const int colony = (int)blockIdx.x / groups;
   const int ant0 = ((int)blockIdx.x % groups) * wpg;
   {
     const uint32_t* T = a.tau + (int64_t)colony * N * N;
-    const int NN = N * N;
-    for (int e = threadIdx.x; e < NN; e += blockDim.x)
-      Wt[e] = (uint64_t)(T[e] >> 8) * a.eta[e];
+    for (int e = threadIdx.x; e < N * NS; e += blockDim.x) {
+      const int i = e / NS, j = e - i * NS;
+      Wt[e] = j < N ? (uint64_t)(T[i * N + j] >> 8) * a.eta[i * N + j] : 0ull;
+    }
   }
   __syncthreads();
   const int wave = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
@@ -1867,7 +1871,7 @@ __global__ __launch_bounds__(1024) void aco_construct_lds_kernel(AcoArgs a, int 
     }
     const uint32_t r_x = (uint32_t)__builtin_amdgcn_readlane((int)rx, s & 63);
     const uint32_t r_y = (uint32_t)__builtin_amdgcn_readlane((int)ry, s & 63);
-    const uint64_t* Wr = Wt + cur * (uint32_t)N + CH * lane;
+    const uint64_t* Wr = Wt + cur * (uint32_t)NS + CH * lane;
     uint64_t w[CH], sum = 0;
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
@@ -1913,7 +1917,9 @@ __global__ __launch_bounds__(1024) void aco_construct_lds_kernel(AcoArgs a, int 
 }
 
 // LDS bytes of aco_construct_lds_kernel (weights + a 256-byte tour buffer per wavefront)
-static size_t aco_lds_bytes(int N, int wpg) { return (((size_t)N * N * 8 + 15) & ~(size_t)15) + 256 * (size_t)wpg; }
+static size_t aco_lds_bytes(int N, int wpg) {
+  return (((size_t)N * ((N + 1) & ~1) * 8 + 15) & ~(size_t)15) + 256 * (size_t)wpg;
+}
 
 struct AcoUpdateArgs {
   int colonies, ants, n, N;
