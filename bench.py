@@ -549,7 +549,8 @@ def quality(ctx, inst, seconds, world, rank, dist, with_cpu, chains=4096, label=
     return out
 
 
-def algo_quality(ctx, inst, seconds, seed=0, polish_steps=100, polish_top=4):
+def algo_quality(ctx, inst, seconds, seed=0, polish_steps=100, polish_top=4,
+                 aco_shape=(64, 64, 5)):
     """The GA and ACO endpoints' best cost at the same wall time as the SA
     quality leg (cfg 2, api/vrp/{ga,aco}/index.py): each runs on the GPU for
     `seconds` of wall time -- GA 256 islands x 256 (randomPermutationCount),
@@ -572,9 +573,10 @@ def algo_quality(ctx, inst, seconds, seed=0, polish_steps=100, polish_top=4):
                                  polish=pol, polish_top=polish_top)
             unit, per = "generations", 20
         else:
-            r = runners.ACORunner(ctx, inst.n, colonies=64, ants=64, seed=seed,
-                                  iters_per_epoch=5, bsf_period=5, polish=pol)
-            unit, per = "iterations", 5
+            r = runners.ACORunner(ctx, inst.n, colonies=aco_shape[0], ants=aco_shape[1],
+                                  seed=seed, iters_per_epoch=aco_shape[2], bsf_period=5,
+                                  polish=pol)
+            unit, per = "iterations", aco_shape[2]
         r.epoch()                              # first launch: code object load
         torch.cuda.synchronize(ctx.dev)
         cool = _TimedCooling(seconds, 0.05 * edge, 0.002 * edge)

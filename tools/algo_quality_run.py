@@ -2,7 +2,8 @@
 """cfg 2 (CVRP-100, K = 8) best cost at equal wall time: GPU SA and host SA
 (bench.quality), then the GA and ACO endpoints' memetic runs
 (bench.algo_quality) for the same seconds.
-usage: algo_quality_run.py [seconds] [polish_steps] [polish_top] [seed]"""
+usage: algo_quality_run.py [seconds] [polish_steps] [polish_top] [seed]
+(ACO_SHAPE=colonies:ants:iterations_per_epoch, default 64:64:5; ONLY=aco|ga)"""
 import json
 import os
 import sys
@@ -24,7 +25,9 @@ ctx.set_instance(CVRP, inst.durations, inst.demand, inst.capacities, inst.start_
 q = bench.quality(ctx, inst, T, 1, 0, None, with_cpu=True)
 print(json.dumps({"sa_gpu": q["gpu"]["duration_sum"], "sa_host": q["cpu"]["duration_sum"],
                   "gap": q.get("gap")}), flush=True)
-by = bench.algo_quality(ctx, inst, T, seed=seed, polish_steps=ps, polish_top=top)
+shape = tuple(int(x) for x in os.environ.get("ACO_SHAPE", "64:64:5").split(":"))
+by = bench.algo_quality(ctx, inst, T, seed=seed, polish_steps=ps, polish_top=top,
+                        aco_shape=shape)
 for k, v in by.items():
     v["gap_vs_host_sa"] = (v["duration_sum"] - q["cpu"]["duration_sum"]) / q["cpu"]["duration_sum"]
 print(json.dumps(by), flush=True)
