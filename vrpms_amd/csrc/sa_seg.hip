@@ -842,7 +842,13 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
         int c_cnt = 0;
         uint32_t isum = 0, imax = 0;
         int icnt = 0, seps = 0, cutc = 0;
-        bool cust = false, dead = false;  // dead: the cuts exceeded the budget
+        bool cust = false;
+        // dead: the cuts exceeded the budget.  An int, not a bool: with two
+        // bools, SimplifyCFG merged run()'s "c_has = true; return" and "dead =
+        // true; return" into one store through a phi of their addresses, which
+        // kept both in scratch memory (a scratch load on every run() call's
+        // critical path); stores of different types are never merged
+        int dead = 0;
         int vo = ra;  // (heterogeneous) the open route's vehicle
         auto close = [&]() __attribute__((always_inline)) {
           const uint32_t d = c_dur + c_pl;
@@ -878,7 +884,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
             int pa = x, pb = y;
             if (!fits) {
               if (cutc >= bud) {  // one cut more than the fleet allows: no search
-                dead = true;
+                dead = 1;
 #ifdef VRPMS_SEG_PROF
                 ++p_dead;
 #endif
