@@ -230,7 +230,13 @@ __global__ __launch_bounds__(BLOCK) void eval_cvrp_packed(PackedArgs a) {
     bool dead = false;  // all K vehicles closed: customers unvisited, separators ignored
     // MODE 0/2 state
     int rcap = MODE == 0 ? capL[0] : cap0;
-    uint32_t cur = 0, hprev = 0;
+    // hprev is held in 64 bits (only its low word is read): as a uint32_t,
+    // SimplifyCFG merged the separator branch's "rcap = ...; return" with the
+    // customer path's "hprev = hi" into one store through a phi of their
+    // addresses, and both stayed in scratch memory (MODE 0 / 2); stores of
+    // different types are never merged
+    uint32_t cur = 0;
+    uint64_t hprev = 0;
     bool open = false;  // the current route holds a customer
     // one split step for token c (A10: c == 0 is a route separator)
     auto step = [&](uint64_t e, uint32_t c) {

@@ -200,51 +200,27 @@ VRPMS_DEV void merge_select(const uint64_t* pk, const uint64_t* ck, int P, uint6
     const bool pad = child && (c & 63) >= P - (own << 6);  // run padding
     const uint64_t k = child ? rk[c] : pk[e];
     const uint32_t v = child ? ri[c] : (uint32_t)e;
-    // The searches this lane owns -- the parents' lower bound (a child's even
-    // lane) and its other runs' -- advance together, two runs at a time with
-    // the parents' last six steps folded into the first pair: one dependent
-    // LDS round per step for all of them (a child's even lane: 3 + 7 rounds
-    // at P = 256 instead of 8 + 2 x 7).  Counts are those of the plain
-    // searches: lower bounds on (key, index), runs of 64 by binary lifting.
     int part = 0;
-    const bool doP = child && half <= 0;
-    const int rstep = half < 0 ? 1 : 2;
-    int r = half < 0 ? 0 : half;
-    if (r == own) r += rstep;
-    int lo = 0;
-    if (doP)  // the parents' first steps (s > 32) alone
-      for (int s = 1 << (31 - __builtin_clz((uint32_t)P)); s > 32; s >>= 1)
-        if (lo + s <= P && pair_less(pk[lo + s - 1], (uint32_t)(lo + s - 1), k, v)) lo += s;
-    bool first = true;
-    do {
-      const int ra = r < R ? r : -1;
-      int r2 = r + rstep;
-      if (r2 == own) r2 += rstep;
-      const int rb = r2 < R ? r2 : -1;
-      r = r2 + rstep;
-      if (r == own) r += rstep;
-      const uint64_t* ka = rk + ((ra < 0 ? 0 : ra) << 6);
-      const uint32_t* ia = ri + ((ra < 0 ? 0 : ra) << 6);
-      const uint64_t* kb = rk + ((rb < 0 ? 0 : rb) << 6);
-      const uint32_t* ib = ri + ((rb < 0 ? 0 : rb) << 6);
-      const bool p6 = first && doP;
-      int pa = 0, pb = 0;
-#pragma unroll
-      for (int s = 32; s > 0; s >>= 1) {
-        const bool ta = ra >= 0 && pair_less(ka[pa + s - 1], ia[pa + s - 1], k, v);
-        const bool tb = rb >= 0 && pair_less(kb[pb + s - 1], ib[pb + s - 1], k, v);
-        const bool tp =
-            p6 && lo + s <= P && pair_less(pk[lo + s - 1], (uint32_t)(lo + s - 1), k, v);
-        pa += ta ? s : 0;
-        pb += tb ? s : 0;
-        lo += tp ? s : 0;
+    if (child && half <= 0) {
+      int lo = 0, hi = P;  // lower bound among the parents
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (pair_less(pk[mid], (uint32_t)mid, k, v)) lo = mid + 1;
+        else hi = mid;
       }
-      if (ra >= 0 && pair_less(ka[pa], ia[pa], k, v)) ++pa;
-      if (rb >= 0 && pair_less(kb[pb], ib[pb], k, v)) ++pb;
-      part += (ra >= 0 ? pa : 0) + (rb >= 0 ? pb : 0);
-      first = false;
-    } while (r < R);
-    if (doP) part += lo;
+      part += lo;
+    }
+    for (int r = half < 0 ? 0 : half; r < R; r += half < 0 ? 1 : 2) {  // every other run
+      if (r == own) continue;
+      const uint64_t* rkr = rk + (r << 6);
+      const uint32_t* rir = ri + (r << 6);
+      int pos = 0;
+#pragma unroll
+      for (int s = 32; s > 0; s >>= 1)
+        if (pair_less(rkr[pos + s - 1], rir[pos + s - 1], k, v)) pos += s;
+      if (pair_less(rkr[pos], rir[pos], k, v)) ++pos;
+      part += pos;
+    }
     if (two)  // both lanes of the pair active here (the loop bound is per pair)
       part += __builtin_amdgcn_mov_dpp(part, 0xB1, 0xF, 0xF, false);
     const int rank = part + (child ? (c & 63) : e);
