@@ -1194,19 +1194,16 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
           reb_a = blo;
           reb_b = hq;
           pe_old = T.PE[hq + 1];
-          // tokens two to a register (16 bits each): the OCC = 2 variant's 256
-          // registers then hold the whole span without spilling to scratch
-          uint32_t v_tk[kSegRegs / 2], v_e[kSegRegs];
-#pragma unroll
-          for (int i = 0; i < kSegRegs / 2; ++i) v_tk[i] = 0u;
+          uint32_t v_tok[kSegRegs], v_e[kSegRegs];
 #pragma unroll
           for (int i = 0; i < kSegRegs; ++i) {
             if (blo + 64 * i > hq) break;
             const int q = blo + lane + 64 * i;
+            v_tok[i] = 0u;
             v_e[i] = 0u;
             if (q > hq) continue;
             const int sq = map_src(mmb, q), sp = map_src(mmb, q - 1);
-            if (q < n) v_tk[i >> 1] |= (uint32_t)T.tok[sq] << (16 * (i & 1));
+            if (q < n) v_tok[i] = T.tok[sq];
             if (q == blo) v_e[i] = w0;
             else if (q == blo + 1) v_e[i] = w1;
             else if (q == bhi) v_e[i] = w2;
@@ -1220,7 +1217,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
             if (blo + 64 * i > hq) break;
             const int q = blo + lane + 64 * i;
             if (q > hq) continue;
-            if (q < n) T.tok[q] = (uint16_t)(v_tk[i >> 1] >> (16 * (i & 1)));
+            if (q < n) T.tok[q] = (uint16_t)v_tok[i];
             T.PE[q + 1] = v_e[i];
           }
         }
