@@ -402,6 +402,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
     // when the span touches 64 segments or more, or the tables were not valid.
     int g_lo = 0, g_hi = S;  // the segments whose routes are (re)written below
     bool inc = false;
+    bool empties_kept = false;  // (incremental) no segment became empty or non-empty
     if (!HET && tab_ok && !(qa == 0 && qb >= n)) {
       const int ga = (int)T.SC[qa];
       const int gb = qb < n ? min((int)T.SC[qb + 1], S) : S;
@@ -437,11 +438,17 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
           R = Rold + dR;
           g_lo = ga;
           g_hi = gb;
+          // LNE1 / FNE (the nearest non-empty segments) change only when one
+          // of the re-split segments became empty or non-empty: LNE1[g] == g
+          // + 1 says segment g was non-empty before the move
+          const bool flip = g <= gb && (T.LNE1[g] == (uint16_t)(g + 1)) !=
+                                           (SPX(g) - 1 >= SPX(g - 1) + 1);
+          empties_kept = __ballot(flip) == 0ull;
           // LNE1 (the last non-empty segment at or before g, + 1): a prefix
           // maximum over the segments, as the full pass forms it
           uint32_t lcarry = 0;
 #pragma unroll 1
-          for (int base = 0; base <= S; base += 64) {
+          for (int base = 0; !empties_kept && base <= S; base += 64) {
             const int gg = base + lane;
             const bool ne = gg <= S && SPX(gg) - 1 >= SPX(gg - 1) + 1;
             uint32_t tl;
@@ -503,7 +510,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
     }
     uint32_t fcarry = 0;  // FNE[g] = S + 1 - (suffix max of S + 1 - g over non-empty g)
 #pragma unroll 1
-    for (int top = (S / 64) * 64; top >= 0; top -= 64) {
+    for (int top = (S / 64) * 64; !empties_kept && top >= 0; top -= 64) {
       const int g = top + lane;
       uint32_t f = 0;
       if (g <= S) {
