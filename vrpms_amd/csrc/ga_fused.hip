@@ -177,6 +177,15 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
   }
   const int cpw = (P + 15) / 16;  // children per wavefront per generation
   int gclr = 0;                   // generation of the last stamp clear
+  // The Philox draws of GB generations are taken in one pass: lane L holds
+  // child w + 16 (L % cg) of generation g0 + L / cg (cg = cpw rounded up to a
+  // power of two), so a wave's 64 lanes draw for 64 / cg generations at once
+  // instead of drawing 16 useful children per pass.  What a draw decides
+  // about the population (the tournaments) is still read each generation.
+  const int cg = cpw <= 1 ? 1 : 1 << (32 - __builtin_clz((uint32_t)(cpw - 1)));
+  const int GB = 64 / cg;
+  uint32_t b_r0 = 0, b_r1 = 0, b_r2 = 0, b_r3 = 0;  // tournament words (A: r0, r1; B: r2, r3)
+  int v_lo = 0, v_hi = 0, v_mut = 0, v_mtyp = 0, v_mi = 0, v_mj = 0;
 
   WordChains<1, CY> ch;
   ch.setup(a.f, smem);
@@ -201,21 +210,22 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
       gclr = g;
     }
     // ---- breed: one child per wavefront at a time --------------------------
-    // Lane k of wave w first draws everything random about child w + 16k in
+    // Lane k of wave w draws everything random about child w + 16k in
     // parallel (two Philox blocks, both tournaments, the OX1 cut points, the
-    // mutation): 64 children per wave in one pass instead of 64 serial ones.
-    int v_pa = 0, v_pb = 0, v_lo = 0, v_hi = 0, v_mut = 0, v_mtyp = 0, v_mi = 0, v_mj = 0;
-    int v_out = 0;
-    {
-      const int child = wave + 16 * lane;
-      if (child < P) {
-        v_out = (int)((uint32_t)crow[child] * rs);
+    // mutation): 64 children per wave in one pass instead of 64 serial ones;
+    // the blocks for GB generations at a time (above).
+    if (g % GB == 0) {
+      const int o = lane / cg, child = wave + 16 * (lane % cg);
+      if (child < P && g + o < a.gens) {
+        const uint64_t gg = gen + (uint64_t)o;
         const uint32_t cid = (uint32_t)(island * P + child);
-        const u32x4 r = philox((uint32_t)gen, (uint32_t)(gen >> 32), cid, 0u, a.seed_lo, a.seed_hi);
-        const u32x4 r2 =
-            philox((uint32_t)gen, (uint32_t)(gen >> 32), cid, 1u, a.seed_lo, a.seed_hi);
-        v_pa = (int)((uint32_t)prow[tourney2(pk, P, r.x, r.y)] * rs);
-        v_pb = (int)((uint32_t)prow[tourney2(pk, P, r.z, r.w)] * rs);
+        const u32x4 r = philox((uint32_t)gg, (uint32_t)(gg >> 32), cid, 0u, a.seed_lo, a.seed_hi);
+        const u32x4 r2 = philox((uint32_t)gg, (uint32_t)(gg >> 32), cid, 1u, a.seed_lo, a.seed_hi);
+        b_r0 = r.x;
+        b_r1 = r.y;
+        b_r2 = r.z;
+        b_r3 = r.w;
+        v_mut = 0;
         if (n >= 2) {
           int lo = (int)(r2.x % (uint32_t)n), hi = (int)(r2.y % (uint32_t)n);
           v_lo = lo < hi ? lo : hi;
@@ -228,6 +238,16 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
             v_mj = m.j;
           }
         }
+      }
+    }
+    const int lb = (g % GB) * cg;  // this generation's lanes: lb .. lb + cg - 1
+    int v_pa = 0, v_pb = 0, v_out = 0;
+    {
+      const int k = lane - lb, child = wave + 16 * k;
+      if (k >= 0 && k < cg && child < P) {
+        v_out = (int)((uint32_t)crow[child] * rs);
+        v_pa = (int)((uint32_t)prow[tourney2(pk, P, b_r0, b_r1)] * rs);
+        v_pb = (int)((uint32_t)prow[tourney2(pk, P, b_r2, b_r3)] * rs);
       }
     }
     // Two children of the wave at a time (each with its own stamp array).
@@ -248,12 +268,12 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
       uint32_t stamp[NC], ga[NC][H], gb[NC][H];
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        const uint8_t* A = rows + (uint32_t)wave_bcast(v_pa, k + c);
-        const uint8_t* B = rows + (uint32_t)wave_bcast(v_pb, k + c);
-        out[c] = rows + (uint32_t)wave_bcast(v_out, k + c);
+        const uint8_t* A = rows + (uint32_t)wave_bcast(v_pa, lb + k + c);
+        const uint8_t* B = rows + (uint32_t)wave_bcast(v_pb, lb + k + c);
+        out[c] = rows + (uint32_t)wave_bcast(v_out, lb + k + c);
         m[c] = mk + (uint32_t)((k + c) % VRPMS_GA_NC) * 16u * (uint32_t)a.f.N;
-        lo[c] = wave_bcast(v_lo, k + c);
-        hi[c] = wave_bcast(v_hi, k + c);
+        lo[c] = wave_bcast(v_lo, lb + k + c);
+        hi[c] = wave_bcast(v_hi, lb + k + c);
         stamp[c] = 1u + (uint32_t)((g - gclr) * cpw + k + c);
         filled[c] = 0;
 #pragma unroll
@@ -317,9 +337,9 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
       // the move touches (the wave's reads finish before its writes)
 #pragma unroll
       for (int c = 0; c < NC; ++c)
-        if (wave_bcast(v_mut, k + c) != 0) {
-          const Move mv{(uint32_t)wave_bcast(v_mtyp, k + c), wave_bcast(v_mi, k + c),
-                        wave_bcast(v_mj, k + c)};
+        if (wave_bcast(v_mut, lb + k + c) != 0) {
+          const Move mv{(uint32_t)wave_bcast(v_mtyp, lb + k + c), wave_bcast(v_mi, lb + k + c),
+                        wave_bcast(v_mj, lb + k + c)};
           const MoveMap fm = move_map(mv);
           const int w0 = min(mv.i, mv.j), w1 = max(mv.i, mv.j);
           wave_sync();
@@ -337,8 +357,8 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
     };
     if (n < 2) {
       for (int k = 0; wave + 16 * k < P; ++k) {
-        const uint8_t* A = rows + (uint32_t)wave_bcast(v_pa, k);
-        uint8_t* out = rows + (uint32_t)wave_bcast(v_out, k);
+        const uint8_t* A = rows + (uint32_t)wave_bcast(v_pa, lb + k);
+        uint8_t* out = rows + (uint32_t)wave_bcast(v_out, lb + k);
         for (int q = lane; q < n; q += 64) out[q] = A[q];
       }
     } else {
