@@ -403,8 +403,6 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
     int g_lo = 0, g_hi = S;  // the segments whose routes are (re)written below
     bool inc = false;
     bool empties_kept = false;  // (incremental) no segment became empty or non-empty
-    int ra_ch = 0, rb_ch = 0;   // (incremental, same route count) routes ra_ch .. rb_ch - 1 changed
-    bool same_routes = false;
     if (!HET && tab_ok && !(qa == 0 && qb >= n)) {
       const int ga = (int)T.SC[qa];
       const int gb = qb < n ? min((int)T.SC[qb + 1], S) : S;
@@ -440,9 +438,6 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
           R = Rold + dR;
           g_lo = ga;
           g_hi = gb;
-          same_routes = dR == 0;
-          ra_ch = r0;
-          rb_ch = r0 + (int)tc;
           // LNE1 / FNE (the nearest non-empty segments) change only when one
           // of the re-split segments became empty or non-empty: LNE1[g] == g
           // + 1 says segment g was non-empty before the move
@@ -592,16 +587,10 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
       wave_sync();
     }
     // per-route prefix sums / maxima (dsp / pmx [r] over routes < r), suffix
-    // maxima (smx [r] over routes >= r), sparse table of maxima.  After an
-    // incremental split that kept the route count, only routes ra_ch ..
-    // rb_ch - 1 changed: the prefixes are rescanned from ra_ch, the suffix
-    // maxima down from rb_ch, and each sparse level only over the entries
-    // whose range meets the changed routes (their inputs are either
-    // rescanned or untouched by the move)
-    const int ra = same_routes ? ra_ch : 0, rb = same_routes ? rb_ch : R;
-    uint32_t cds = ra ? T.dsp[ra] : 0u, cmx = ra ? T.pmx[ra] : 0u;
+    // maxima (smx [r] over routes >= r), sparse table of maxima
+    uint32_t cds = 0, cmx = 0;
 #pragma unroll 1
-    for (int base = ra; base < R; base += 64) {
+    for (int base = 0; base < R; base += 64) {
       const int r = base + lane;
       const uint32_t d = r < R ? T.dur[r] : 0u;
       uint32_t ts, tm;
@@ -613,13 +602,13 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
       cds += ts;
       cmx = max(cmx, tm);
     }
-    uint32_t smx = rb < R ? T.smx[rb] : 0u;
+    uint32_t smx = 0;
 #pragma unroll 1
-    for (int top = rb - 63; top > -64; top -= 64) {  // lanes top .. top + 63, downwards
+    for (int top = (R / 64) * 64; top >= 0; top -= 64) {
       const int r = top + lane;
       uint32_t tm;
-      const uint32_t sm = max(dpp_rscan_max(r >= 0 && r < R ? T.dur[r] : 0u, tm), smx);
-      if (r >= 0 && r <= rb) T.smx[r] = sm;
+      const uint32_t sm = max(dpp_rscan_max(r < R ? T.dur[r] : 0u, tm), smx);
+      if (r <= R) T.smx[r] = sm;
       smx = max(smx, tm);
     }
     if (lane == 0) {
@@ -633,9 +622,7 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
       const int w = 1 << (l - 1);
       const uint32_t* src = SPv(l - 1);
       uint32_t* dst = SPv(l);
-      const int j0 = same_routes ? max(0, ra - 2 * w + 1) : 0;
-      const int j1 = same_routes ? rb - 1 : R;
-      for (int r = j0 + lane; r <= j1 && r + 2 * w <= R; r += 64) dst[r] = max(src[r], src[r + w]);
+      for (int r = lane; r + 2 * w <= R; r += 64) dst[r] = max(src[r], src[r + w]);
       wave_sync();
     }
     SEG_PT(11);
