@@ -280,8 +280,10 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
         for (int h = 0; h < H; ++h) {
           // lanes past the tour read its last position (unused)
           const int q = min(lane + 64 * h, n - 1);
-          int src = hi[c] + 1 + q;
-          src = src >= n ? src - n : src;
+          // (hi + 1 + q) mod n with hi, q < n: the smaller of x and x - n
+          // as unsigned (x - n wraps above x exactly when x < n)
+          const uint32_t sx = (uint32_t)(hi[c] + 1 + q);
+          const uint32_t src = min(sx, sx - (uint32_t)n);
           ga[c][h] = (uint32_t)A[q];
           gb[c][h] = (uint32_t)B[src];
         }
@@ -326,8 +328,8 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
           const int slot = filled[c] + (int)__builtin_amdgcn_mbcnt_hi(
                                            (uint32_t)(ball >> 32),
                                            __builtin_amdgcn_mbcnt_lo((uint32_t)ball, 0u));
-          int dst = hi[c] + 1 + slot;
-          dst = dst >= n ? dst - n : dst;
+          const uint32_t dx = (uint32_t)(hi[c] + 1 + slot);  // mod n, as above
+          const uint32_t dst = min(dx, dx - (uint32_t)n);
           // (a kept gene's slot is always < n - (hi - lo + 1): exactly that
           // many of B's genes lie outside A's span, and dst stays in [0, n))
           *(keep ? out[c] + dst : sink) = (uint8_t)gb[c][h];
