@@ -108,9 +108,9 @@ static GaFusedLayout ga_fused_layout(int N, int n, int P) {
   return L;
 }
 
-// Tournament of two: the lower (key, index) wins (as ga_breed_kernel).
-VRPMS_DEV int tourney2(const uint64_t* keys, int pop, uint32_t r0, uint32_t r1) {
-  const int x = (int)(r0 % (uint32_t)pop), y = (int)(r1 % (uint32_t)pop);
+// Tournament of two between members x and y (x = r0 % pop, y = r1 % pop):
+// the lower (key, index) wins (as ga_breed_kernel).
+VRPMS_DEV int tourney2_xy(const uint64_t* keys, int x, int y) {
   const uint64_t kx = keys[x], ky = keys[y];
   return (ky < kx || (ky == kx && y < x)) ? y : x;
 }
@@ -184,7 +184,7 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
   // about the population (the tournaments) is still read each generation.
   const int cg = cpw <= 1 ? 1 : 1 << (32 - __builtin_clz((uint32_t)(cpw - 1)));
   const int GB = 64 / cg;
-  uint32_t b_r0 = 0, b_r1 = 0, b_r2 = 0, b_r3 = 0;  // tournament words (A: r0, r1; B: r2, r3)
+  int b_x0 = 0, b_y0 = 0, b_x1 = 0, b_y1 = 0;  // tournament members (A: x0, y0; B: x1, y1)
   int v_lo = 0, v_hi = 0, v_mut = 0, v_mtyp = 0, v_mi = 0, v_mj = 0;
 
   WordChains<1, CY> ch;
@@ -221,10 +221,10 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
         const uint32_t cid = (uint32_t)(island * P + child);
         const u32x4 r = philox((uint32_t)gg, (uint32_t)(gg >> 32), cid, 0u, a.seed_lo, a.seed_hi);
         const u32x4 r2 = philox((uint32_t)gg, (uint32_t)(gg >> 32), cid, 1u, a.seed_lo, a.seed_hi);
-        b_r0 = r.x;
-        b_r1 = r.y;
-        b_r2 = r.z;
-        b_r3 = r.w;
+        b_x0 = (int)(r.x % (uint32_t)P);
+        b_y0 = (int)(r.y % (uint32_t)P);
+        b_x1 = (int)(r.z % (uint32_t)P);
+        b_y1 = (int)(r.w % (uint32_t)P);
         v_mut = 0;
         if (n >= 2) {
           int lo = (int)(r2.x % (uint32_t)n), hi = (int)(r2.y % (uint32_t)n);
@@ -246,8 +246,8 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
       const int k = lane - lb, child = wave + 16 * k;
       if (k >= 0 && k < cg && child < P) {
         v_out = (int)((uint32_t)crow[child] * rs);
-        v_pa = (int)((uint32_t)prow[tourney2(pk, P, b_r0, b_r1)] * rs);
-        v_pb = (int)((uint32_t)prow[tourney2(pk, P, b_r2, b_r3)] * rs);
+        v_pa = (int)((uint32_t)prow[tourney2_xy(pk, b_x0, b_y0)] * rs);
+        v_pb = (int)((uint32_t)prow[tourney2_xy(pk, b_x1, b_y1)] * rs);
       }
     }
     // Two children of the wave at a time (each with its own stamp array).
@@ -260,6 +260,13 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
     // mutation is applied afterwards, in place, to the children that mutate.
     // (Issuing the next pair's reads before the current pair's writes
     // measured slower: the breed is issue-bound, not read-latency bound.)
+    // lanes holding a position of chunk h (lane + 64 h < n), as a wave mask
+    uint64_t vmask[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const int rem = n - 64 * h;
+      vmask[h] = rem >= 64 ? ~0ull : (rem <= 0 ? 0ull : (1ull << rem) - 1ull);
+    }
     auto breed = [&](auto nc_tag, int k) __attribute__((always_inline)) {
       constexpr int NC = decltype(nc_tag)::value;
       uint8_t* out[NC];
@@ -324,7 +331,10 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
 #pragma unroll
         for (int h = 0; h < H; ++h) {
           const bool keep = (lane + 64 * h < n) & (st[c][h] != (stamp[c] & 0xFFu));
-          const uint64_t ball = __ballot(keep);
+          // the compare's own lane mask (v_cmp to an SGPR pair) instead of
+          // __ballot(keep), which materialises keep in a VGPR and compares again
+          const uint64_t ball =
+              __builtin_amdgcn_uicmp(st[c][h], stamp[c] & 0xFFu, 33 /* ICMP_NE */) & vmask[h];
           const int slot = filled[c] + (int)__builtin_amdgcn_mbcnt_hi(
                                            (uint32_t)(ball >> 32),
                                            __builtin_amdgcn_mbcnt_lo((uint32_t)ball, 0u));
