@@ -165,18 +165,36 @@ VRPMS_DEV bool pair_less(uint64_t ka, uint32_t ia, uint64_t kb, uint32_t ib) {
 // position in its own run plus a lower bound in each other run.  Pairs are
 // unique (the index breaks ties), so sk[0..P) / si[0..P) equal the first P of
 // block_sort_pairs over the 2P pairs.  rk / ri hold the child runs
-// (64 * ceil(P / 64) entries); needs blockDim.x >= 64 * ceil(P / 64).
+// (64 * ceil(P / 64) entries); sk must hold 2P entries (its upper half keeps
+// the children's parent ranks meanwhile); needs blockDim.x >= 64 * ceil(P / 64).
 // With pmap / cmap, si receives pmap[index] for a parent and
 // cmap[index - P] for a child instead of the index (the fused GA's LDS rows
 // of the survivors), and lost[rank - P] the row of each pair ranked P .. 2P - 1
 // (the rows no survivor holds; lost must not alias cmap).  Every thread of the
 // block must call it.
+//
+// Latency, not issue, bounds the rank searches (each a chain of dependent
+// LDS reads): the wavefronts that sort no run search the children's ranks
+// among the parents while the others sort, and a lane's searches in two runs
+// step together, so a pair waits for one 7-step chain instead of up to three.
 VRPMS_DEV void merge_select(const uint64_t* pk, const uint64_t* ck, int P, uint64_t* rk,
                             uint32_t* ri, uint64_t* sk, uint32_t* si,
                             const uint16_t* pmap = nullptr, const uint16_t* cmap = nullptr,
                             uint16_t* lost = nullptr) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int R = (P + 63) >> 6;
+  // lower bound of (k, v) among the parents (8 steps for P = 256)
+  auto parent_rank = [&](uint64_t k, uint32_t v) {
+    int lo = 0, hi = P;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (pair_less(pk[mid], (uint32_t)mid, k, v)) lo = mid + 1;
+      else hi = mid;
+    }
+    return lo;
+  };
+  const int spare = (int)blockDim.x - 64 * R;  // lanes of the waves that sort no run
+  uint32_t* prank = reinterpret_cast<uint32_t*>(sk + P);  // [P] (dead until the writes below)
   if (w < R) {  // wave-uniform
     const int c = (w << 6) | l;
     uint64_t k = c < P ? ck[c] : ~0ull;  // padding sorts last (index > 2P)
@@ -184,14 +202,18 @@ VRPMS_DEV void merge_select(const uint64_t* pk, const uint64_t* ck, int P, uint6
     wave_sort64(k, v);
     rk[c] = k;
     ri[c] = v;
+  } else {
+    for (int c = (int)threadIdx.x - 64 * R; c < P; c += spare)
+      prank[c] = (uint32_t)parent_rank(ck[c], (uint32_t)(P + c));
   }
   __syncthreads();
-  // the lower bounds a pair needs in the other runs (and a child's among the
-  // parents) are independent searches: with 4P <= blockDim.x two lanes share
-  // each pair, lane bit 0 choosing the runs of that parity (the even lane
-  // also takes the parents' search), their counts added by a DPP swap
+  // the lower bounds a pair needs in the other runs are independent
+  // searches: with 4P <= blockDim.x two lanes share each pair, lane bit 0
+  // choosing the runs of that parity (the even lane also adds the child's
+  // parent rank), their counts added by a DPP swap
   const bool two = 4 * P <= (int)blockDim.x;  // block-uniform
   const int step = two ? (int)blockDim.x >> 1 : (int)blockDim.x;
+  const int inc = two ? 2 : 1;
   for (int t = two ? (int)threadIdx.x >> 1 : (int)threadIdx.x; t < 2 * P; t += step) {
     const int half = two ? (int)(threadIdx.x & 1u) : -1;
     const int e = t;
@@ -201,25 +223,27 @@ VRPMS_DEV void merge_select(const uint64_t* pk, const uint64_t* ck, int P, uint6
     const uint64_t k = child ? rk[c] : pk[e];
     const uint32_t v = child ? ri[c] : (uint32_t)e;
     int part = 0;
-    if (child && half <= 0) {
-      int lo = 0, hi = P;  // lower bound among the parents
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (pair_less(pk[mid], (uint32_t)mid, k, v)) lo = mid + 1;
-        else hi = mid;
-      }
-      part += lo;
-    }
-    for (int r = half < 0 ? 0 : half; r < R; r += half < 0 ? 1 : 2) {  // every other run
-      if (r == own) continue;
-      const uint64_t* rkr = rk + (r << 6);
-      const uint32_t* rir = ri + (r << 6);
-      int pos = 0;
+    if (child && half <= 0 && !pad)
+      part += spare > 0 ? (int)prank[v - (uint32_t)P] : parent_rank(k, v);
+    // runs r0, r0 + inc stepped together
+    for (int r0 = half < 0 ? 0 : half; r0 < R; r0 += 2 * inc) {
+      const int r1 = r0 + inc;
+      const bool v0 = r0 != own, v1 = r1 < R && r1 != own;
+      const uint64_t* k0 = rk + (r0 << 6);
+      const uint32_t* i0 = ri + (r0 << 6);
+      const uint64_t* k1 = rk + ((v1 ? r1 : r0) << 6);
+      const uint32_t* i1 = ri + ((v1 ? r1 : r0) << 6);
+      int p0 = 0, p1 = 0;
 #pragma unroll
-      for (int s = 32; s > 0; s >>= 1)
-        if (pair_less(rkr[pos + s - 1], rir[pos + s - 1], k, v)) pos += s;
-      if (pair_less(rkr[pos], rir[pos], k, v)) ++pos;
-      part += pos;
+      for (int s = 32; s > 0; s >>= 1) {
+        const bool a0 = pair_less(k0[p0 + s - 1], i0[p0 + s - 1], k, v);
+        const bool a1 = pair_less(k1[p1 + s - 1], i1[p1 + s - 1], k, v);
+        p0 += a0 ? s : 0;
+        p1 += a1 ? s : 0;
+      }
+      p0 += pair_less(k0[p0], i0[p0], k, v) ? 1 : 0;
+      p1 += pair_less(k1[p1], i1[p1], k, v) ? 1 : 0;
+      part += (v0 ? p0 : 0) + (v1 ? p1 : 0);
     }
     if (two)  // both lanes of the pair active here (the loop bound is per pair)
       part += __builtin_amdgcn_mov_dpp(part, 0xB1, 0xF, 0xF, false);
