@@ -49,17 +49,20 @@ def run():
                               pmut=pmut)
         ga.epoch()
         torch.cuda.synchronize()
-        buf = (ctypes.c_ulonglong * (5 * 4096))()
-        lib.vrpms_debug_ga_prof(buf, 5 * 4096, 1)
+        buf = (ctypes.c_ulonglong * (6 * 4096))()
+        lib.vrpms_debug_ga_prof(buf, 6 * 4096, 1)
         ga.epoch()
         torch.cuda.synchronize()
-        lib.vrpms_debug_ga_prof(buf, 5 * 4096, 1)
+        lib.vrpms_debug_ga_prof(buf, 6 * 4096, 1)
         a = np.array(buf[:4 * islands], dtype=np.float64).reshape(islands, 4) / 20
         redo = np.array(buf[4 * 4096:4 * 4096 + islands], dtype=np.float64) / 20
+        # selection up to the run-sort barrier (sorted-parents generations)
+        sort_a = np.array(buf[5 * 4096:5 * 4096 + islands], dtype=np.uint64).astype(np.float64) / 20
         names = ["breed", "score", "sort", "survivors"]
         print(json.dumps({"islands": islands, "pop": pop, "pmut": pmut,
                           "ticks_per_generation": dict(zip(names, a.mean(0).round(1).tolist())),
                           "us_per_generation": round(a.mean(0).sum() / 100.0, 2),
+                          "sort_to_run_barrier": round(float(sort_a.mean()), 1),
                           "exact_rewalks_per_generation": {"mean": round(redo.mean(), 2),
                                                            "islands_with_any": int((redo > 0).sum())}}),
               flush=True)

@@ -25,6 +25,20 @@
 // crosses HBM between generations.
 #include <hip/hip_runtime.h>
 
+#ifdef VRPMS_GA_PROF
+// phase cycle counters per island (A/B builds only: tools/ga_prof.py)
+// [island][0..3]: phase cycles; [4096 * 4 + island]: children re-walked
+// exactly (met the fleet limit); [4096 * 5 + island]: cycles of the
+// selection up to merge_select's run-sort barrier
+namespace vrpms {
+__device__ unsigned long long g_ga_prof[6 * 4096];
+}
+#define VRPMS_MS_MARK()                                                                \
+  do {                                                                                 \
+    if (threadIdx.x == 0) g_ga_prof[5 * 4096 + blockIdx.x] += wall_clock64();         \
+  } while (0)
+#endif
+
 #include <algorithm>
 #include <type_traits>
 
@@ -43,10 +57,6 @@ namespace vrpms {
 #endif
 
 #ifdef VRPMS_GA_PROF
-// phase cycle counters per island (A/B builds only: tools/ga_prof.py)
-// [island][0..3]: phase cycles; [4096 * 4 + island]: children re-walked
-// exactly (met the fleet limit)
-__device__ unsigned long long g_ga_prof[5 * 4096];
 #define GA_T(k)                                                                        \
   do {                                                                                 \
     __syncthreads();                                                                   \
@@ -455,6 +465,9 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
     // ---- (mu + lambda) survivors by (key, index) -----------------------------
     // si receives the survivors' LDS rows (merge_select maps them)
     if (sorted_parents) {
+#ifdef VRPMS_GA_PROF
+      if (threadIdx.x == 0) g_ga_prof[5 * 4096 + blockIdx.x] -= t_last;
+#endif
       merge_select(pk, ck, P, reinterpret_cast<uint64_t*>(smem + a.off_rk),
                    reinterpret_cast<uint32_t*>(smem + a.off_ri), sk, si, prow, crow, crow_next);
     } else {
@@ -552,7 +565,7 @@ extern "C" int vrpms_debug_ga_prof(unsigned long long* out, int count, int reset
       hipSuccess)
     return -2;
   if (reset) {
-    static unsigned long long zero[5 * 4096];
+    static unsigned long long zero[6 * 4096];
     (void)hipMemcpyToSymbol(HIP_SYMBOL(vrpms::g_ga_prof), zero, sizeof(zero));
   }
   return 0;

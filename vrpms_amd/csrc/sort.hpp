@@ -6,6 +6,13 @@
 
 #include "common.hpp"
 
+// hook of the GA phase profile (ga_fused.hip, -DVRPMS_GA_PROF builds)
+#ifndef VRPMS_MS_MARK
+#define VRPMS_MS_MARK() \
+  do {                  \
+  } while (0)
+#endif
+
 namespace vrpms {
 
 // ---------------------------------------------------------------------------
@@ -132,25 +139,48 @@ VRPMS_DEV uint32_t xor_lanes(uint32_t x, int stride) {
   }
 }
 
-// Bitonic sort of one (key, index) pair per lane across a wavefront
-// (ascending by lane; 21 compare-exchange stages over xor_lanes).  All 64
-// lanes must be active.
+// x from lane (lane ^ (size - 1)): the mirror image inside groups of `size`
+// lanes (a compile-time power of two after unrolling): DPP quad_perm (2, 4),
+// row_half_mirror (8), row_mirror (16), then the 16 / 32 swaps of xor_lanes.
+VRPMS_DEV uint32_t mirror_lanes(uint32_t x, int size) {
+  switch (size) {
+    case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);
+    case 4: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x1B, 0xF, 0xF, true);
+    case 8: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, true);
+    case 16: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, true);
+    case 32: return xor_lanes((uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, true), 16);
+    default:
+      return xor_lanes(
+          xor_lanes((uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, true), 16), 32);
+  }
+}
+
+// Sort of one (key, index) pair per lane across a wavefront (ascending by
+// lane; 21 compare-exchange stages).  The bitonic network in its
+// mirror form: each merge of two sorted halves of `size` lanes first
+// compares lane l with lane l ^ (size - 1), then runs its half-cleaners
+// (l ^ stride), every stage ascending -- so the lane keeping the smaller pair
+// is always the one with the compared bit clear (six fixed masks instead of
+// one direction mask per stage).  All 64 lanes must be active.
 VRPMS_DEV void wave_sort64(uint64_t& k, uint32_t& v) {
-  const int l = threadIdx.x & 63;
+  const uint32_t l = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  auto cx = [&](uint32_t okh, uint32_t okl, uint32_t ov, int bit) __attribute__((always_inline)) {
+    const uint64_t ok = ((uint64_t)okh << 32) | okl;
+    const bool other_less = ok < k || (ok == k && ov < v);
+    const bool low = (l & (uint32_t)bit) == 0;  // keeps the smaller pair
+    if (other_less == low) {
+      k = ok;
+      v = ov;
+    }
+  };
 #pragma unroll
   for (int size = 2; size <= 64; size <<= 1) {
+    cx(mirror_lanes((uint32_t)(k >> 32), size), mirror_lanes((uint32_t)k, size),
+       mirror_lanes(v, size), size >> 1);
 #pragma unroll
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      const uint64_t ok = ((uint64_t)xor_lanes((uint32_t)(k >> 32), stride) << 32) |
-                          xor_lanes((uint32_t)k, stride);
-      const uint32_t ov = xor_lanes(v, stride);
-      const bool lower = (l & stride) == 0, up = (l & size) == 0;
-      const bool other_less = ok < k || (ok == k && ov < v);
-      if (lower == up ? other_less : !other_less) {
-        k = ok;
-        v = ov;
-      }
-    }
+    for (int stride = size >> 2; stride > 0; stride >>= 1)
+      cx(xor_lanes((uint32_t)(k >> 32), stride), xor_lanes((uint32_t)k, stride),
+         xor_lanes(v, stride), stride);
   }
 }
 
@@ -207,6 +237,7 @@ VRPMS_DEV void merge_select(const uint64_t* pk, const uint64_t* ck, int P, uint6
       prank[c] = (uint32_t)parent_rank(ck[c], (uint32_t)(P + c));
   }
   __syncthreads();
+  VRPMS_MS_MARK();
   // the lower bounds a pair needs in the other runs are independent
   // searches: with 4P <= blockDim.x two lanes share each pair, lane bit 0
   // choosing the runs of that parity (the even lane also adds the child's
