@@ -463,8 +463,17 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
     __syncthreads();
     GA_T(1);
     // ---- (mu + lambda) survivors by (key, index) -----------------------------
-    // si receives the survivors' LDS rows (merge_select maps them)
-    if (sorted_parents) {
+    // si receives the survivors' LDS rows (merge_select maps them); with
+    // 4P <= 1024 they are written straight over pk / prow
+    const bool inplace = sorted_parents && 4 * P <= (int)blockDim.x;
+    if (inplace) {
+#ifdef VRPMS_GA_PROF
+      if (threadIdx.x == 0) g_ga_prof[5 * 4096 + blockIdx.x] -= t_last;
+#endif
+      merge_select_inplace(pk, prow, ck, crow, crow_next, P,
+                           reinterpret_cast<uint64_t*>(smem + a.off_rk),
+                           reinterpret_cast<uint32_t*>(smem + a.off_ri), reinterpret_cast<uint32_t*>(sk));
+    } else if (sorted_parents) {
 #ifdef VRPMS_GA_PROF
       if (threadIdx.x == 0) g_ga_prof[5 * 4096 + blockIdx.x] -= t_last;
 #endif
@@ -496,11 +505,13 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
       __syncthreads();
     }
     GA_T(2);
-    for (int i = threadIdx.x; i < P; i += blockDim.x) {
-      prow[i] = (uint16_t)si[i];
-      pk[i] = sk[i];
+    if (!inplace) {
+      for (int i = threadIdx.x; i < P; i += blockDim.x) {
+        prow[i] = (uint16_t)si[i];
+        pk[i] = sk[i];
+      }
+      __syncthreads();
     }
-    __syncthreads();
     {  // the rows the selection dropped take the next children
       uint16_t* t = crow;
       crow = crow_next;

@@ -207,10 +207,17 @@ VRPMS_DEV bool pair_less(uint64_t ka, uint32_t ia, uint64_t kb, uint32_t ib) {
 // LDS reads): the wavefronts that sort no run search the children's ranks
 // among the parents while the others sort, and a lane's searches in two runs
 // step together, so a pair waits for one 7-step chain instead of up to three.
-VRPMS_DEV void merge_select(const uint64_t* pk, const uint64_t* ck, int P, uint64_t* rk,
-                            uint32_t* ri, uint64_t* sk, uint32_t* si,
-                            const uint16_t* pmap = nullptr, const uint16_t* cmap = nullptr,
-                            uint16_t* lost = nullptr) {
+//
+// IN (merge_select_inplace): the survivors are written over the parents
+// (sk aliases pk, orow receives the rows instead of si aliasing pmap); needs
+// 4P <= blockDim.x and a wavefront that sorts no run, so each thread holds at
+// most one pair, reads its parent's key and row before the run-sort barrier,
+// and nothing reads pk / pmap after it.
+template <bool IN>
+VRPMS_DEV void merge_select_impl(const uint64_t* pk, const uint64_t* ck, int P, uint64_t* rk,
+                                 uint32_t* ri, uint64_t* sk, uint32_t* si, const uint16_t* pmap,
+                                 const uint16_t* cmap, uint16_t* lost, uint32_t* prank_in,
+                                 uint16_t* orow) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int R = (P + 63) >> 6;
   // lower bound of (k, v) among the parents (8 steps for P = 256)
@@ -224,7 +231,14 @@ VRPMS_DEV void merge_select(const uint64_t* pk, const uint64_t* ck, int P, uint6
     return lo;
   };
   const int spare = (int)blockDim.x - 64 * R;  // lanes of the waves that sort no run
-  uint32_t* prank = reinterpret_cast<uint32_t*>(sk + P);  // [P] (dead until the writes below)
+  // [P] (dead until the writes below)
+  uint32_t* prank = IN ? prank_in : reinterpret_cast<uint32_t*>(sk + P);
+  uint64_t pkey = 0;  // IN: the parent pair this thread ranks, read before any write
+  uint32_t prow_own = 0;
+  if (IN && ((int)threadIdx.x >> 1) < P) {
+    pkey = pk[threadIdx.x >> 1];
+    prow_own = pmap[threadIdx.x >> 1];
+  }
   if (w < R) {  // wave-uniform
     const int c = (w << 6) | l;
     uint64_t k = c < P ? ck[c] : ~0ull;  // padding sorts last (index > 2P)
@@ -251,7 +265,7 @@ VRPMS_DEV void merge_select(const uint64_t* pk, const uint64_t* ck, int P, uint6
     const bool child = e >= P;
     const int c = e - P, own = child ? c >> 6 : -1;
     const bool pad = child && (c & 63) >= P - (own << 6);  // run padding
-    const uint64_t k = child ? rk[c] : pk[e];
+    const uint64_t k = child ? rk[c] : (IN ? pkey : pk[e]);
     const uint32_t v = child ? ri[c] : (uint32_t)e;
     int part = 0;
     if (child && half <= 0 && !pad)
@@ -280,16 +294,33 @@ VRPMS_DEV void merge_select(const uint64_t* pk, const uint64_t* ck, int P, uint6
       part += __builtin_amdgcn_mov_dpp(part, 0xB1, 0xF, 0xF, false);
     const int rank = part + (child ? (c & 63) : e);
     if (!pad && half <= 0) {
-      const uint32_t row = pmap ? (uint32_t)(child ? cmap[v - P] : pmap[v]) : v;
+      const uint32_t row =
+          pmap ? (uint32_t)(child ? cmap[v - P] : (IN ? prow_own : pmap[v])) : v;
       if (rank < P) {
         sk[rank] = k;
-        si[rank] = row;
+        if (IN) orow[rank] = (uint16_t)row;
+        else si[rank] = row;
       } else if (lost) {
         lost[rank - P] = (uint16_t)row;
       }
     }
   }
   __syncthreads();
+}
+
+VRPMS_DEV void merge_select(const uint64_t* pk, const uint64_t* ck, int P, uint64_t* rk,
+                            uint32_t* ri, uint64_t* sk, uint32_t* si,
+                            const uint16_t* pmap = nullptr, const uint16_t* cmap = nullptr,
+                            uint16_t* lost = nullptr) {
+  merge_select_impl<false>(pk, ck, P, rk, ri, sk, si, pmap, cmap, lost, nullptr, nullptr);
+}
+
+// pk / prow <- the survivors' keys and rows (see IN above); prank: P scratch
+// words.  Every thread of the block must call it.
+VRPMS_DEV void merge_select_inplace(uint64_t* pk, uint16_t* prow, const uint64_t* ck,
+                                    const uint16_t* crow, uint16_t* lost, int P, uint64_t* rk,
+                                    uint32_t* ri, uint32_t* prank) {
+  merge_select_impl<true>(pk, ck, P, rk, ri, pk, nullptr, prow, crow, lost, prank, prow);
 }
 
 }  // namespace vrpms
