@@ -617,34 +617,13 @@ __global__ __launch_bounds__(64 * kSegMaxWaves, OCC) void sa_seg_kernel(SegArgs 
     }
     wave_sync();
     SEG_PT(10);
-    if (R <= 128) {
-      // the levels in registers (routes lane and lane + 64), the partner
-      // entry r + w by ds_bpermute: one cross-lane round trip per level
-      // instead of a store and a wave-wide wait; levels past R hold no entry
-      uint32_t v0 = lane < R ? T.dur[lane] : 0u, v1 = lane + 64 < R ? T.dur[lane + 64] : 0u;
 #pragma unroll 1
-      for (int l = 1; l < LV && (1 << l) <= R; ++l) {
-        const int w = 1 << (l - 1);
-        const int src = (lane + w) & 63;
-        const uint32_t a0 = (uint32_t)__shfl((int)v0, src, 64);
-        const uint32_t a1 = (uint32_t)__shfl((int)v1, src, 64);
-        // entry lane + 64 is stored only when lane + w < 64 (lane + 64 + 2w <= R <= 128)
-        v0 = max(v0, lane + w < 64 ? a0 : a1);
-        v1 = max(v1, a1);
-        uint32_t* dst = SPv(l);
-        if (lane + 2 * w <= R) dst[lane] = v0;
-        if (lane + 64 + 2 * w <= R) dst[lane + 64] = v1;
-      }
+    for (int l = 1; l < LV; ++l) {
+      const int w = 1 << (l - 1);
+      const uint32_t* src = SPv(l - 1);
+      uint32_t* dst = SPv(l);
+      for (int r = lane; r + 2 * w <= R; r += 64) dst[r] = max(src[r], src[r + w]);
       wave_sync();
-    } else {
-#pragma unroll 1
-      for (int l = 1; l < LV; ++l) {
-        const int w = 1 << (l - 1);
-        const uint32_t* src = SPv(l - 1);
-        uint32_t* dst = SPv(l);
-        for (int r = lane; r + 2 * w <= R; r += 64) dst[r] = max(src[r], src[r + w]);
-        wave_sync();
-      }
     }
     SEG_PT(11);
     rb_valid = true;
