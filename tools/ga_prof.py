@@ -58,11 +58,20 @@ def run():
         redo = np.array(buf[4 * 4096:4 * 4096 + islands], dtype=np.float64) / 20
         # selection up to the run-sort barrier (sorted-parents generations)
         sort_a = np.array(buf[5 * 4096:5 * 4096 + islands], dtype=np.uint64).astype(np.float64) / 20
+        # whole calls (prologue + 20 generations + epilogue) by HIP events
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            ga.epoch()
+        e1.record()
+        torch.cuda.synchronize()
+        call_us = e0.elapsed_time(e1) * 1e3 / 5
         names = ["breed", "score", "sort", "survivors"]
         print(json.dumps({"islands": islands, "pop": pop, "pmut": pmut,
                           "ticks_per_generation": dict(zip(names, a.mean(0).round(1).tolist())),
                           "us_per_generation": round(a.mean(0).sum() / 100.0, 2),
                           "sort_to_run_barrier": round(float(sort_a.mean()), 1),
+                          "call_us_per_generation": round(call_us / 20, 2),
                           "exact_rewalks_per_generation": {"mean": round(redo.mean(), 2),
                                                            "islands_with_any": int((redo > 0).sum())}}),
               flush=True)

@@ -161,10 +161,9 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
   for (uint32_t i = threadIdx.x; i < (uint32_t)P * rs / 2; i += blockDim.x)
     reinterpret_cast<uint32_t*>(rows)[i] = 0u;
   stage_table(a.f.pack, a.f.N, smem);  // ends with a barrier
-  for (int64_t e = threadIdx.x; e < (int64_t)P * n; e += blockDim.x) {
-    const int i = (int)(e / n), q = (int)(e % n);
-    rows[(uint32_t)i * rs + q] = (uint8_t)gpop[e];
-  }
+  // a wavefront per row (no 64-bit division per element)
+  for (int i = wave; i < P; i += (int)(blockDim.x >> 6))
+    for (int q = lane; q < n; q += 64) rows[(uint32_t)i * rs + q] = (uint8_t)gpop[(int64_t)i * n + q];
   for (int i = threadIdx.x; i < P; i += blockDim.x) {
     prow[i] = (uint16_t)i;
     crow[i] = (uint16_t)(P + i);
@@ -519,9 +518,9 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
     }
     GA_T(3);
   }
-  for (int64_t e = threadIdx.x; e < (int64_t)P * n; e += blockDim.x) {
-    const int i = (int)(e / n), q = (int)(e % n);
-    gpop[e] = rows[(uint32_t)prow[i] * rs + q];
+  for (int i = wave; i < P; i += (int)(blockDim.x >> 6)) {
+    const uint32_t src = (uint32_t)prow[i] * rs;
+    for (int q = lane; q < n; q += 64) gpop[(int64_t)i * n + q] = rows[src + q];
   }
   for (int i = threadIdx.x; i < P; i += blockDim.x) gkeys[i] = pk[i];
 }
