@@ -250,13 +250,15 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
       }
     }
     const int lb = (g % GB) * cg;  // this generation's lanes: lb .. lb + cg - 1
-    int v_pa = 0, v_pb = 0, v_out = 0;
+    // per child two broadcast words instead of five: the parents' LDS rows
+    // (11 bits each) and the child's row with the OX1 cut points (n <= 255)
+    int v_ab = 0, v_olh = 0;
     {
       const int k = lane - lb, child = wave + 16 * k;
       if (k >= 0 && k < cg && child < P) {
-        v_out = (int)((uint32_t)crow[child] * rs);
-        v_pa = (int)((uint32_t)prow[tourney2_xy(pk, b_x0, b_y0)] * rs);
-        v_pb = (int)((uint32_t)prow[tourney2_xy(pk, b_x1, b_y1)] * rs);
+        v_olh = (int)((uint32_t)crow[child] | ((uint32_t)v_lo << 11) | ((uint32_t)v_hi << 19));
+        v_ab = (int)((uint32_t)prow[tourney2_xy(pk, b_x0, b_y0)] |
+                     ((uint32_t)prow[tourney2_xy(pk, b_x1, b_y1)] << 11));
       }
     }
     // Two children of the wave at a time (each with its own stamp array).
@@ -284,12 +286,14 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
       uint32_t stamp[NC], ga[NC][H], gb[NC][H];
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        const uint8_t* A = rows + (uint32_t)wave_bcast(v_pa, lb + k + c);
-        const uint8_t* B = rows + (uint32_t)wave_bcast(v_pb, lb + k + c);
-        out[c] = rows + (uint32_t)wave_bcast(v_out, lb + k + c);
+        const uint32_t ab = (uint32_t)wave_bcast(v_ab, lb + k + c);
+        const uint32_t olh = (uint32_t)wave_bcast(v_olh, lb + k + c);
+        const uint8_t* A = rows + (ab & 0x7FFu) * rs;
+        const uint8_t* B = rows + (ab >> 11) * rs;
+        out[c] = rows + (olh & 0x7FFu) * rs;
         m[c] = mk + (uint32_t)((k + c) % VRPMS_GA_NC) * 16u * (uint32_t)a.f.N;
-        lo[c] = wave_bcast(v_lo, lb + k + c);
-        hi[c] = wave_bcast(v_hi, lb + k + c);
+        lo[c] = (int)((olh >> 11) & 0xFFu);
+        hi[c] = (int)(olh >> 19);
         stamp[c] = 1u + (uint32_t)((g - gclr) * cpw + k + c);
         filled[c] = 0;
 #pragma unroll
@@ -378,8 +382,8 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
     };
     if (n < 2) {
       for (int k = 0; wave + 16 * k < P; ++k) {
-        const uint8_t* A = rows + (uint32_t)wave_bcast(v_pa, lb + k);
-        uint8_t* out = rows + (uint32_t)wave_bcast(v_out, lb + k);
+        const uint8_t* A = rows + ((uint32_t)wave_bcast(v_ab, lb + k) & 0x7FFu) * rs;
+        uint8_t* out = rows + ((uint32_t)wave_bcast(v_olh, lb + k) & 0x7FFu) * rs;
         for (int q = lane; q < n; q += 64) out[q] = A[q];
       }
     } else {
