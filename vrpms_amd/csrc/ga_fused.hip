@@ -194,7 +194,8 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
   const int cg = cpw <= 1 ? 1 : 1 << (32 - __builtin_clz((uint32_t)(cpw - 1)));
   const int GB = 64 / cg;
   int b_x0 = 0, b_y0 = 0, b_x1 = 0, b_y1 = 0;  // tournament members (A: x0, y0; B: x1, y1)
-  int v_lo = 0, v_hi = 0, v_mut = 0, v_mtyp = 0, v_mi = 0, v_mj = 0;
+  int v_lo = 0, v_hi = 0, v_mut = 0;
+  int v_mv = 0;  // the mutation: type | i << 2 | j << 10 (n <= 255)
 
   WordChains<1, CY> ch;
   ch.setup(a.f, smem);
@@ -242,9 +243,7 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
           v_mut = r2.z < a.pmut ? 1 : 0;
           if (v_mut) {
             const Move m = decode_move(r2.w, r.x ^ r2.x, r.y ^ r2.y, n);
-            v_mtyp = (int)m.typ;
-            v_mi = m.i;
-            v_mj = m.j;
+            v_mv = (int)(m.typ | ((uint32_t)m.i << 2) | ((uint32_t)m.j << 10));
           }
         }
       }
@@ -252,11 +251,13 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
     const int lb = (g % GB) * cg;  // this generation's lanes: lb .. lb + cg - 1
     // per child two broadcast words instead of five: the parents' LDS rows
     // (11 bits each) and the child's row with the OX1 cut points (n <= 255)
+    // and the mutation flag (bit 27)
     int v_ab = 0, v_olh = 0;
     {
       const int k = lane - lb, child = wave + 16 * k;
       if (k >= 0 && k < cg && child < P) {
-        v_olh = (int)((uint32_t)crow[child] | ((uint32_t)v_lo << 11) | ((uint32_t)v_hi << 19));
+        v_olh = (int)((uint32_t)crow[child] | ((uint32_t)v_lo << 11) | ((uint32_t)v_hi << 19) |
+                      ((uint32_t)v_mut << 27));
         v_ab = (int)((uint32_t)prow[tourney2_xy(pk, b_x0, b_y0)] |
                      ((uint32_t)prow[tourney2_xy(pk, b_x1, b_y1)] << 11));
       }
@@ -283,17 +284,19 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
       uint8_t* out[NC];
       uint8_t* m[NC];
       int lo[NC], hi[NC], filled[NC];
+      uint32_t mut[NC];
       uint32_t stamp[NC], ga[NC][H], gb[NC][H];
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         const uint32_t ab = (uint32_t)wave_bcast(v_ab, lb + k + c);
         const uint32_t olh = (uint32_t)wave_bcast(v_olh, lb + k + c);
+        mut[c] = (olh >> 27) & 1u;
         const uint8_t* A = rows + (ab & 0x7FFu) * rs;
         const uint8_t* B = rows + (ab >> 11) * rs;
         out[c] = rows + (olh & 0x7FFu) * rs;
         m[c] = mk + (uint32_t)((k + c) % VRPMS_GA_NC) * 16u * (uint32_t)a.f.N;
         lo[c] = (int)((olh >> 11) & 0xFFu);
-        hi[c] = (int)(olh >> 19);
+        hi[c] = (int)((olh >> 19) & 0xFFu);
         stamp[c] = 1u + (uint32_t)((g - gclr) * cpw + k + c);
         filled[c] = 0;
 #pragma unroll
@@ -362,9 +365,9 @@ __global__ __launch_bounds__(1024) void ga_fused_kernel(GaFusedArgs a) {
       // the move touches (the wave's reads finish before its writes)
 #pragma unroll
       for (int c = 0; c < NC; ++c)
-        if (wave_bcast(v_mut, lb + k + c) != 0) {
-          const Move mv{(uint32_t)wave_bcast(v_mtyp, lb + k + c), wave_bcast(v_mi, lb + k + c),
-                        wave_bcast(v_mj, lb + k + c)};
+        if (mut[c] != 0) {
+          const uint32_t w = (uint32_t)wave_bcast(v_mv, lb + k + c);
+          const Move mv{w & 3u, (int)((w >> 2) & 0xFFu), (int)(w >> 10)};
           const MoveMap fm = move_map(mv);
           const int w0 = min(mv.i, mv.j), w1 = max(mv.i, mv.j);
           wave_sync();
